@@ -1,0 +1,48 @@
+# vccl-mi355x build: hand-written HIP for gfx950 + host C++ into one C-ABI
+# shared library (vccl_amd/lib/libvccl.so), plus the CPU oracle (test-only).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CXXFLAGS := -std=c++20 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+            --offload-arch=$(ARCH) -I include
+OBJ := build/obj
+LIB := vccl_amd/lib/libvccl.so
+DEV := vccl_amd/csrc/device
+HOST := vccl_amd/csrc/host
+KTS := 0 1 2 3 4 5 6
+HDRS := $(wildcard $(DEV)/*.hpp) $(wildcard $(HOST)/*.h) $(wildcard include/*.h)
+
+RC_OBJS := $(foreach k,$(KTS),$(OBJ)/rc_kernels_$(k).o)
+RING_OBJS := $(foreach k,$(KTS),$(OBJ)/ring_kernels_$(k).o)
+API_OBJS := $(OBJ)/rc_api.o
+HOST_OBJS := $(patsubst $(HOST)/%.cc,$(OBJ)/host_%.o,$(wildcard $(HOST)/*.cc))
+
+all: $(LIB) oracle
+
+$(LIB): $(RC_OBJS) $(RING_OBJS) $(API_OBJS) $(HOST_OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lpthread
+
+$(OBJ)/rc_kernels_%.o: $(DEV)/rc_kernels.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -DVCCL_KT=$* -c $< -o $@
+
+$(OBJ)/ring_kernels_%.o: $(DEV)/ring_kernels.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -DVCCL_KT=$* -c $< -o $@
+
+$(OBJ)/rc_api.o: $(DEV)/rc_api.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(OBJ)/host_%.o: $(HOST)/%.cc $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -x hip --offload-host-only -c $< -o $@
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Benchmark of the bucket-reduction hot path (BASELINE.json metric).
+
+N = 1 (default): BASELINE config 2 — 2-input fp32 sum reduce-copy, 256 MiB
+  device-resident buffers, through the C ABI (vcclReduceCopy).  One step = one
+  launch over the whole bucket; value = algorithmic GB/s = 3 * 2^28 B per step
+  / time.  Adds `roofline` (per-launch HIP-event duration vs 8 TB/s HBM3E) and
+  `cpu_baseline` (the oracle's C restatement on the host cores, bounded sample).
+N > 1 (torch.distributed.run, one process per GPU): BASELINE config 3 at a
+  fixed bucket — ring all-reduce fp32 sum through ncclAllReduce (the repo's
+  own ring over xGMI peer memory; no RCCL).  value = aggregate bus bandwidth
+  = sum over ranks of busbw, busbw = (S/t) * 2(n-1)/n (nccl-tests convention).
+  torch.distributed (gloo, CPU tensors) only ships the unique id, barriers and
+  the max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--bytes S]
+       [--workload reduce_copy|allreduce|rs_ag] [--sweep]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from vccl_amd import nccl  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.6 / 2    # per link per direction (spec 153.6 GB/s bidirectional)
+
+
+def _evt():
+    return torch.cuda.Event(enable_timing=True)
+
+
+def bench_reduce_copy(args):
+    n = (args.bytes or (256 << 20)) // 4
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    g1 = torch.Generator(device="cuda").manual_seed(1)
+    g2 = torch.Generator(device="cuda").manual_seed(2)
+    a = torch.rand(n, device="cuda", generator=g1) * 2 - 1
+    b = torch.rand(n, device="cuda", generator=g2) * 2 - 1
+    d = torch.empty_like(a)
+    cfg = None
+    if args.block or args.unroll or args.grid or args.nt_loads or args.nt_stores:
+        cfg = {"blockSize": args.block, "unroll": args.unroll, "gridBlocks": args.grid,
+               "ntLoads": args.nt_loads, "ntStores": args.nt_stores}
+    srcs, dsts = [a.data_ptr(), b.data_ptr()], [d.data_ptr()]
+
+    def step():
+        nccl.reduce_copy(0, nccl.ncclFloat32, 0, srcs, dsts, n, sp, config=cfg)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness guard on the measured buffers (bit-exact f32 add)
+    assert torch.equal(d.view(torch.int32), (a + b).view(torch.int32)), "reduce-copy mismatch"
+    torch.cuda.synchronize()
+    starts = [_evt() for _ in range(args.steps)]
+    ends = [_evt() for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    bytes_per = 3 * n * 4
+    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    achieved = bytes_per / avg_kern_s / 1e9
+    value = bytes_per * args.steps / wall / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("reduce_copy", bytes_per),
+            "kernel": "k_reduce_copy<FnSum<float>,2,1>", "algorithmic_bytes_per_launch": bytes_per,
+            "avg_launch_us": round(avg_kern_s * 1e6, 2), "min_launch_us": round(min(kern_ms) * 1e3, 2)}
+    out = {"metric": "device reduce-copy GB/s vs HBM peak; all-reduce busbw at 1/2/4/8 GPUs",
+           "value": round(value, 1), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic uniform[-1,1) seeds 1,2 (device-resident)",
+           "config": {"workload": "reduce_copy 2-src fp32 sum, 256 MiB buffers (BASELINE config 2)",
+                      "bytes_per_buffer": n * 4, "n_srcs": 2, "n_dsts": 1,
+                      "launch": cfg or "library default"},
+           "roofline": roof}
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(n)
+    return out
+
+
+def _pmc_traffic(workload, algo_bytes):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py),
+    or None when no summary for this workload exists."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        rec = d.get(workload)
+        if rec and rec.get("algorithmic_bytes_per_launch") == algo_bytes:
+            return rec["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(n_full):
+    """Oracle restatement (oracle/reduce_ref.c, -O3) on the host cores: the
+    same 2-src f32 sum shape, bounded to ~10 s of CPU work."""
+    from oracle import oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    n = min(n_full, 1 << 24)  # 64 MiB per buffer sample
+    rng = np.random.default_rng(1)
+    a = rng.uniform(-1, 1, n).astype(np.float32)
+    b = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
+    d = [np.empty_like(a)]
+    O.reduce_copy(0, 7, 0, [a, b], out=d, nthreads=threads)  # warm / page in
+    assert np.array_equal(d[0], a + b)
+    iters, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 10.0:
+        O.reduce_copy(0, 7, 0, [a, b], out=d, nthreads=threads)
+        iters += 1
+    dt = time.perf_counter() - t0
+    gbs = 3 * n * 4 * iters / dt / 1e9
+    return {"value": round(gbs, 2), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{iters} x 2-src f32 sum over {n} elems (3 x {n*4 >> 20} MiB host buffers), "
+                      f"{dt:.1f} s, oracle/reduce_ref.c {threads} pthreads"}
+
+
+def _dist_setup():
+    import torch.distributed as dist
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    comm = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank)
+    return dist, rank, world, comm
+
+
+def _time_coll(dist, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dist.barrier()
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_allreduce(args):
+    dist, rank, world, comm = _dist_setup()
+    sp = torch.cuda.current_stream().cuda_stream
+    sizes = [1 << p for p in range(3, 31)] if args.sweep else [args.bytes or (1 << 30)]
+    rows = []
+    for S in sizes:
+        n = max(1, S // 4)
+        g = torch.Generator(device="cuda").manual_seed(1000 + rank)
+        x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+        y = torch.empty_like(x)
+        steps = args.steps if S >= (64 << 20) else max(args.steps, 20)
+
+        def fn():
+            comm.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+        dt = _time_coll(dist, fn, steps, args.warmup)
+        algbw = n * 4 * steps / dt / 1e9
+        busbw = algbw * 2 * (world - 1) / world
+        rows.append({"bytes": n * 4, "us": dt / steps * 1e6, "algbw": algbw, "busbw": busbw})
+        if rank == 0 and args.sweep:
+            print(f"# allreduce {n*4:>12d} B  {dt/steps*1e6:10.1f} us  algbw {algbw:8.2f}  "
+                  f"busbw {busbw:8.2f} GB/s", file=sys.stderr, flush=True)
+    err = comm.async_error()
+    comm.destroy()
+    last = rows[-1]
+    links = {2: 1, 4: 3, 8: 7}.get(world, 1)
+    peak = links * XGMI_LINK_GBS
+    out = {"metric": "device reduce-copy GB/s vs HBM peak; all-reduce busbw at 1/2/4/8 GPUs",
+           "value": round(last["busbw"] * world, 2), "unit": "GB/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(last["us"] / 1e3, 4),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic uniform[-1,1) seed 1000+rank (device-resident)",
+           "config": {"workload": f"ring all-reduce fp32 sum, {last['bytes']} B per rank "
+                                  "(BASELINE config 3), value = aggregate busbw over ranks",
+                      "bytes_per_rank": last["bytes"], "busbw_per_rank": round(last["busbw"], 2),
+                      "algbw": round(last["algbw"], 2), "parallelism": f"ring x{world}",
+                      "async_error": err},
+           "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": peak,
+                        "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
+                        "note": f"per-rank busbw vs {links} links x {XGMI_LINK_GBS} GB/s/direction (spec)"}}
+    if args.sweep:
+        out["sweep"] = [{k: round(v, 3) if isinstance(v, float) else v for k, v in r.items()} for r in rows]
+    dist.destroy_process_group()
+    return out if rank == 0 else None
+
+
+def bench_rs_ag(args):
+    """BASELINE config 4: reduce-scatter + all-gather bf16 bucket."""
+    dist, rank, world, comm = _dist_setup()
+    sp = torch.cuda.current_stream().cuda_stream
+    S = args.bytes or (4 << 30)
+    n = S // 2
+    rc = n // world
+    g = torch.Generator(device="cuda").manual_seed(2000 + rank)
+    x = (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    shard = torch.empty(rc, dtype=torch.bfloat16, device="cuda")
+    y = torch.empty_like(x)
+
+    def rs():
+        comm.reduce_scatter(x.data_ptr(), shard.data_ptr(), rc, nccl.ncclBfloat16, nccl.ncclSum, sp)
+
+    def ag():
+        comm.all_gather(shard.data_ptr(), y.data_ptr(), rc, nccl.ncclBfloat16, sp)
+    t_rs = _time_coll(dist, rs, args.steps, args.warmup)
+    t_ag = _time_coll(dist, ag, args.steps, args.warmup)
+    frac = (world - 1) / world
+    bw_rs = S * args.steps / t_rs / 1e9 * frac
+    bw_ag = S * args.steps / t_ag / 1e9 * frac
+    comm.destroy()
+    dist.destroy_process_group()
+    if rank:
+        return None
+    return {"metric": "reduce-scatter + all-gather busbw (BASELINE config 4)",
+            "value": round((bw_rs + bw_ag) / 2 * world, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round((t_rs + t_ag) / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"RS+AG bf16 {S} B bucket", "rs_busbw": round(bw_rs, 2),
+                       "ag_busbw": round(bw_ag, 2)}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--bytes", type=int, default=0)
+    ap.add_argument("--workload", default="")
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--nt-loads", type=int, default=0)
+    ap.add_argument("--nt-stores", type=int, default=0)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    workload = args.workload or ("reduce_copy" if world == 1 else "allreduce")
+    if workload == "reduce_copy":
+        out = bench_reduce_copy(args)
+    elif workload == "allreduce":
+        out = bench_allreduce(args)
+    else:
+        out = bench_rs_ag(args)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,130 @@
+"""ORACLE — test infrastructure only.
+
+ctypes + numpy wrapper over ``oracle/build/liboracle.so`` (the C restatement of
+VCCL's reduction semantics, see ``reduce_ref.h``).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module; the product path (``vccl_amd``) never does.
+
+Parity status: dispatch table pinned by the reference's ``generate.py``; the
+arithmetic is pinned against numpy/torch IEEE implementations only (CUDA's
+fp16/bf16 intrinsic headers are not in /root/reference) — see DESIGN.md.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+
+# ncclDataType_t (nccl.h.in:239-252) -> numpy storage dtype
+NP_DTYPE = {
+    0: np.int8, 1: np.uint8, 2: np.int32, 3: np.uint32, 4: np.int64, 5: np.uint64,
+    6: np.float16, 7: np.float32, 8: np.float64, 9: np.uint16,  # bf16 stored as raw bits
+}
+TYPE_NAMES = {0: "i8", 1: "u8", 2: "i32", 3: "u32", 4: "i64", 5: "u64",
+              6: "f16", 7: "f32", 8: "f64", 9: "bf16"}
+OP_NAMES = {0: "sum", 1: "prod", 2: "max", 3: "min", 4: "avg"}
+DEV_SUM, DEV_PROD, DEV_MINMAX, DEV_PREMULSUM, DEV_SUMPOSTDIV = range(5)
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u64, i32, vp = ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
+        L.ref_host_to_dev_redop.argtypes = [i32, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(u64)]
+        L.ref_reduce_copy.argtypes = [i32, i32, u64, ctypes.POINTER(u64), i32, i32, i32,
+                                      ctypes.POINTER(vp), i32, ctypes.POINTER(vp), ctypes.c_size_t, i32]
+        L.ref_ring_fold.argtypes = [i32, i32, u64, i32, i32, ctypes.POINTER(vp),
+                                    vp, vp, ctypes.c_size_t]
+        L.ref_chain_fold.argtypes = [i32, i32, u64, i32, i32, ctypes.POINTER(vp), vp, ctypes.c_size_t]
+        L.ref_f32_to_f16.restype = ctypes.c_uint16
+        L.ref_f32_to_f16.argtypes = [ctypes.c_float]
+        L.ref_f32_to_bf16.restype = ctypes.c_uint16
+        L.ref_f32_to_bf16.argtypes = [ctypes.c_float]
+        _lib = L
+    return _lib
+
+
+def host_to_dev_redop(op: int, dtype: int, nranks: int) -> tuple[int, int]:
+    d, a = ctypes.c_int(), ctypes.c_uint64()
+    rc = lib().ref_host_to_dev_redop(op, dtype, nranks, ctypes.byref(d), ctypes.byref(a))
+    if rc != 0:
+        raise ValueError(f"invalid op/type {op}/{dtype}")
+    return d.value, a.value
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def reduce_copy(dev_op, dtype, red_arg, srcs, n_dsts=1, pre_op_args=(), post_op=False,
+                nthreads=1, out=None):
+    """dst = postOp(preOp(src0) (+) preOp(src1) (+) ...) elementwise."""
+    srcs = [np.ascontiguousarray(s) for s in srcs]
+    n = srcs[0].size
+    if out is None:
+        out = [np.empty_like(srcs[0]) for _ in range(n_dsts)]
+    pre = (ctypes.c_uint64 * max(1, len(pre_op_args)))(*pre_op_args) if pre_op_args else None
+    lib().ref_reduce_copy(dev_op, dtype, red_arg, pre, len(pre_op_args), int(post_op),
+                          len(srcs), _ptrs(srcs), len(out), _ptrs(out), n, nthreads)
+    return out
+
+
+def ring_fold(dev_op, dtype, red_arg, pre_op, inputs_ring_order, owner):
+    inputs = [np.ascontiguousarray(x) for x in inputs_ring_order]
+    owner = np.ascontiguousarray(owner, dtype=np.int32)
+    out = np.empty_like(inputs[0])
+    lib().ref_ring_fold(dev_op, dtype, red_arg, int(pre_op), len(inputs), _ptrs(inputs),
+                        owner.ctypes.data, out.ctypes.data, out.size)
+    return out
+
+
+def chain_fold(dev_op, dtype, red_arg, pre_op, inputs_chain_order):
+    inputs = [np.ascontiguousarray(x) for x in inputs_chain_order]
+    out = np.empty_like(inputs[0])
+    lib().ref_chain_fold(dev_op, dtype, red_arg, int(pre_op), len(inputs), _ptrs(inputs),
+                         out.ctypes.data, out.size)
+    return out
+
+
+def allreduce(op, dtype, inputs, owner_fn=None):
+    """Full API-level all-reduce semantics: hostToDevRedOp + ring fold.
+
+    ``inputs`` are per-rank arrays indexed by rank; ``owner_fn(n_elems)`` gives
+    for each element the ring index that finishes it (ring = identity order
+    unless the caller permutes ``inputs``)."""
+    n = len(inputs)
+    dev_op, arg = host_to_dev_redop(op, dtype, n)
+    owner = owner_fn(inputs[0].size) if owner_fn else np.zeros(inputs[0].size, np.int32)
+    if n == 1:  # ncclLaunchOneRank (onerank.cu:47-83): copy, or PreMulSum kernel
+        x = inputs[0]
+        if dev_op == DEV_PREMULSUM:
+            return reduce_copy(dev_op, dtype, arg, [x], pre_op_args=[arg], post_op=True)[0]
+        return x.copy()
+    return ring_fold(dev_op, dtype, arg, dev_op == DEV_PREMULSUM, inputs, owner)
+
+
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """Vectorised RN-even f32 -> bf16 bits (NaN kept NaN), matches ref_f32_to_bf16."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    r[nan] = ((u[nan] >> 16) | 0x40).astype(np.uint16)
+    return r
+
+
+def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
+    return (np.ascontiguousarray(b, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)

@@ -1,0 +1,64 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol declared in
+include/*.h (plus the pnccl* aliases), and its host-only entry points behave.
+No GPU call is made."""
+import ctypes
+import os
+import re
+
+from oracle import oracle as O
+from vccl_amd import nccl
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in ("nccl.h", "vccl_device.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        names |= set(re.findall(r"^\s*(?:ncclResult_t|const char\*|int)\s+(p?(?:nccl|vccl)[A-Z]\w*)\s*\(",
+                                text, flags=re.M))
+    return names
+
+
+def test_every_declared_symbol_exported():
+    L = nccl.lib()
+    declared = _declared()
+    assert "ncclAllReduce" in declared and "pncclReduceScatter" in declared
+    assert "vcclReduceCopy" in declared
+    missing = [n for n in declared if not hasattr(L, n)]
+    assert not missing, missing
+    for n in nccl.EXPORTED:
+        assert n in declared, n
+
+
+def test_version_and_errors():
+    assert nccl.get_version() == 22662  # NCCL_VERSION(2,26,62)
+    L = nccl.lib()
+    for code in range(8):
+        assert L.ncclGetErrorString(code)
+    L.pncclGetErrorString.restype = ctypes.c_char_p
+    assert L.pncclGetErrorString(4) == L.ncclGetErrorString(4)
+
+
+def test_host_to_dev_redop_matches_oracle():
+    for op in range(5):
+        for t in range(10):
+            for n in (1, 2, 3, 8):
+                assert nccl.host_to_dev_redop(op, t, n) == O.host_to_dev_redop(op, t, n), (op, t, n)
+    assert nccl.lib().vcclHostToDevRedOp(0, 12, 1, ctypes.byref(ctypes.c_int()),
+                                         ctypes.byref(ctypes.c_uint64())) == nccl.ncclInvalidArgument
+
+
+def test_unique_id_is_fresh():
+    a = nccl.unique_id_to_bytes(nccl.get_unique_id())
+    b = nccl.unique_id_to_bytes(nccl.get_unique_id())
+    assert len(a) == 128 and a != b
+    assert nccl.unique_id_to_bytes(nccl.unique_id_from_bytes(a)) == a
+
+
+def test_null_comm_queries():
+    L = nccl.lib()
+    v = ctypes.c_int()
+    assert L.ncclCommCount(None, ctypes.byref(v)) == nccl.ncclInvalidArgument
+    assert L.ncclCommDestroy(None) == nccl.ncclSuccess
+    assert L.ncclAllReduce(None, None, 1, 7, 0, None, None) == nccl.ncclInvalidArgument

@@ -1,0 +1,132 @@
+"""NCCL C API on one rank (BASELINE config 1) and API-level error behaviour.
+
+Reference paths: ncclEnqueueCheck (enqueue.cc:2448-2525), ArgsCheck
+(misc/argcheck.cc:45-86), nRanks==1 -> ncclLaunchOneRank (onerank.cu:47-83),
+ncclRedOpCreatePreMulSum (enqueue.cc:2528-2567).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from tests.gpu_util import stream_ptr  # noqa: E402
+from vccl_amd import nccl  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def comm1():
+    uid = nccl.get_unique_id()
+    c = nccl.Comm.init_rank(1, uid, 0)
+    yield c
+    c.destroy()
+
+
+def test_comm_queries(comm1):
+    assert comm1.count == 1 and comm1.rank == 0 and comm1.device == 0
+    assert comm1.async_error() == nccl.ncclSuccess
+
+
+def test_config1_allreduce_1kib_identity(comm1):
+    """ncclAllReduce fp32 sum, 1 KiB, world 1: output bitwise equal to input."""
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.rand(256, device="cuda", generator=g) * 2 - 1
+    y = torch.full_like(x, float("nan"))
+    comm1.all_reduce(x.data_ptr(), y.data_ptr(), 256, nccl.ncclFloat32, nccl.ncclSum, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+    x0 = x.clone()
+    comm1.all_reduce(x.data_ptr(), x.data_ptr(), 256, nccl.ncclFloat32, nccl.ncclSum, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(x0.view(torch.int32), x.view(torch.int32))
+
+
+@pytest.mark.parametrize("dt,tdt", [(nccl.ncclFloat32, torch.float32), (nccl.ncclFloat16, torch.float16),
+                                    (nccl.ncclBfloat16, torch.bfloat16), (nccl.ncclFloat64, torch.float64),
+                                    (nccl.ncclInt32, torch.int32), (nccl.ncclUint8, torch.uint8)])
+@pytest.mark.parametrize("op", [0, 1, 2, 3, 4])
+def test_one_rank_all_ops(comm1, dt, tdt, op):
+    n = 4099
+    if tdt.is_floating_point:
+        x = torch.randn(n, device="cuda").to(tdt)
+    else:
+        x = torch.randint(0, 100, (n,), device="cuda").to(tdt)
+    y = torch.empty_like(x)
+    comm1.all_reduce(x.data_ptr(), y.data_ptr(), n, dt, op, stream_ptr())
+    torch.cuda.synchronize()
+    # avg on floats runs the PreMulSum kernel with scalar 1/1 = 1: x*1 == x
+    assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+    z = torch.empty_like(x)
+    comm1.reduce_scatter(x.data_ptr(), z.data_ptr(), n, dt, op, stream_ptr())
+    w = torch.empty_like(x)
+    comm1.all_gather(x.data_ptr(), w.data_ptr(), n, dt, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(x.view(torch.uint8), z.view(torch.uint8))
+    assert torch.equal(x.view(torch.uint8), w.view(torch.uint8))
+
+
+def test_user_premulsum(comm1):
+    n = 1000
+    x = torch.randn(n, device="cuda")
+    y = torch.empty_like(x)
+    half = ctypes.c_float(0.5)
+    op = comm1.create_premulsum(ctypes.addressof(half), nccl.ncclFloat32, nccl.ncclScalarHostImmediate)
+    assert op >= nccl.ncclAvg + 1
+    comm1.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, op, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(y, x * 0.5)
+    # device-resident scalar, read by the kernel
+    s = torch.tensor([3.0], device="cuda")
+    op2 = comm1.create_premulsum(s.data_ptr(), nccl.ncclFloat32, nccl.ncclScalarDevice)
+    comm1.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, op2, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(y, x * 3.0)
+    # type mismatch with the op's datatype -> invalid argument (enqueue.cc:2301-2305)
+    with pytest.raises(nccl.VcclError) as e:
+        comm1.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat64, op, stream_ptr())
+    assert e.value.code == nccl.ncclInvalidArgument
+    comm1.destroy_op(op)
+    comm1.destroy_op(op2)
+    with pytest.raises(nccl.VcclError):
+        comm1.destroy_op(op)
+
+
+def test_arg_errors(comm1):
+    L = nccl.lib()
+    x = torch.zeros(16, device="cuda")
+    p = x.data_ptr()
+    assert L.ncclAllReduce(p, p, 16, 12, 0, comm1.handle, None) == nccl.ncclInvalidArgument  # bad type
+    assert L.ncclAllReduce(p, p, 16, 7, 17, comm1.handle, None) == nccl.ncclInvalidArgument  # unknown op
+    assert L.ncclAllReduce(p, p, 16, 7, -1, comm1.handle, None) == nccl.ncclInvalidArgument
+    assert L.ncclAllReduce(p, p, 16, 7, 0, None, None) == nccl.ncclInvalidArgument  # NULL comm
+    assert L.ncclAllReduce(p, p, 16, nccl.ncclFloat8e4m3, 0, comm1.handle, None) == nccl.ncclInvalidArgument
+    assert L.ncclAllReduce(p, p, 0, 7, 0, comm1.handle, None) == nccl.ncclSuccess  # empty: no-op
+    assert L.ncclGroupEnd() == nccl.ncclInvalidUsage  # not in a group
+    assert nccl.lib().ncclGetErrorString(4) == b"invalid argument (run with NCCL_DEBUG=WARN for details)"
+
+
+def test_group_calls(comm1):
+    xs = [torch.randn(1000 + i, device="cuda") for i in range(4)]
+    ys = [torch.empty_like(x) for x in xs]
+    nccl.group_start()
+    nccl.group_start()  # nested
+    for x, y in zip(xs, ys):
+        comm1.all_reduce(x.data_ptr(), y.data_ptr(), x.numel(), nccl.ncclFloat32, nccl.ncclSum, stream_ptr())
+    nccl.group_end()
+    nccl.group_end()
+    torch.cuda.synchronize()
+    for x, y in zip(xs, ys):
+        assert torch.equal(x, y)
+
+
+def test_oracle_allreduce_one_rank_semantics():
+    # the oracle's API-level restatement agrees (world 1: copy / x*1)
+    x = np.arange(10, dtype=np.float32)
+    assert np.array_equal(O.allreduce(4, 7, [x]), x)

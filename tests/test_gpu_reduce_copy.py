@@ -1,0 +1,153 @@
+"""Parity of the HIP reduce-copy engine (vcclReduceCopy C ABI) on MI355X.
+
+* every golden vector (10 types x 5 ops x {2,3,8} sources), bit-exact;
+* the same against the CPU oracle at ragged sizes, misaligned pointers,
+  several destinations, in-place operation;
+* full-size (256 MiB, BASELINE config 2) 2-source f32 sum: bit-exact to
+  numpy's a + b;
+* C-ABI error behaviour (invalid op/type/counts).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests._util import FLOAT_TYPES, assert_bitexact, golden_rc_cases
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU, skipped there
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from tests.gpu_util import empty_dev, from_dev, stream_ptr, to_dev  # noqa: E402
+from vccl_amd import nccl  # noqa: E402
+
+
+def _run(dev_op, t, arg, srcs_np, n_dsts=1, pre=0, post=False, offsets=None, config=None):
+    n = srcs_np[0].size
+    dt = srcs_np[0].dtype
+    offsets = offsets or [0] * (len(srcs_np) + n_dsts)
+    keep, sp, dp = [], [], []
+    for i, s in enumerate(srcs_np):
+        tt, p = to_dev(s, offset=offsets[i])
+        keep.append(tt)
+        sp.append(p)
+    outs = []
+    for j in range(n_dsts):
+        tt, p = empty_dev(n * dt.itemsize, offset=offsets[len(srcs_np) + j])
+        outs.append((tt, offsets[len(srcs_np) + j]))
+        dp.append(p)
+    nccl.reduce_copy(dev_op, t, arg, sp, dp, n, stream_ptr(), pre_op_srcs=pre, post_op=post,
+                     config=config)
+    torch.cuda.synchronize()
+    return [from_dev(tt, dt, n, off) for tt, off in outs]
+
+
+def _dev_args(op, t, nsrc):
+    dev_op, arg = nccl.host_to_dev_redop(op, t, nsrc)
+    assert (dev_op, arg) == O.host_to_dev_redop(op, t, nsrc)
+    pre = nsrc if dev_op == nccl.vcclDevPreMulSum else 0
+    return dev_op, arg, pre, dev_op == nccl.vcclDevSumPostDiv
+
+
+def test_golden_vectors_bitexact(golden):
+    n = 0
+    for key, t, op, nsrc, inp, exp in golden_rc_cases(golden):
+        dev_op, arg, pre, post = _dev_args(op, t, nsrc)
+        got = _run(dev_op, t, arg, [inp[i] for i in range(nsrc)], pre=pre, post=post)[0]
+        assert_bitexact(t, got, exp, minmax=op in (2, 3), what=key)
+        n += 1
+    assert n == 150
+
+
+def _rand(rng, t, n):
+    if t in (0, 1, 2, 3, 4, 5):
+        dt = O.NP_DTYPE[t]
+        return rng.integers(0, 2**63, size=n, dtype=np.int64).astype(np.uint64).view(np.int64).astype(dt)
+    if t == 9:
+        return O.f32_to_bf16_bits(rng.uniform(-2, 2, n).astype(np.float32))
+    return rng.uniform(-2, 2, n).astype(O.NP_DTYPE[t])
+
+
+@pytest.mark.parametrize("t", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("op", [0, 1, 2, 3, 4])
+def test_ragged_sizes_vs_oracle(t, op):
+    rng = np.random.default_rng(100 * t + op)
+    for n in (1, 7, 16, 1000, 4099, 65536 + 13, 1 << 20):
+        nsrc = 2 if n % 2 else 3
+        srcs = [_rand(rng, t, n) for _ in range(nsrc)]
+        dev_op, arg, pre, post = _dev_args(op, t, nsrc)
+        got = _run(dev_op, t, arg, srcs, pre=pre, post=post)[0]
+        exp = O.reduce_copy(dev_op, t, arg, srcs, pre_op_args=[arg] * pre, post_op=post)[0]
+        assert_bitexact(t, got, exp, minmax=op in (2, 3), what=f"t{t} op{op} n{n}")
+
+
+@pytest.mark.parametrize("t", [1, 6, 7, 8, 9])
+def test_misaligned_and_multi_dst(t):
+    rng = np.random.default_rng(7 + t)
+    n = 100_003
+    sz = np.dtype(O.NP_DTYPE[t]).itemsize
+    srcs = [_rand(rng, t, n) for _ in range(3)]
+    exp = O.reduce_copy(0, t, 0, srcs)[0]
+    # same misalignment on every pointer, then different misalignments
+    for offs in ([sz] * 6, [0, sz, 2 * sz, 0, sz, 3 * sz]):
+        outs = _run(0, t, 0, srcs, n_dsts=3, offsets=offs)
+        for o in outs:
+            assert_bitexact(t, o, exp, what=f"t{t} offs{offs}")
+
+
+def test_eight_sources_and_geometry_sweep():
+    rng = np.random.default_rng(11)
+    n = (1 << 22) + 5
+    srcs = [rng.standard_normal(n).astype(np.float32) for _ in range(8)]
+    exp = O.reduce_copy(0, 7, 0, srcs)[0]
+    got = _run(0, 7, 0, srcs)[0]
+    assert_bitexact(7, got, exp, what="8 srcs")
+    two = srcs[:2]
+    exp2 = two[0] + two[1]
+    for cfg in ({"blockSize": 256, "unroll": 4, "gridBlocks": 0, "ntLoads": 0, "ntStores": 0},
+                {"blockSize": 512, "unroll": 8, "gridBlocks": 1024, "ntLoads": 1, "ntStores": 1},
+                {"blockSize": 1024, "unroll": 2, "gridBlocks": 7, "ntLoads": 0, "ntStores": 1},
+                {"blockSize": 256, "unroll": 8, "gridBlocks": 0, "ntLoads": 1, "ntStores": 0}):
+        got = _run(0, 7, 0, two, config=cfg)[0]
+        assert np.array_equal(got.view(np.uint32), exp2.view(np.uint32)), cfg
+
+
+def test_in_place():
+    rng = np.random.default_rng(5)
+    n = 1 << 20
+    a = rng.standard_normal(n).astype(np.float32)
+    b = rng.standard_normal(n).astype(np.float32)
+    ta, pa = to_dev(a)
+    tb, pb = to_dev(b)
+    nccl.reduce_copy(0, 7, 0, [pa, pb], [pa], n, stream_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(from_dev(ta, np.float32, n), a + b)
+
+
+def test_full_size_config2_bitexact():
+    """BASELINE config 2: 2 x 256 MiB f32 -> 256 MiB, seeds 1 and 2."""
+    n = 1 << 26
+    g1 = torch.Generator(device="cuda").manual_seed(1)
+    g2 = torch.Generator(device="cuda").manual_seed(2)
+    a = torch.rand(n, device="cuda", generator=g1) * 2 - 1
+    b = torch.rand(n, device="cuda", generator=g2) * 2 - 1
+    d = torch.empty_like(a)
+    nccl.reduce_copy(0, 7, 0, [a.data_ptr(), b.data_ptr()], [d.data_ptr()], n, stream_ptr())
+    torch.cuda.synchronize()
+    ref = a + b  # IEEE f32 add, same single rounding
+    assert torch.equal(d.view(torch.int32), ref.view(torch.int32))
+
+
+def test_abi_errors():
+    L = nccl.lib()
+    import ctypes
+    s = (ctypes.c_void_p * 1)(0x1000)
+    d = (ctypes.c_void_p * 1)(0x2000)
+    # SumPostDiv on float, copy on non-byte type, 0 / 9 sources
+    assert L.vcclReduceCopy(4, 7, 0, 0, 0, 1, s, 1, d, 16, None) == nccl.ncclInvalidArgument
+    assert L.vcclReduceCopy(15, 7, 0, 0, 0, 1, s, 1, d, 16, None) == nccl.ncclInvalidArgument
+    assert L.vcclReduceCopy(0, 7, 0, 0, 0, 0, s, 1, d, 16, None) == nccl.ncclInvalidArgument
+    assert L.vcclReduceCopy(0, 12, 0, 0, 0, 1, s, 1, d, 16, None) == nccl.ncclInvalidArgument
+    # count 0 is a successful no-op even with bogus pointers
+    assert L.vcclReduceCopy(0, 7, 0, 0, 0, 1, s, 1, d, 0, None) == nccl.ncclSuccess

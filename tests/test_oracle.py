@@ -1,0 +1,130 @@
+"""Pin the CPU oracle (oracle/reduce_ref.c) before trusting it.
+
+* against the independent golden vectors (numpy / torch-CPU IEEE semantics);
+* against the reference's own generate.py dispatch table (functable.json);
+* f16 / bf16 conversion exhaustively against numpy / torch.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests._util import (FLOAT_TYPES, assert_bitexact, golden_rc_cases)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _api_to_dev(op, t, n):
+    dev_op, arg = O.host_to_dev_redop(op, t, n)
+    pre = [arg] * n if dev_op == O.DEV_PREMULSUM else []
+    return dev_op, arg, pre, dev_op == O.DEV_SUMPOSTDIV
+
+
+def test_oracle_matches_golden_reduce_copy(golden):
+    n_cases = 0
+    for key, t, op, nsrc, inp, exp in golden_rc_cases(golden):
+        dev_op, arg, pre, post = _api_to_dev(op, t, nsrc)
+        srcs = [inp[i] for i in range(nsrc)]
+        got = O.reduce_copy(dev_op, t, arg, srcs, pre_op_args=pre, post_op=post)[0]
+        assert_bitexact(t, got, exp, minmax=op in (2, 3), what=key)
+        n_cases += 1
+    assert n_cases == 10 * 5 * 3
+
+
+def test_oracle_ring_fold_matches_golden(golden):
+    for k in golden.files:
+        if not (k.startswith("ring_") and k.endswith("_in")):
+            continue
+        base = k[:-3]
+        t = {"f32": 7, "f16": 6, "bf16": 9}[base.split("_")[1]]
+        inp, owner, exp = golden[k], golden[base + "_owner"], golden[base + "_out"]
+        got = O.ring_fold(O.DEV_SUM, t, 0, False, [inp[i] for i in range(inp.shape[0])], owner)
+        assert_bitexact(t, got, exp, what=base)
+
+
+def test_oracle_threads_agree():
+    rng = np.random.default_rng(1)
+    a = rng.standard_normal(100_003).astype(np.float32)
+    b = rng.standard_normal(100_003).astype(np.float32)
+    one = O.reduce_copy(O.DEV_SUM, 7, 0, [a, b], nthreads=1)[0]
+    many = O.reduce_copy(O.DEV_SUM, 7, 0, [a, b], nthreads=7)[0]
+    assert np.array_equal(one.view(np.uint32), many.view(np.uint32))
+    assert np.array_equal(one, a + b)
+
+
+def test_f16_conversion_exhaustive():
+    L = O.lib()
+    bits = np.arange(0, 1 << 16, dtype=np.uint32).astype(np.uint16)
+    f = bits.view(np.float16).astype(np.float32)
+    # f16 -> f32 -> f16 round trip is the identity (NaNs stay NaN)
+    rt = np.array([L.ref_f32_to_f16(float(x)) for x in f[::7]], dtype=np.uint16)
+    src = bits[::7]
+    nan = np.isnan(f[::7])
+    assert np.array_equal(rt[~nan], src[~nan])
+    assert np.all(np.isnan(rt[nan].view(np.float16)))
+    # f32 -> f16 rounding against numpy on random + boundary values
+    rng = np.random.default_rng(2)
+    xs = np.concatenate([rng.standard_normal(4000).astype(np.float32) * 10.0 ** rng.integers(-9, 6, 4000),
+                         np.float32([65504, 65519.99, 65520, 6.1035156e-05, 5.96e-08, 2.98e-08,
+                                     2.99e-08, 1e-30, -0.0])]).astype(np.float32)
+    ours = np.array([L.ref_f32_to_f16(float(x)) for x in xs], dtype=np.uint16)
+    assert np.array_equal(ours, xs.astype(np.float16).view(np.uint16))
+
+
+def test_bf16_conversion_against_torch():
+    L = O.lib()
+    rng = np.random.default_rng(3)
+    xs = np.concatenate([rng.standard_normal(4000).astype(np.float32) * 10.0 ** rng.integers(-30, 30, 4000),
+                         np.float32([3.3895e38, 3.4e38, 1e-40, -0.0, np.inf])]).astype(np.float32)
+    ours = np.array([L.ref_f32_to_bf16(float(x)) for x in xs], dtype=np.uint16)
+    ref = torch.from_numpy(xs).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+    assert np.array_equal(ours, ref)
+    assert np.array_equal(O.f32_to_bf16_bits(xs), ref)
+
+
+def test_host_to_dev_redop_encoding():
+    # enqueue.cc:2240-2256 — xormask for min/max
+    assert O.host_to_dev_redop(3, 2, 4) == (2, 0x80000000)        # min i32
+    assert O.host_to_dev_redop(2, 2, 4) == (2, 0x7FFFFFFF)        # max i32
+    assert O.host_to_dev_redop(3, 3, 4) == (2, 0)                 # min u32
+    assert O.host_to_dev_redop(2, 5, 4) == (2, 0xFFFFFFFFFFFFFFFF)  # max u64
+    assert O.host_to_dev_redop(2, 7, 4) == (2, 0xFFFFFFFF)        # max f32: bit0 = 1
+    assert O.host_to_dev_redop(3, 9, 4) == (2, 0)                 # min bf16
+    # avg: ints SumPostDiv nRanks<<1|signed, floats PreMulSum 1/n bits
+    assert O.host_to_dev_redop(4, 0, 8) == (4, (8 << 1) | 1)
+    assert O.host_to_dev_redop(4, 5, 3) == (4, 3 << 1)
+    assert O.host_to_dev_redop(4, 7, 4) == (3, int(np.float32(0.25).view(np.uint32)))
+    assert O.host_to_dev_redop(4, 6, 3) == (3, int(np.float16(1 / 3).view(np.uint16)))
+
+
+def test_functable_signed_maps_to_unsigned():
+    """Reference generate.py (run unmodified, tests/golden/gen_functable.py):
+    rows sharing a primary id run one kernel.  Our dispatch
+    (vcclKernelTypeOf, vccl_amd/csrc/device/dispatch.hpp) maps (devOp, type)
+    to a kernel element type; two rows share a reference id iff they share
+    our kernel type, and a row the reference does not build (id -1) is
+    rejected by ours (-1).  Loads libvccl.so; makes no GPU call."""
+    from vccl_amd import nccl
+    table = json.load(open(os.path.join(ROOT, "tests", "golden", "functable.json")))
+    devop = {"Sum": 0, "Prod": 1, "MinMax": 2, "PreMulSum": 3, "SumPostDiv": 4}
+    tyid = {"i8": 0, "u8": 1, "i32": 2, "u32": 3, "i64": 4, "u64": 5, "f16": 6, "f32": 7,
+            "f64": 8, "bf16": 9}
+    by_key = {}
+    for r in table["rows"]:
+        if r["coll"] == "AllGather" or r["type"] in ("f8e4m3", "f8e5m2"):
+            continue
+        by_key.setdefault((r["coll"], r["redop"], r["algo"], r["proto"]), []).append(r)
+    kt = lambda r: nccl.kernel_type_of(devop[r["redop"]], tyid[r["type"]])  # noqa: E731
+    checked = 0
+    for rows in by_key.values():
+        for r1 in rows:
+            assert (kt(r1) >= 0) == (r1["id"] != -1), r1
+            for r2 in rows:
+                if r1["id"] == -1 or r2["id"] == -1:
+                    continue
+                assert (r1["id"] == r2["id"]) == (kt(r1) == kt(r2)), (r1, r2)
+                checked += 1
+    assert checked > 500

@@ -1,0 +1,28 @@
+// Host-side launcher declarations shared by the per-type kernel TUs and the
+// C-ABI layer (one explicit specialisation per kernel element type).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dispatch.hpp"
+#include "reduce_copy.hpp"
+
+namespace vccl {
+
+// Library defaults for the grid-wide reduce-copy.
+constexpr int kRcDefBlock = 256;
+constexpr int kRcDefUnroll = 4;
+constexpr int kRcDefBlocksPerCU = 8;
+
+// Internal entry used by both the C ABI and the one-rank path.  `a` holds the
+// pointers; geometry from cfg (nullptr = defaults).
+struct vcclLaunchConfigLite {
+  int blockSize, unroll, gridBlocks, ntLoads, ntStores;
+};
+hipError_t reduce_copy_launch(int devOp, int datatype, uint64_t redArg, RCArgs a, int64_t nElts,
+                              const vcclLaunchConfigLite* cfg, hipStream_t stream);
+
+template <int K>
+hipError_t rc_launch(int devOp, const RCArgs& a, int64_t nElts, uint64_t redArg,
+                     const LaunchGeom& lg, hipStream_t stream);
+
+}  // namespace vccl

@@ -1,0 +1,267 @@
+// Reduction-op functors for the bucket-reduction path, written for gfx950.
+//
+// Semantics follow VCCL src/device/reduce_kernel.h (file:line per functor);
+// the implementation is CDNA4-native: 16-byte packs are processed as plain
+// element loops that hipcc lowers to packed VALU (v_pk_add_f32, v_pk_add_f16,
+// v_pk_mul_f32, ...); bf16 goes through f32 and v_cvt_pk_bf16_f32 (RN-even,
+// NaN-preserving), which is bit-identical to __hadd/__hmul on bf16 because f32
+// carries 24 >= 2*8+2 significand bits (no double-rounding error).
+//
+// Kernel element types (KT) follow generate.py:129-137: signed integers run the
+// unsigned kernel (two's-complement wrap; MinMax restores signed order through
+// the xormask, reduce_kernel.h:193-198 / enqueue.cc:2240-2256).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vccl {
+
+// ---------------------------------------------------------------- bf16 bits
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __builtin_bit_cast(float, (uint32_t)h << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  return __builtin_bit_cast(uint16_t, (__bf16)f);  // v_cvt_pk_bf16_f32: RN-even
+}
+
+struct bf16_t { uint16_t bits; };  // storage-only tag type
+
+// ---------------------------------------------------------------- helpers
+template <typename T> struct IsFloat { static constexpr bool value = false; };
+template <> struct IsFloat<_Float16> { static constexpr bool value = true; };
+template <> struct IsFloat<float> { static constexpr bool value = true; };
+template <> struct IsFloat<double> { static constexpr bool value = true; };
+template <> struct IsFloat<bf16_t> { static constexpr bool value = true; };
+
+template <typename T>
+__device__ __forceinline__ T from_arg(uint64_t arg) {
+  union { uint64_t u; T v; } x;
+  x.u = arg;
+  return x.v;
+}
+
+// IEEE minNum/maxNum as fminf/fmaxf (reduce_kernel.h:264-265) and
+// __hmin/__hmax (:282-284, :297-299): NaN-avoiding.
+__device__ __forceinline__ float minmax_f32(float a, float b, bool isMin) {
+  return isMin ? __builtin_fminf(a, b) : __builtin_fmaxf(a, b);
+}
+
+// ---------------------------------------------------------------- Sum
+// reduce_kernel.h:181-186 (generic), :267-272 (f16 __hadd), :291-293 (bf16)
+template <typename T> struct FnSum {
+  using EltType = T;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  __device__ FnSum(uint64_t = 0) {}
+  __device__ __forceinline__ T reduce(T a, T b) const { return a + b; }
+  __device__ __forceinline__ T preOp(T a) const { return a; }
+  __device__ __forceinline__ T postOp(T a) const { return a; }
+};
+template <> struct FnSum<bf16_t> {
+  using EltType = bf16_t;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  __device__ FnSum(uint64_t = 0) {}
+  __device__ __forceinline__ bf16_t reduce(bf16_t a, bf16_t b) const {
+    return {f32_to_bf16(bf16_to_f32(a.bits) + bf16_to_f32(b.bits))};
+  }
+  __device__ __forceinline__ bf16_t preOp(bf16_t a) const { return a; }
+  __device__ __forceinline__ bf16_t postOp(bf16_t a) const { return a; }
+};
+
+// ---------------------------------------------------------------- Prod
+// reduce_kernel.h:187-192, :273-275 (f16 __hmul), :294-296 (bf16)
+template <typename T> struct FnProd {
+  using EltType = T;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  __device__ FnProd(uint64_t = 0) {}
+  __device__ __forceinline__ T reduce(T a, T b) const { return a * b; }
+  __device__ __forceinline__ T preOp(T a) const { return a; }
+  __device__ __forceinline__ T postOp(T a) const { return a; }
+};
+template <> struct FnProd<uint8_t> {  // per-byte product mod 256 (:237-250)
+  using EltType = uint8_t;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  __device__ FnProd(uint64_t = 0) {}
+  __device__ __forceinline__ uint8_t reduce(uint8_t a, uint8_t b) const {
+    return (uint8_t)((uint32_t)a * (uint32_t)b);
+  }
+  __device__ __forceinline__ uint8_t preOp(uint8_t a) const { return a; }
+  __device__ __forceinline__ uint8_t postOp(uint8_t a) const { return a; }
+};
+template <> struct FnProd<bf16_t> {
+  using EltType = bf16_t;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  __device__ FnProd(uint64_t = 0) {}
+  __device__ __forceinline__ bf16_t reduce(bf16_t a, bf16_t b) const {
+    return {f32_to_bf16(bf16_to_f32(a.bits) * bf16_to_f32(b.bits))};
+  }
+  __device__ __forceinline__ bf16_t preOp(bf16_t a) const { return a; }
+  __device__ __forceinline__ bf16_t postOp(bf16_t a) const { return a; }
+};
+
+// ---------------------------------------------------------------- MinMax
+// reduce_kernel.h:47-56 (ctor: xormask, isMinNotMax = (opArg&1)==0), :193-198
+template <typename T> struct FnMinMax {  // unsigned integer kernels
+  using EltType = T;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  T xormask;
+  __device__ FnMinMax(uint64_t arg = 0) : xormask((T)arg) {}
+  __device__ __forceinline__ T reduce(T a, T b) const {
+    return (T)(a ^ xormask) < (T)(b ^ xormask) ? a : b;
+  }
+  __device__ __forceinline__ T preOp(T a) const { return a; }
+  __device__ __forceinline__ T postOp(T a) const { return a; }
+};
+template <> struct FnMinMax<float> {
+  using EltType = float;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  bool isMin;
+  __device__ FnMinMax(uint64_t arg = 0) : isMin((arg & 1) == 0) {}
+  __device__ __forceinline__ float reduce(float a, float b) const { return minmax_f32(a, b, isMin); }
+  __device__ __forceinline__ float preOp(float a) const { return a; }
+  __device__ __forceinline__ float postOp(float a) const { return a; }
+};
+template <> struct FnMinMax<double> {
+  using EltType = double;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  bool isMin;
+  __device__ FnMinMax(uint64_t arg = 0) : isMin((arg & 1) == 0) {}
+  __device__ __forceinline__ double reduce(double a, double b) const {
+    return isMin ? __builtin_fmin(a, b) : __builtin_fmax(a, b);
+  }
+  __device__ __forceinline__ double preOp(double a) const { return a; }
+  __device__ __forceinline__ double postOp(double a) const { return a; }
+};
+template <> struct FnMinMax<_Float16> {
+  using EltType = _Float16;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  bool isMin;
+  __device__ FnMinMax(uint64_t arg = 0) : isMin((arg & 1) == 0) {}
+  __device__ __forceinline__ _Float16 reduce(_Float16 a, _Float16 b) const {
+    return (_Float16)minmax_f32((float)a, (float)b, isMin);  // exact both ways
+  }
+  __device__ __forceinline__ _Float16 preOp(_Float16 a) const { return a; }
+  __device__ __forceinline__ _Float16 postOp(_Float16 a) const { return a; }
+};
+template <> struct FnMinMax<bf16_t> {
+  using EltType = bf16_t;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  bool isMin;
+  __device__ FnMinMax(uint64_t arg = 0) : isMin((arg & 1) == 0) {}
+  __device__ __forceinline__ bf16_t reduce(bf16_t a, bf16_t b) const {
+    return {f32_to_bf16(minmax_f32(bf16_to_f32(a.bits), bf16_to_f32(b.bits), isMin))};
+  }
+  __device__ __forceinline__ bf16_t preOp(bf16_t a) const { return a; }
+  __device__ __forceinline__ bf16_t postOp(bf16_t a) const { return a; }
+};
+
+// ---------------------------------------------------------------- PreMulSum
+// reduce_kernel.h:424-583: reduce = Sum, preOp = x * scalar (in T).
+template <typename T> struct FnPreMulSum {
+  using EltType = T;
+  static constexpr bool kPreOp = true, kPostOp = false;
+  T scalar;
+  __device__ FnPreMulSum(uint64_t arg = 0) : scalar(from_arg<T>(arg)) {}
+  __device__ __forceinline__ T reduce(T a, T b) const { return a + b; }
+  __device__ __forceinline__ T preOp(T a) const { return a * scalar; }
+  __device__ __forceinline__ T postOp(T a) const { return a; }
+};
+template <> struct FnPreMulSum<uint8_t> {
+  using EltType = uint8_t;
+  static constexpr bool kPreOp = true, kPostOp = false;
+  uint8_t scalar;
+  __device__ FnPreMulSum(uint64_t arg = 0) : scalar((uint8_t)arg) {}
+  __device__ __forceinline__ uint8_t reduce(uint8_t a, uint8_t b) const { return (uint8_t)(a + b); }
+  __device__ __forceinline__ uint8_t preOp(uint8_t a) const { return (uint8_t)((uint32_t)a * scalar); }
+  __device__ __forceinline__ uint8_t postOp(uint8_t a) const { return a; }
+};
+template <> struct FnPreMulSum<bf16_t> {
+  using EltType = bf16_t;
+  static constexpr bool kPreOp = true, kPostOp = false;
+  float scalar;
+  __device__ FnPreMulSum(uint64_t arg = 0) : scalar(bf16_to_f32((uint16_t)arg)) {}
+  __device__ __forceinline__ bf16_t reduce(bf16_t a, bf16_t b) const {
+    return {f32_to_bf16(bf16_to_f32(a.bits) + bf16_to_f32(b.bits))};
+  }
+  __device__ __forceinline__ bf16_t preOp(bf16_t a) const {
+    return {f32_to_bf16(bf16_to_f32(a.bits) * scalar)};
+  }
+  __device__ __forceinline__ bf16_t postOp(bf16_t a) const { return a; }
+};
+
+// ---------------------------------------------------------------- SumPostDiv
+// reduce_kernel.h:641-688: integer avg = sum, then truncating divide at the
+// final step through a 32/64-bit reciprocal and one fix-up.
+template <typename T> struct FnSumPostDiv {
+  using EltType = T;
+  using U = typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type;
+  static constexpr bool kPreOp = false, kPostOp = true;
+  uint32_t divisor;
+  bool isSigned;
+  U recip;
+  __device__ FnSumPostDiv(uint64_t arg = 0)
+      : divisor((uint32_t)((arg >> 1) & 0x7fffffffu)), isSigned(arg & 1),
+        recip(divisor ? U(-1) / divisor : 0) {}
+  __device__ __forceinline__ T reduce(T a, T b) const { return (T)(a + b); }
+  __device__ __forceinline__ T preOp(T a) const { return a; }
+  __device__ __forceinline__ T postOp(T x) const {
+    bool xneg = isSigned && (x & ~(T(-1) >> 1));
+    U xabs = xneg ? (U)(T)(T(0) - x) : (U)x;
+    U q;
+    if constexpr (sizeof(T) == 8) q = __umul64hi(xabs, recip);
+    else q = __umulhi(xabs, recip);
+    if (xabs - q * divisor >= divisor) q += 1;
+    return xneg ? (T)(T(0) - (T)q) : (T)q;
+  }
+};
+
+// ---------------------------------------------------------------- Copy
+// FuncCopy (reduce_kernel.h:41, :176-180): used by all-gather / one-rank copy.
+template <typename T> struct FnCopy {
+  using EltType = T;
+  static constexpr bool kPreOp = false, kPostOp = false;
+  __device__ FnCopy(uint64_t = 0) {}
+  __device__ __forceinline__ T reduce(T a, T) const { return a; }
+  __device__ __forceinline__ T preOp(T a) const { return a; }
+  __device__ __forceinline__ T postOp(T a) const { return a; }
+};
+
+// ---------------------------------------------------------------- packs
+// 16-byte pack = one global_load_dwordx4 per lane.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+union Pack16 {
+  u32x4 v;
+  T e[16 / sizeof(T)];
+};
+
+template <class Fn>
+__device__ __forceinline__ u32x4 pack_reduce(const Fn& fn, u32x4 a, u32x4 b) {
+  using T = typename Fn::EltType;
+  Pack16<T> x, y;
+  x.v = a;
+  y.v = b;
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(T)); i++) x.e[i] = fn.reduce(x.e[i], y.e[i]);
+  return x.v;
+}
+template <class Fn>
+__device__ __forceinline__ u32x4 pack_preop(const Fn& fn, u32x4 a) {
+  using T = typename Fn::EltType;
+  Pack16<T> x;
+  x.v = a;
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(T)); i++) x.e[i] = fn.preOp(x.e[i]);
+  return x.v;
+}
+template <class Fn>
+__device__ __forceinline__ u32x4 pack_postop(const Fn& fn, u32x4 a) {
+  using T = typename Fn::EltType;
+  Pack16<T> x;
+  x.v = a;
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(T)); i++) x.e[i] = fn.postOp(x.e[i]);
+  return x.v;
+}
+
+}  // namespace vccl

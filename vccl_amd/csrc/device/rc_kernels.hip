@@ -1,0 +1,65 @@
+// Grid-wide reduce-copy kernels for ONE kernel element type (VCCL_KT), so the
+// build compiles the 7 element types in parallel.  Semantics: reduceCopy()
+// (common_kernel.h:208-285) and oneRankReduce (onerank.cu:13-44).
+#include <hip/hip_runtime.h>
+
+#include "dispatch.hpp"
+#include "launch.hpp"
+#include "reduce_copy.hpp"
+
+#ifndef VCCL_KT
+#error "compile with -DVCCL_KT=<kernel element type>"
+#endif
+
+namespace vccl {
+
+template <class Fn, int NS, int ND, int UNROLL, int LD, int ST>
+__global__ __launch_bounds__(1024) void k_reduce_copy(RCArgs a, int64_t nElts, uint64_t redArg) {
+  Fn fn(load_op_arg(a.argPtr, a.argBytes, redArg));
+  reduce_copy<Fn, NS, ND, UNROLL, LD, ST>(fn, a, nElts, blockIdx.x, gridDim.x, threadIdx.x,
+                                          blockDim.x);
+}
+
+template <class Fn, int NS, int ND>
+static hipError_t launch_nsnd(const RCArgs& a, int64_t nElts, uint64_t redArg,
+                              const LaunchGeom& lg, hipStream_t s) {
+  dim3 g(lg.grid), b(lg.block);
+  // Only the benchmark shape (2-src f32 sum) carries the full sweep set; every
+  // other functor gets the default geometry (keeps the code object small).
+  constexpr bool kSweep = std::is_same<Fn, FnSum<float>>::value && NS == 2 && ND == 1;
+#define VCCL_RC_LAUNCH(U, L, S)                                                             \
+  hipLaunchKernelGGL((k_reduce_copy<Fn, NS, ND, U, L, S>), g, b, 0, s, a, nElts, redArg); \
+  return hipGetLastError();
+  if constexpr (!kSweep) {
+    VCCL_RC_LAUNCH(kRcDefUnroll, kLdPlain, kStPlain)
+  } else {
+    const int ntl = lg.ntLoads, nts = lg.ntStores;
+    if (lg.unroll == 8) {
+      if (ntl && nts) { VCCL_RC_LAUNCH(8, kLdNT, kStNT) }
+      if (ntl) { VCCL_RC_LAUNCH(8, kLdNT, kStPlain) }
+      if (nts) { VCCL_RC_LAUNCH(8, kLdPlain, kStNT) }
+      VCCL_RC_LAUNCH(8, kLdPlain, kStPlain)
+    }
+    if (lg.unroll == 2) { VCCL_RC_LAUNCH(2, kLdPlain, kStPlain) }
+    if (ntl && nts) { VCCL_RC_LAUNCH(4, kLdNT, kStNT) }
+    if (ntl) { VCCL_RC_LAUNCH(4, kLdNT, kStPlain) }
+    if (nts) { VCCL_RC_LAUNCH(4, kLdPlain, kStNT) }
+    VCCL_RC_LAUNCH(4, kLdPlain, kStPlain)
+  }
+#undef VCCL_RC_LAUNCH
+}
+
+template <>
+hipError_t rc_launch<VCCL_KT>(int devOp, const RCArgs& a, int64_t nElts, uint64_t redArg,
+                              const LaunchGeom& lg, hipStream_t stream) {
+  using T = typename KTypeOf<VCCL_KT>::T;
+  hipError_t err = hipErrorInvalidValue;
+  dispatch_op<T>(devOp, [&]<class Fn>() {
+    if (a.nSrcs == 2 && a.nDsts == 1) err = launch_nsnd<Fn, 2, 1>(a, nElts, redArg, lg, stream);
+    else if (a.nSrcs == 1 && a.nDsts == 1) err = launch_nsnd<Fn, 1, 1>(a, nElts, redArg, lg, stream);
+    else err = launch_nsnd<Fn, 0, 0>(a, nElts, redArg, lg, stream);
+  });
+  return err;
+}
+
+}  // namespace vccl

@@ -1,0 +1,222 @@
+// Ring primitives and schedules (SIMPLE protocol) for gfx950.
+//
+// Protocol semantics follow prims_simple.h:108-319 (waitPeer / genericOp /
+// postPeer) and the schedules all_reduce.h:12-83, reduce_scatter.h:12-55,
+// all_gather.h:12-83.  The MI355X design differs where the hardware does:
+//  * one workgroup per channel, no role warps or named barriers: lane 0 of
+//    wave 0 polls both credits, one s_barrier releases the workgroup, every
+//    thread copies/reduces, every wave drains its stores (s_waitcnt vmcnt(0)),
+//    s_barrier, lane 0 publishes (system-scope release fence + relaxed
+//    system-scope store of the step counter into the peer's flag);
+//  * FIFOs are uncached receiver-side HBM reached over xGMI by the sender;
+//  * every spin is bounded (abort flag + wall-clock timeout via s_memrealtime)
+//    so a lost peer ends the kernel instead of hanging the GPU.
+#pragma once
+#include "reduce_copy.hpp"
+#include "ring_types.hpp"
+
+namespace vccl {
+
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+struct RingCtx {
+  DevChannel* ch;
+  const DevComm* comm;
+  uint64_t recvStep, sendStep;
+  int tid, nthreads;
+  int slotBytes;
+  int* shAbort;  // LDS
+
+  // Bounded spin on `flag` until pred(value); returns false on abort/timeout.
+  // The timeout is per wait (no progress for spinTimeoutTicks), not per call.
+  __device__ bool spin_ge(const uint64_t* flag, uint64_t target) {
+    uint64_t spins = 0, start = 0;
+    while (ld_sys(flag) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (start == 0) start = now;
+        if (*comm->abortFlag) return false;
+        if (now - start > comm->spinTimeoutTicks) {
+          __hip_atomic_store(comm->errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return false;
+        }
+        if (__hip_atomic_load(comm->errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+          return false;
+      }
+    }
+    return true;
+  }
+
+  __device__ bool aborted() const { return *shAbort != 0; }
+
+  // One primitive call: at most one slot of payload.
+  //   srcs = [SRC ? own input] ++ [RECV ? recv slot]
+  //   dsts = [SEND ? peer slot] ++ [DST ? own output]
+  template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
+  __device__ void prim(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp) {
+    if (aborted()) return;
+    if (tid == 0) {
+      bool ok = true;
+      if (RECV) ok = spin_ge(ch->recvTail, recvStep + 1);
+      if (SEND && ok && sendStep + 1 > (uint64_t)kSteps) ok = spin_ge(ch->sendHead, sendStep + 1 - kSteps);
+      if (!ok) *shAbort = 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
+      drain_vmem();
+    }
+    __syncthreads();
+    if (aborted()) return;
+    if (nelem > 0) {
+      constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
+      constexpr int ND = (SEND ? 1 : 0) + (DST ? 1 : 0);
+      RCArgs a;
+      int s = 0, d = 0;
+      if (SRC) a.srcs[s++] = (const char*)src;
+      if (RECV) a.srcs[s++] = ch->recvFifo + (int64_t)(recvStep % kSteps) * slotBytes;
+      if (SEND) a.dsts[d++] = ch->sendFifo + (int64_t)(sendStep % kSteps) * slotBytes;
+      if (DST) a.dsts[d++] = (char*)dst;
+      a.nSrcs = NS;
+      a.nDsts = ND;
+      a.preOpSrcs = SRC ? 1 : 0;
+      a.postOp = postOp ? 1 : 0;
+      reduce_copy<Fn, NS, ND, UNROLL, kLdPlain, kStPlain>(fn, a, nelem, 0, 1, tid, nthreads);
+    }
+    drain_vmem();  // every storing wave: its payload stores are complete
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system-scope release
+      drain_vmem();
+      if (SEND) st_sys(ch->nextRecvTail, sendStep + 1);
+      if (RECV) st_sys(ch->prevSendHead, recvStep + 1);
+    }
+    if (SEND) sendStep++;
+    if (RECV) recvStep++;
+  }
+};
+
+__device__ __forceinline__ int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+__device__ __forceinline__ int64_t div_up(int64_t x, int64_t a) { return (x + a - 1) / a; }
+
+// Channel part of [0, count): contiguous, 16-byte-aligned element ranges.
+__device__ __forceinline__ void channel_part(int64_t count, int nch, int c, int64_t eltAlign,
+                                             int64_t* off, int64_t* len) {
+  int64_t per = align_up(div_up(count, nch), eltAlign);
+  int64_t lo = per * c < count ? per * c : count;
+  int64_t hi = per * (c + 1) < count ? per * (c + 1) : count;
+  *off = lo;
+  *len = hi - lo;
+}
+
+// ----------------------------------------------------------------- AllReduce
+// all_reduce.h:12-83 (runRing): RS then AG within one kernel, chunk c of each
+// round finishing at ring position c.
+template <class Fn, int UNROLL>
+__device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
+  using T = typename Fn::EltType;
+  const int n = w.nRanks;
+  const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
+  int64_t gridOff, chCount;
+  channel_part((int64_t)w.count, w.nChannels, c, eltAlign, &gridOff, &chCount);
+  const T* in = (const T*)w.sendbuff;
+  T* out = (T*)w.recvbuff;
+  const int ringIx = r.ch->ringPos;
+  int64_t chunkCount = w.slotBytes / (int64_t)sizeof(T);
+  const int64_t loopCount = (int64_t)n * chunkCount;
+  auto modRanks = [n](int x) { return x >= n ? x - n : x; };
+  for (int64_t eo = 0; eo < chCount; eo += loopCount) {
+    const int64_t rem = chCount - eo;
+    if (rem < loopCount) chunkCount = align_up(div_up(rem, n), eltAlign);
+    auto off_of = [&](int chunk) { return gridOff + eo + chunk * chunkCount; };
+    auto len_of = [&](int chunk) {
+      int64_t l = rem - (int64_t)chunk * chunkCount;
+      return l < chunkCount ? (l < 0 ? 0 : l) : chunkCount;
+    };
+    int chunk = modRanks(ringIx + n - 1);  // step 0: send own chunk
+    r.prim<Fn, false, true, true, false, UNROLL>(fn, in + off_of(chunk), nullptr, len_of(chunk), false);
+    for (int j = 2; j < n; ++j) {          // n-2 recv-reduce-send
+      chunk = modRanks(ringIx + n - j);
+      r.prim<Fn, true, true, true, false, UNROLL>(fn, in + off_of(chunk), nullptr, len_of(chunk), false);
+    }
+    chunk = ringIx;                         // final reduce: output + send
+    r.prim<Fn, true, true, true, true, UNROLL>(fn, in + off_of(chunk), out + off_of(chunk),
+                                               len_of(chunk), true);
+    for (int j = 1; j < n - 1; ++j) {      // n-2 recv-copy-send
+      chunk = modRanks(ringIx + n - j);
+      r.prim<Fn, true, true, false, true, UNROLL>(fn, nullptr, out + off_of(chunk), len_of(chunk), false);
+    }
+    chunk = modRanks(ringIx + 1);          // final recv
+    r.prim<Fn, true, false, false, true, UNROLL>(fn, nullptr, out + off_of(chunk), len_of(chunk), false);
+  }
+}
+
+// ------------------------------------------------------------- ReduceScatter
+// reduce_scatter.h:12-55: the chunk owned by rank ringRanks[k] starts at its
+// ring successor; the owner writes output[off] with postOp.
+template <class Fn, int UNROLL>
+__device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
+  using T = typename Fn::EltType;
+  const int n = w.nRanks;
+  const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
+  const int64_t count = (int64_t)w.count;
+  int64_t gridOff, chCount;
+  channel_part(count, w.nChannels, c, eltAlign, &gridOff, &chCount);
+  const T* in = (const T*)w.sendbuff;
+  T* out = (T*)w.recvbuff;
+  const int* ringRanks = r.ch->ringRanks;
+  const int64_t chunkCount = w.slotBytes / (int64_t)sizeof(T);
+  for (int64_t eo = 0; eo < chCount; eo += chunkCount) {
+    const int64_t nelem = chCount - eo < chunkCount ? chCount - eo : chunkCount;
+    const int64_t dataOff = gridOff + eo;
+    int rankDest = ringRanks[n - 1];
+    r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false);
+    for (int j = 2; j < n; ++j) {
+      rankDest = ringRanks[n - j];
+      r.prim<Fn, true, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false);
+    }
+    rankDest = ringRanks[0];
+    r.prim<Fn, true, false, true, true, UNROLL>(fn, in + dataOff + rankDest * count, out + dataOff,
+                                                nelem, true);
+  }
+}
+
+// ----------------------------------------------------------------- AllGather
+// all_gather.h:12-83: byte copies (enqueue.cc:2400-2404 rewrites AG as int8).
+template <int UNROLL>
+__device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
+  using Fn = FnCopy<uint8_t>;
+  const Fn fn(0);
+  const int n = w.nRanks;
+  const int64_t count = (int64_t)w.count;  // bytes per rank
+  int64_t partOff, partCount;
+  channel_part(count, w.nChannels, c, 16, &partOff, &partCount);
+  const uint8_t* in = (const uint8_t*)w.sendbuff;
+  uint8_t* out = (uint8_t*)w.recvbuff;
+  const int* ringRanks = r.ch->ringRanks;
+  const int64_t chunkCount = w.slotBytes;
+  for (int64_t eo = 0; eo < partCount; eo += chunkCount) {
+    const int64_t nelem = partCount - eo < chunkCount ? partCount - eo : chunkCount;
+    const int64_t dataOff = partOff + eo;
+    int rankDest = ringRanks[0];
+    int64_t off = dataOff + rankDest * count;
+    if (in + dataOff == out + off)
+      r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff, nullptr, nelem, false);
+    else
+      r.prim<Fn, false, true, true, true, UNROLL>(fn, in + dataOff, out + off, nelem, false);
+    for (int j = 1; j < n - 1; ++j) {
+      rankDest = ringRanks[n - j];
+      off = dataOff + rankDest * count;
+      r.prim<Fn, true, true, false, true, UNROLL>(fn, nullptr, out + off, nelem, false);
+    }
+    rankDest = ringRanks[1];
+    off = dataOff + rankDest * count;
+    r.prim<Fn, true, false, false, true, UNROLL>(fn, nullptr, out + off, nelem, false);
+  }
+}
+
+}  // namespace vccl

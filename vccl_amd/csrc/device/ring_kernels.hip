@@ -1,0 +1,70 @@
+// Ring collective kernels for ONE kernel element type (VCCL_KT): all-reduce
+// and reduce-scatter per reduction functor, plus (in the K_U8 unit) the
+// type-agnostic all-gather.  One workgroup per channel (enqueue.cc:1576-1666).
+#include <hip/hip_runtime.h>
+
+#include "dispatch.hpp"
+#include "ring.hpp"
+#include "ring_launch.hpp"
+
+#ifndef VCCL_KT
+#error "compile with -DVCCL_KT=<kernel element type>"
+#endif
+
+namespace vccl {
+
+template <int COLL, class Fn, int UNROLL>
+__global__ __launch_bounds__(1024) void k_ring(RingWork w) {
+  __shared__ int shAbort;
+  if (threadIdx.x == 0) shAbort = 0;
+  __syncthreads();
+  DevChannel* ch = &w.channels[blockIdx.x];
+  RingCtx r;
+  r.ch = ch;
+  r.comm = w.comm;
+  r.recvStep = ch->recvStep;
+  r.sendStep = ch->sendStep;
+  r.tid = threadIdx.x;
+  r.nthreads = blockDim.x;
+  r.slotBytes = w.slotBytes;
+  r.shAbort = &shAbort;
+  const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
+  if constexpr (COLL == kCollAllReduce) ring_allreduce<Fn, UNROLL>(r, fn, w, blockIdx.x);
+  else if constexpr (COLL == kCollReduceScatter) ring_reducescatter<Fn, UNROLL>(r, fn, w, blockIdx.x);
+  else ring_allgather<UNROLL>(r, w, blockIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ch->recvStep = r.recvStep;
+    ch->sendStep = r.sendStep;
+  }
+}
+
+template <>
+hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingWork& w, int nthreads,
+                                hipStream_t stream) {
+  using T = typename KTypeOf<VCCL_KT>::T;
+  hipError_t err = hipErrorInvalidValue;
+  dim3 grid(w.nChannels), block(nthreads);
+  if (coll == kCollAllGather) {
+    if constexpr (VCCL_KT == K_U8) {
+      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, kRingUnroll>), grid, block, 0,
+                         stream, w);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  dispatch_op<T>(devOp, [&]<class Fn>() {
+    if constexpr (std::is_same<Fn, FnCopy<T>>::value) {
+      err = hipErrorInvalidValue;
+    } else if (coll == kCollAllReduce) {
+      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, kRingUnroll>), grid, block, 0, stream, w);
+      err = hipGetLastError();
+    } else if (coll == kCollReduceScatter) {
+      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, kRingUnroll>), grid, block, 0, stream, w);
+      err = hipGetLastError();
+    }
+  });
+  return err;
+}
+
+}  // namespace vccl

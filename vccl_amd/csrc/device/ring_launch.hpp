@@ -1,0 +1,16 @@
+// Host-side declarations for the ring kernels (one specialisation per kernel
+// element type, compiled in parallel).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ring_types.hpp"
+
+namespace vccl {
+
+enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2 };
+constexpr int kRingUnroll = 4;
+
+template <int K>
+hipError_t ring_launch(int coll, int devOp, const RingWork& w, int nthreads, hipStream_t stream);
+
+}  // namespace vccl

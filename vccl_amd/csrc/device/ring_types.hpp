@@ -1,0 +1,68 @@
+// Host/device-shared layout of the ring transport (POD, no HIP types).
+//
+// Replaces ncclDevChannel / ncclConnInfo (src/include/device.h) with the
+// minimum the MI355X ring needs.  One channel = one workgroup = one ring
+// position with its own FIFO pair (reference: one block per channel,
+// enqueue.cc:1576-1666).  FIFOs follow the SIMPLE protocol of
+// prims_simple.h:108-181: kSteps slots, the sender waits for a free slot
+// (head + kSteps > step), the receiver waits for a posted slot (tail > step).
+//
+// Memory placement: every FIFO and flag lives in the
+// RECEIVER's HBM, allocated uncached (hipDeviceMallocUncached) so peer writes
+// over xGMI are never hidden behind a stale L2/L1 line; the sender writes the
+// slot payload remotely ("P2P write", as NCCL on NVLink, transport/p2p.cc:484-503).
+#pragma once
+#include <stdint.h>
+
+namespace vccl {
+
+constexpr int kSteps = 8;            // NCCL_STEPS (device.h:24)
+constexpr int kMaxRanks = 64;
+constexpr int kMaxChannels = 64;     // MAXCHANNELS (device.h:62)
+constexpr int kFlagStride = 128;     // bytes between flags (one line each)
+
+struct DevChannel {
+  // ring order: ringRanks[k] = rank at ring position (myPos + k) mod n
+  // (userRanks rotated to self, init.cc:599-615)
+  int ringRanks[kMaxRanks];
+  int ringPos;                       // my index in the ring (ring->index)
+  int pad0;
+  // receive side: data arrives in MY memory
+  char* recvFifo;                    // kSteps * slotBytes, local
+  uint64_t* recvTail;                // local flag, written by prev: slots posted
+  uint64_t* prevSendHead;            // prev's flag (remote): slots I consumed
+  // send side: data goes to NEXT's memory
+  char* sendFifo;                    // next's recvFifo (remote)
+  uint64_t* nextRecvTail;            // next's recvTail (remote)
+  uint64_t* sendHead;                // local flag, written by next
+  // persistent step counters (kernel reads at start, writes at end)
+  uint64_t recvStep;
+  uint64_t sendStep;
+};
+
+struct DevComm {
+  int rank, nRanks;
+  int nChannels;
+  int slotBytes;                     // bytes per FIFO slot
+  volatile int* abortFlag;           // host-pinned, mapped (ncclCommAbort)
+  int* errorFlag;                    // host-pinned, mapped: 1 = spin timeout
+  uint64_t spinTimeoutTicks;         // s_memrealtime ticks (100 MHz)
+};
+
+// Per-launch work descriptor (kernel argument, by value).
+struct RingWork {
+  DevComm* comm;                     // device-resident
+  DevChannel* channels;              // device-resident, nChannels entries
+  const void* sendbuff;
+  void* recvbuff;
+  uint64_t count;                    // AR: count; RS: recvcount; AG: bytes per rank
+  uint64_t redArg;                   // device op argument (also the preOp scalar)
+  const void* redArgPtr;             // ncclScalarDevice scalar (read on device)
+  int redArgBytes;
+  int preOp;                         // PreMulSum: scale own input
+  int nChannels;                     // channels used by this launch
+  int slotBytes;
+  int nRanks;
+};
+
+}  // namespace vccl

@@ -1,0 +1,115 @@
+// Internal host-side structures of libvccl (not part of the ABI).
+//
+// The communicator keeps only what the MI355X ring needs; its fields map to
+// the reference's ncclComm (src/include/comm.h) where one exists.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/nccl.h"
+#include "../device/ring_types.hpp"
+
+namespace vccl {
+
+// ----------------------------------------------------------------- logging
+// NCCL_DEBUG=WARN|INFO|TRACE (debug.h:22-34); VCCL_DEBUG is an alias.
+enum LogLevel { kLogNone = 0, kLogWarn = 1, kLogInfo = 2, kLogTrace = 3 };
+int log_level();
+void log_msg(int level, const char* file, int line, const char* fmt, ...)
+    __attribute__((format(printf, 4, 5)));
+#define VWARN(...) ::vccl::log_msg(::vccl::kLogWarn, __FILE__, __LINE__, __VA_ARGS__)
+#define VINFO(...)                                                                   \
+  do {                                                                               \
+    if (::vccl::log_level() >= ::vccl::kLogInfo)                                     \
+      ::vccl::log_msg(::vccl::kLogInfo, __FILE__, __LINE__, __VA_ARGS__);            \
+  } while (0)
+
+#define HIPCHECK(cmd)                                                                \
+  do {                                                                               \
+    hipError_t e_ = (cmd);                                                           \
+    if (e_ != hipSuccess) {                                                          \
+      VWARN("HIP failure '%s' in %s", hipGetErrorString(e_), #cmd);                 \
+      return ncclUnhandledCudaError;                                                 \
+    }                                                                                \
+  } while (0)
+#define NCCLCHECK(cmd)                                                               \
+  do {                                                                               \
+    ncclResult_t r_ = (cmd);                                                         \
+    if (r_ != ncclSuccess) return r_;                                                \
+  } while (0)
+
+// ----------------------------------------------------------------- params
+// NCCL_PARAM idiom (param.h:17-25): env NCCL_<name> (or VCCL_<name>), cached.
+int64_t param_int(const char* name, int64_t deflt);
+
+// ----------------------------------------------------------------- bootstrap
+struct Bootstrap;  // opaque (bootstrap.cc)
+ncclResult_t bootstrap_get_unique_id(ncclUniqueId* id);
+ncclResult_t bootstrap_init(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out);
+// allgather of `bytes` per rank: buf holds nranks*bytes, own slot filled in.
+ncclResult_t bootstrap_allgather(Bootstrap* b, void* buf, size_t bytes);
+ncclResult_t bootstrap_barrier(Bootstrap* b);
+void bootstrap_close(Bootstrap* b);
+
+// ----------------------------------------------------------------- rings
+// Ring orders for one node: for n in {2,4,8} the
+// arc-balanced ring sets over the fully connected xGMI mesh; otherwise the
+// identity ring.  Returns the list of rings (each a permutation of 0..n-1).
+std::vector<std::vector<int>> ring_orders(int nranks);
+
+// ----------------------------------------------------------------- comm
+struct PeerMap {               // what one rank published about itself
+  int pid;
+  int device;
+  uint64_t hostHash;
+  hipIpcMemHandle_t fifoHandle;
+  hipIpcMemHandle_t flagHandle;
+  char* fifoPtr;               // raw pointers (valid only in the owner process)
+  char* flagPtr;
+};
+
+struct UserRedOp {             // ncclRedOpCreatePreMulSum state (enqueue.cc:2528-2567)
+  int freeNext;                // -1 = allocated
+  ncclDataType_t datatype;
+  int devOp;
+  bool argIsPtr;
+  uint64_t arg;
+};
+
+}  // namespace vccl
+
+struct ncclComm {
+  uint64_t magic;
+  int rank = 0, nRanks = 1, device = 0;
+  int nChannels = 0, slotBytes = 0, nThreads = 0;
+  vccl::Bootstrap* bootstrap = nullptr;
+  // device resources
+  char* fifoBuf = nullptr;     // nChannels * kSteps * slotBytes, uncached
+  char* flagBuf = nullptr;     // nChannels * 2 flags * kFlagStride, uncached
+  vccl::DevComm* devComm = nullptr;
+  vccl::DevChannel* devChannels = nullptr;
+  volatile int* abortFlag = nullptr;  // host pinned, mapped
+  int* errorFlag = nullptr;           // host pinned, mapped
+  std::vector<void*> ipcOpened;       // peer mappings to close
+  std::vector<vccl::PeerMap> peers;
+  // ordering of launches on this comm across user streams
+  hipEvent_t lastLaunch = nullptr;
+  hipStream_t lastStream = nullptr;
+  // state
+  std::atomic<int> asyncError{0};
+  std::vector<vccl::UserRedOp> userOps;
+  int userOpFreeHead = 0;
+  uint64_t opCount = 0;
+  bool destroyed = false;
+};
+
+namespace vccl {
+constexpr uint64_t kCommMagic = 0x76636363'6c6d6933ull;  // "vccclmi3"
+ncclResult_t comm_check(const ncclComm* comm, const char* api);
+}  // namespace vccl

@@ -1,0 +1,64 @@
+// Logging and environment parameters.
+// Reference idioms: NCCL_DEBUG / ncclDebugLog (src/debug.cc, include/debug.h:22-34)
+// and NCCL_PARAM (include/param.h:17-25, misc/param.cc:52-98).
+#include <cstdarg>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <unistd.h>
+
+#include "core.h"
+
+namespace vccl {
+
+static int parse_level(const char* s) {
+  if (!s) return kLogWarn;
+  if (!strcasecmp(s, "VERSION") || !strcasecmp(s, "WARN")) return kLogWarn;
+  if (!strcasecmp(s, "INFO")) return kLogInfo;
+  if (!strcasecmp(s, "TRACE")) return kLogTrace;
+  if (!strcasecmp(s, "NONE")) return kLogNone;
+  return kLogWarn;
+}
+
+int log_level() {
+  static int level = [] {
+    const char* s = getenv("VCCL_DEBUG");
+    if (!s) s = getenv("NCCL_DEBUG");
+    return parse_level(s);
+  }();
+  return level;
+}
+
+void log_msg(int level, const char* file, int line, const char* fmt, ...) {
+  if (log_level() < level) return;
+  static std::mutex mu;
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  const char* base = strrchr(file, '/');
+  std::lock_guard<std::mutex> lk(mu);
+  fprintf(stderr, "[vccl %d] %s %s:%d %s\n", (int)getpid(), level == kLogWarn ? "WARN" : "INFO",
+          base ? base + 1 : file, line, buf);
+}
+
+int64_t param_int(const char* name, int64_t deflt) {
+  char key[128];
+  snprintf(key, sizeof(key), "VCCL_%s", name);
+  const char* s = getenv(key);
+  if (!s) {
+    snprintf(key, sizeof(key), "NCCL_%s", name);
+    s = getenv(key);
+  }
+  if (!s || !*s) return deflt;
+  char* end = nullptr;
+  long long v = strtoll(s, &end, 0);
+  if (end == s) {
+    VWARN("invalid value '%s' for %s, using %lld", s, key, (long long)deflt);
+    return deflt;
+  }
+  return v;
+}
+
+}  // namespace vccl

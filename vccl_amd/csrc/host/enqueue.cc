@@ -1,0 +1,418 @@
+// Collective API -> argument check -> op encoding -> task -> launch.
+//
+// Keeps the observable semantics of the reference's dispatch surface
+// (collectives.cc:77-158 -> ncclEnqueueCheck enqueue.cc:2448-2525 -> ArgsCheck
+// misc/argcheck.cc:45-86 -> taskAppend enqueue.cc:2315-2442 with
+// hostToDevRedOp :2217-2310 and the nRanks==1 shortcut ncclLaunchOneRank
+// onerank.cu:47-83), re-implemented for one node: the planner has a single
+// algorithm (ring / SIMPLE over xGMI), so "planning" is the channel partition
+// done on the device (ring.hpp channel_part).  Group semantics
+// (group.cc:92-110, :393-506): calls between ncclGroupStart/End are queued
+// per thread and launched, in call order, at the outermost ncclGroupEnd.
+#include <cstring>
+#include <vector>
+
+#include "../../../include/vccl_device.h"
+#include "../device/dispatch.hpp"
+#include "../device/launch.hpp"
+#include "../device/ring_launch.hpp"
+#include "core.h"
+
+namespace vccl {
+
+enum Coll { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2 };
+
+struct Task {
+  int coll;
+  const void* sendbuff;
+  void* recvbuff;
+  size_t count;
+  ncclDataType_t datatype;
+  int devOp;
+  uint64_t arg;
+  const void* argPtr;  // ncclScalarDevice PreMulSum scalar
+  ncclComm* comm;
+  hipStream_t stream;
+};
+
+static thread_local int tl_groupDepth = 0;
+static thread_local std::vector<Task> tl_tasks;
+static thread_local ncclResult_t tl_groupError = ncclSuccess;
+
+static int type_size(ncclDataType_t t) {
+  switch (t) {
+    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return -1;
+  }
+}
+
+// hostToDevRedOp (enqueue.cc:2217-2310) for built-in ops.
+static ncclResult_t host_to_dev_redop(ncclRedOp_t op, ncclDataType_t dt, int nRanks, int* devOp,
+                                      uint64_t* arg) {
+  const int nbits = 8 * type_size(dt);
+  if (nbits <= 0) return ncclInvalidArgument;
+  const uint64_t allBits = ~0ull >> (64 - nbits);
+  const uint64_t signBit = allBits ^ (allBits >> 1);
+  const bool isSigned = dt == ncclInt8 || dt == ncclInt32 || dt == ncclInt64;
+  *arg = 0;
+  switch ((int)op) {
+    case ncclSum: *devOp = OP_SUM; return ncclSuccess;
+    case ncclProd: *devOp = OP_PROD; return ncclSuccess;
+    case ncclMin:
+    case ncclMax:
+      *devOp = OP_MINMAX;
+      if (isSigned) *arg ^= signBit;
+      if (op == ncclMax) *arg ^= allBits;
+      return ncclSuccess;
+    case ncclAvg:
+      switch ((int)dt) {
+        case ncclInt8: case ncclInt32: case ncclInt64:
+        case ncclUint8: case ncclUint32: case ncclUint64:
+          *devOp = OP_SUMPOSTDIV;
+          *arg = ((uint64_t)nRanks << 1) | (isSigned ? 1 : 0);
+          return ncclSuccess;
+        case ncclFloat16: {
+          *devOp = OP_PREMULSUM;
+          _Float16 h = (_Float16)(float)(1.0 / nRanks);
+          uint16_t b;
+          memcpy(&b, &h, 2);
+          *arg = b;
+          return ncclSuccess;
+        }
+        case ncclBfloat16: {
+          *devOp = OP_PREMULSUM;
+          __bf16 h = (__bf16)(float)(1.0 / nRanks);
+          uint16_t b;
+          memcpy(&b, &h, 2);
+          *arg = b;
+          return ncclSuccess;
+        }
+        case ncclFloat32: {
+          *devOp = OP_PREMULSUM;
+          float f = (float)(1.0 / nRanks);
+          uint32_t b;
+          memcpy(&b, &f, 4);
+          *arg = b;
+          return ncclSuccess;
+        }
+        case ncclFloat64: {
+          *devOp = OP_PREMULSUM;
+          double d = 1.0 / nRanks;
+          memcpy(arg, &d, 8);
+          return ncclSuccess;
+        }
+      }
+      return ncclInvalidArgument;
+  }
+  return ncclInvalidArgument;
+}
+
+static ncclResult_t resolve_op(ncclComm* comm, ncclRedOp_t op, ncclDataType_t dt, int* devOp,
+                               uint64_t* arg, const void** argPtr) {
+  *argPtr = nullptr;
+  if ((int)op < (int)ncclNumOps) return host_to_dev_redop(op, dt, comm->nRanks, devOp, arg);
+  const int ix = (int)op - (int)ncclNumOps;
+  if (ix >= (int)comm->userOps.size() || comm->userOps[ix].freeNext != -1) return ncclInvalidArgument;
+  const UserRedOp& u = comm->userOps[ix];
+  if (u.datatype != dt) {  // enqueue.cc:2301-2305
+    VWARN("Data type supplied to user-created ncclRedOp_t does not match type given to reduction operation");
+    return ncclInvalidArgument;
+  }
+  *devOp = u.devOp;
+  *arg = u.argIsPtr ? 0 : u.arg;
+  if (u.argIsPtr) *argPtr = (const void*)u.arg;
+  return ncclSuccess;
+}
+
+// ArgsCheck (misc/argcheck.cc:45-86) minus the root check (no rooted colls).
+static ncclResult_t args_check(ncclComm* comm, const char* name, ncclDataType_t dt, ncclRedOp_t op,
+                               bool hasOp) {
+  if ((int)dt < 0 || (int)dt >= (int)ncclNumTypes) {
+    VWARN("%s : invalid type %d", name, (int)dt);
+    return ncclInvalidArgument;
+  }
+  if (hasOp) {
+    if ((int)op < 0 || (int)op > (int)ncclMaxRedOp) {
+      VWARN("%s : invalid reduction operation %d", name, (int)op);
+      return ncclInvalidArgument;
+    }
+    const int ix = (int)op - (int)ncclNumOps;
+    if (ix >= 0 && (ix >= (int)comm->userOps.size() || comm->userOps[ix].freeNext != -1)) {
+      VWARN("%s : reduction operation %d unknown to this communicator", name, (int)op);
+      return ncclInvalidArgument;
+    }
+  }
+  if (dt == ncclFloat8e4m3 || dt == ncclFloat8e5m2) {  // enqueue.cc:2379-2384
+    VWARN("%s : fp8 reductions are not built in this release", name);
+    return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
+// Order launches of one comm across different user streams (the reference
+// serialises through its internal strong stream, enqueue.cc:1445-1548).
+static ncclResult_t stream_order(ncclComm* comm, hipStream_t s) {
+  if (comm->lastStream != nullptr && comm->lastStream != s)
+    HIPCHECK(hipStreamWaitEvent(s, comm->lastLaunch, 0));
+  return ncclSuccess;
+}
+static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s) {
+  HIPCHECK(hipEventRecord(comm->lastLaunch, s));
+  comm->lastStream = s;
+  return ncclSuccess;
+}
+
+// ncclLaunchOneRank (onerank.cu:47-83): a copy, or the PreMulSum kernel.
+static ncclResult_t launch_one_rank(const Task& t) {
+  const size_t bytes = t.count * (size_t)type_size(t.datatype);
+  if (t.devOp != OP_PREMULSUM) {
+    if (t.recvbuff != t.sendbuff)
+      HIPCHECK(hipMemcpyAsync(t.recvbuff, t.sendbuff, bytes, hipMemcpyDeviceToDevice, t.stream));
+    return ncclSuccess;
+  }
+  RCArgs a = {};
+  a.srcs[0] = (const char*)t.sendbuff;
+  a.dsts[0] = (char*)t.recvbuff;
+  a.nSrcs = a.nDsts = 1;
+  a.preOpSrcs = 1;  // onerank.cu:43: PreOpSrcs=1, postOp=true
+  a.postOp = 1;
+  a.argPtr = t.argPtr;
+  hipError_t e = reduce_copy_launch(t.devOp, (int)t.datatype, t.arg, a, (int64_t)t.count, nullptr,
+                                    t.stream);
+  return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+}
+
+static ncclResult_t launch_ring(const Task& t) {
+  ncclComm* comm = t.comm;
+  RingWork w{};
+  w.comm = comm->devComm;
+  w.channels = comm->devChannels;
+  w.sendbuff = t.sendbuff;
+  w.recvbuff = t.recvbuff;
+  w.redArg = t.arg;
+  w.preOp = t.devOp == OP_PREMULSUM;
+  w.nChannels = comm->nChannels;
+  w.slotBytes = comm->slotBytes;
+  w.nRanks = comm->nRanks;
+  int kt, devOp = t.devOp;
+  if (t.coll == kAllGather) {
+    w.count = t.count * (uint64_t)type_size(t.datatype);  // bytes (enqueue.cc:2400-2404)
+    kt = K_U8;
+    devOp = OP_COPY;
+  } else {
+    w.count = t.count;
+    kt = kernel_type_of(t.devOp, (int)t.datatype);
+    if (kt < 0) return ncclInvalidArgument;
+  }
+  w.redArgPtr = t.argPtr;  // ncclScalarDevice: dereferenced by the kernel (nccl.h.in:255-262)
+  w.redArgBytes = type_size(t.datatype);
+  const int coll = t.coll == kAllReduce ? kCollAllReduce
+                   : t.coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
+  hipError_t e = hipErrorInvalidValue;
+  switch (kt) {
+    case K_U8: e = ring_launch<K_U8>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_U32: e = ring_launch<K_U32>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_U64: e = ring_launch<K_U64>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_F16: e = ring_launch<K_F16>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_F32: e = ring_launch<K_F32>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_F64: e = ring_launch<K_F64>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_BF16: e = ring_launch<K_BF16>(coll, devOp, w, comm->nThreads, t.stream); break;
+  }
+  if (e != hipSuccess) {
+    VWARN("ring kernel launch failed: %s", hipGetErrorString(e));
+    return ncclUnhandledCudaError;
+  }
+  return ncclSuccess;
+}
+
+static ncclResult_t launch_task(const Task& t) {
+  int old = -1;
+  HIPCHECK(hipGetDevice(&old));
+  if (old != t.comm->device) HIPCHECK(hipSetDevice(t.comm->device));
+  ncclResult_t r = stream_order(t.comm, t.stream);
+  if (r == ncclSuccess) {
+    if (t.comm->nRanks == 1 && t.coll == kAllGather) {
+      if (t.recvbuff != t.sendbuff) {
+        hipError_t e = hipMemcpyAsync(t.recvbuff, t.sendbuff,
+                                      t.count * (size_t)type_size(t.datatype),
+                                      hipMemcpyDeviceToDevice, t.stream);
+        r = e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+      }
+    } else if (t.comm->nRanks == 1) {
+      r = launch_one_rank(t);
+    } else {
+      r = launch_ring(t);
+    }
+  }
+  if (r == ncclSuccess) r = stream_mark(t.comm, t.stream);
+  t.comm->opCount++;
+  if (old != t.comm->device) (void)hipSetDevice(old);
+  return r;
+}
+
+static ncclResult_t enqueue_check(int coll, const char* name, const void* sendbuff, void* recvbuff,
+                                  size_t count, ncclDataType_t dt, ncclRedOp_t op, ncclComm* comm,
+                                  hipStream_t stream) {
+  NCCLCHECK(comm_check(comm, name));
+  NCCLCHECK(args_check(comm, name, dt, op, coll != kAllGather));
+  VINFO("%s: opCount %lx sendbuff %p recvbuff %p count %zu datatype %d op %d comm %p [nranks=%d] stream %p",
+        name, (unsigned long)comm->opCount, sendbuff, recvbuff, count, (int)dt, (int)op,
+        (void*)comm, comm->nRanks, (void*)stream);
+  if (count == 0) return ncclSuccess;  // enqueue.cc:2372
+  if (!sendbuff || !recvbuff) {
+    VWARN("%s : NULL buffer", name);
+    return ncclInvalidArgument;
+  }
+  Task t{};
+  t.coll = coll;
+  t.sendbuff = sendbuff;
+  t.recvbuff = recvbuff;
+  t.count = count;
+  t.datatype = dt;
+  t.comm = comm;
+  t.stream = stream;
+  if (coll != kAllGather) NCCLCHECK(resolve_op(comm, op, dt, &t.devOp, &t.arg, &t.argPtr));
+  else t.devOp = OP_COPY;
+  if (*(volatile int*)comm->errorFlag) {
+    comm->asyncError = ncclRemoteError;
+    return ncclRemoteError;
+  }
+  if (tl_groupDepth > 0) {
+    tl_tasks.push_back(t);
+    return ncclSuccess;
+  }
+  return launch_task(t);
+}
+
+}  // namespace vccl
+
+using namespace vccl;
+
+#define VCCL_EXPORT extern "C" __attribute__((visibility("default")))
+#define VCCL_ALIAS(name) __attribute__((alias(#name), visibility("default")))
+
+VCCL_EXPORT ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count,
+                                       ncclDataType_t datatype, ncclRedOp_t op, ncclComm_t comm,
+                                       hipStream_t stream) {
+  return enqueue_check(kAllReduce, "AllReduce", sendbuff, recvbuff, count, datatype, op, comm,
+                       stream);
+}
+
+VCCL_EXPORT ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recvcount,
+                                           ncclDataType_t datatype, ncclRedOp_t op,
+                                           ncclComm_t comm, hipStream_t stream) {
+  return enqueue_check(kReduceScatter, "ReduceScatter", sendbuff, recvbuff, recvcount, datatype,
+                       op, comm, stream);
+}
+
+VCCL_EXPORT ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount,
+                                       ncclDataType_t datatype, ncclComm_t comm,
+                                       hipStream_t stream) {
+  return enqueue_check(kAllGather, "AllGather", sendbuff, recvbuff, sendcount, datatype, ncclSum,
+                       comm, stream);
+}
+
+VCCL_EXPORT ncclResult_t ncclGroupStart(void) {
+  tl_groupDepth++;
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t ncclGroupEnd(void) {
+  if (tl_groupDepth == 0) {
+    VWARN("ncclGroupEnd: not in a group call.");
+    return ncclInvalidUsage;
+  }
+  if (--tl_groupDepth > 0) return ncclSuccess;
+  ncclResult_t ret = tl_groupError;
+  std::vector<Task> tasks;
+  tasks.swap(tl_tasks);
+  for (const Task& t : tasks) {
+    ncclResult_t r = launch_task(t);
+    if (ret == ncclSuccess) ret = r;
+  }
+  tl_groupError = ncclSuccess;
+  return ret;
+}
+
+VCCL_EXPORT ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar,
+                                                  ncclDataType_t datatype,
+                                                  ncclScalarResidence_t residence,
+                                                  ncclComm_t comm) {
+  NCCLCHECK(comm_check(comm, "ncclRedOpCreatePreMulSum"));
+  if (!op || !scalar) return ncclInvalidArgument;
+  const int sz = type_size(datatype);
+  if (sz < 1 || datatype == ncclFloat8e4m3 || datatype == ncclFloat8e5m2) return ncclInvalidArgument;
+  int ix = -1;
+  for (int i = 0; i < (int)comm->userOps.size(); i++)
+    if (comm->userOps[i].freeNext != -1) { ix = i; break; }
+  if (ix < 0) {
+    comm->userOps.push_back(UserRedOp{});
+    ix = (int)comm->userOps.size() - 1;
+  }
+  UserRedOp& u = comm->userOps[ix];
+  u.freeNext = -1;
+  u.datatype = datatype;
+  u.devOp = OP_PREMULSUM;
+  if (residence == ncclScalarHostImmediate) {
+    u.argIsPtr = false;
+    u.arg = 0;
+    memcpy(&u.arg, scalar, (size_t)sz);
+  } else {
+    u.argIsPtr = true;
+    u.arg = (uint64_t)(uintptr_t)scalar;
+  }
+  *op = (ncclRedOp_t)((int)ncclNumOps + ix);
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t ncclRedOpDestroy(ncclRedOp_t op, ncclComm_t comm) {
+  if (0 <= (int)op && (int)op < (int)ncclNumOps) {
+    VWARN("ncclRedOpDestroy : operator is a NCCL builtin.");
+    return ncclInvalidArgument;
+  }
+  if ((int)op < 0) {
+    VWARN("ncclRedOpDestroy :  operator is garbage.");
+    return ncclInvalidArgument;
+  }
+  if (comm == nullptr) {
+    VWARN("ncclRedOpDestroy : invalid communicator passed.");
+    return ncclInvalidArgument;
+  }
+  NCCLCHECK(comm_check(comm, "ncclRedOpDestroy"));
+  const int ix = (int)op - (int)ncclNumOps;
+  if (ix >= (int)comm->userOps.size() || comm->userOps[ix].freeNext != -1) {
+    VWARN("ncclRedOpDestroy : operator unknown to this communicator.");
+    return ncclInvalidArgument;
+  }
+  comm->userOps[ix].freeNext = 0;  // free
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t vcclHostToDevRedOp(ncclRedOp_t op, ncclDataType_t datatype, int nRanks,
+                                            int* devOp, uint64_t* opArg) {
+  if (!devOp || !opArg || nRanks < 1) return ncclInvalidArgument;
+  if ((int)datatype < 0 || (int)datatype >= (int)ncclNumTypes) return ncclInvalidArgument;
+  return host_to_dev_redop(op, datatype, nRanks, devOp, opArg);
+}
+
+VCCL_EXPORT const char* vcclBuildInfo(void) {
+  return "vccl-mi355x " __DATE__ " gfx950; ring SIMPLE over xGMI (uncached receiver FIFOs); "
+         "reduce-copy 16B packs";
+}
+
+extern "C" {
+ncclResult_t pncclAllReduce(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) VCCL_ALIAS(ncclAllReduce);
+ncclResult_t pncclReduceScatter(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t,
+                                ncclComm_t, hipStream_t) VCCL_ALIAS(ncclReduceScatter);
+ncclResult_t pncclAllGather(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t)
+    VCCL_ALIAS(ncclAllGather);
+ncclResult_t pncclGroupStart(void) VCCL_ALIAS(ncclGroupStart);
+ncclResult_t pncclGroupEnd(void) VCCL_ALIAS(ncclGroupEnd);
+ncclResult_t pncclRedOpCreatePreMulSum(ncclRedOp_t*, void*, ncclDataType_t, ncclScalarResidence_t,
+                                       ncclComm_t) VCCL_ALIAS(ncclRedOpCreatePreMulSum);
+ncclResult_t pncclRedOpDestroy(ncclRedOp_t, ncclComm_t) VCCL_ALIAS(ncclRedOpDestroy);
+}

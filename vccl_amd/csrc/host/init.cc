@@ -1,0 +1,424 @@
+// Communicator lifecycle: unique id, init (rank / all), destroy, abort, queries.
+//
+// Reference: src/init.cc (ncclCommInitRankDev :1651-1730, ncclCommInitAll
+// :1750-1814, initTransportsRank :672-1276, setupChannel :599-615) and the
+// P2P transport (src/transport/p2p.cc:209-560).  MI355X design: no topology
+// search — one node, fully connected xGMI mesh, fixed arc-balanced ring sets
+// (SURVEY.md Appendix D); each channel's FIFO and flags live in the receiver's
+// HBM (uncached) and are mapped into the sender by hipIpc* (multi-process) or
+// peer access (single process).
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+
+#include "core.h"
+
+namespace vccl {
+
+ncclResult_t comm_check(const ncclComm* comm, const char* api) {
+  if (comm == nullptr) {
+    VWARN("%s : comm argument is NULL", api);
+    return ncclInvalidArgument;
+  }
+  if (comm->magic != kCommMagic || comm->destroyed) {
+    VWARN("%s : comm argument is invalid or destroyed", api);
+    return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
+// SURVEY.md Appendix D (exhaustive search, verified by tests/test_rings.py):
+// 8 GPUs: 7 arc-disjoint directed Hamiltonian cycles (every xGMI link used by
+// exactly one ring per direction); 4 GPUs: all 6 directed Hamiltonian cycles
+// (every arc in exactly 2); 2 GPUs: the single ring.
+std::vector<std::vector<int>> ring_orders(int n) {
+  if (n == 8)
+    return {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 2, 1, 3, 5, 4, 7, 6}, {0, 3, 1, 4, 6, 2, 7, 5},
+            {0, 4, 1, 5, 7, 2, 6, 3}, {0, 5, 3, 6, 1, 7, 4, 2}, {0, 6, 5, 2, 4, 3, 7, 1},
+            {0, 7, 3, 2, 5, 1, 6, 4}};
+  if (n == 4)
+    return {{0, 1, 2, 3}, {0, 1, 3, 2}, {0, 2, 1, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {0, 3, 2, 1}};
+  std::vector<int> id(n);
+  for (int i = 0; i < n; i++) id[i] = i;
+  return {id};
+}
+
+static uint64_t host_hash() {
+  char name[256] = {0};
+  gethostname(name, sizeof(name) - 1);
+  uint64_t h = 1469598103934665603ull;
+  for (char* p = name; *p; p++) h = (h ^ (uint8_t)*p) * 1099511628211ull;
+  return h;
+}
+
+static ncclResult_t alloc_uncached(void** p, size_t bytes) {
+  // NCCL_FIFO_ALLOC: 0 = uncached (default), 1 = fine-grained, 2 = coarse (hipMalloc)
+  int mode = (int)param_int("FIFO_ALLOC", 0);
+  hipError_t e;
+  if (mode == 2) e = hipMalloc(p, bytes);
+  else e = hipExtMallocWithFlags(p, bytes, mode == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached);
+  if (e != hipSuccess) {
+    VWARN("FIFO allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
+    return ncclUnhandledCudaError;
+  }
+  return ncclSuccess;
+}
+
+static void free_resources(ncclComm* c) {
+  for (void* p : c->ipcOpened) (void)hipIpcCloseMemHandle(p);
+  c->ipcOpened.clear();
+  if (c->fifoBuf) (void)hipFree(c->fifoBuf);
+  if (c->flagBuf) (void)hipFree(c->flagBuf);
+  if (c->devComm) (void)hipFree(c->devComm);
+  if (c->devChannels) (void)hipFree(c->devChannels);
+  if (c->abortFlag) (void)hipHostFree((void*)c->abortFlag);
+  if (c->errorFlag) (void)hipHostFree(c->errorFlag);
+  if (c->lastLaunch) (void)hipEventDestroy(c->lastLaunch);
+  c->fifoBuf = c->flagBuf = nullptr;
+  c->devComm = nullptr;
+  c->devChannels = nullptr;
+  c->abortFlag = nullptr;
+  c->errorFlag = nullptr;
+  c->lastLaunch = nullptr;
+}
+
+// Map a peer's buffer into this process/device.
+static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, bool fifo,
+                             char** out) {
+  char* raw = fifo ? p.fifoPtr : p.flagPtr;
+  if (p.pid == me.pid && p.hostHash == me.hostHash) {
+    if (p.device != c->device) {
+      hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        VWARN("hipDeviceEnablePeerAccess(%d -> %d) failed: %s", c->device, p.device,
+              hipGetErrorString(e));
+        return ncclUnhandledCudaError;
+      }
+      (void)hipGetLastError();
+    }
+    *out = raw;
+    return ncclSuccess;
+  }
+  void* ptr = nullptr;
+  hipError_t e = hipIpcOpenMemHandle(&ptr, fifo ? p.fifoHandle : p.flagHandle,
+                                     hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) {
+    VWARN("hipIpcOpenMemHandle failed: %s", hipGetErrorString(e));
+    return ncclUnhandledCudaError;
+  }
+  c->ipcOpened.push_back(ptr);
+  *out = (char*)ptr;
+  return ncclSuccess;
+}
+
+static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
+  NCCLCHECK(bootstrap_init(id, c->rank, c->nRanks, &c->bootstrap));
+  const int n = c->nRanks;
+  const auto rings = ring_orders(n);
+  const int nRings = (int)rings.size();
+  // Channel count: NCCL_NCHANNELS total, else VCCL_CHANNELS_PER_RING x rings.
+  int perRing = (int)param_int("CHANNELS_PER_RING", n == 8 ? 4 : (n == 4 ? 4 : 16));
+  int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
+  nch = std::max(1, std::min(nch, kMaxChannels));
+  c->nChannels = n > 1 ? nch : 0;
+  c->slotBytes = (int)param_int("SLOT_BYTES", 256 << 10);
+  if (c->slotBytes < 4096 || c->slotBytes % 4096) {
+    VWARN("NCCL_SLOT_BYTES must be a multiple of 4096, using 262144");
+    c->slotBytes = 256 << 10;
+  }
+  c->nThreads = (int)param_int("NTHREADS", 512);
+  if (c->nThreads != 256 && c->nThreads != 512 && c->nThreads != 1024) c->nThreads = 512;
+
+  HIPCHECK(hipHostMalloc((void**)&c->abortFlag, sizeof(int), hipHostMallocMapped));
+  HIPCHECK(hipHostMalloc((void**)&c->errorFlag, sizeof(int), hipHostMallocMapped));
+  *c->abortFlag = 0;
+  *c->errorFlag = 0;
+  HIPCHECK(hipEventCreateWithFlags(&c->lastLaunch, hipEventDisableTiming));
+
+  PeerMap me{};
+  me.pid = (int)getpid();
+  me.device = c->device;
+  me.hostHash = host_hash();
+  if (n > 1) {
+    const size_t fifoBytes = (size_t)c->nChannels * kSteps * c->slotBytes;
+    const size_t flagBytes = (size_t)c->nChannels * 2 * kFlagStride;
+    NCCLCHECK(alloc_uncached((void**)&c->fifoBuf, fifoBytes));
+    NCCLCHECK(alloc_uncached((void**)&c->flagBuf, flagBytes));
+    HIPCHECK(hipMemset(c->flagBuf, 0, flagBytes));
+    HIPCHECK(hipIpcGetMemHandle(&me.fifoHandle, c->fifoBuf));
+    HIPCHECK(hipIpcGetMemHandle(&me.flagHandle, c->flagBuf));
+    me.fifoPtr = c->fifoBuf;
+    me.flagPtr = c->flagBuf;
+  }
+  c->peers.assign(n, PeerMap{});
+  c->peers[c->rank] = me;
+  NCCLCHECK(bootstrap_allgather(c->bootstrap, c->peers.data(), sizeof(PeerMap)));
+  for (int r = 0; r < n; r++) {
+    if (c->peers[r].hostHash != me.hostHash) {
+      VWARN("rank %d is on another node: inter-node transport is out of scope", r);
+      return ncclInvalidUsage;
+    }
+  }
+
+  DevComm dc{};
+  dc.rank = c->rank;
+  dc.nRanks = n;
+  dc.nChannels = c->nChannels;
+  dc.slotBytes = c->slotBytes;
+  HIPCHECK(hipHostGetDevicePointer((void**)&dc.abortFlag, (void*)c->abortFlag, 0));
+  HIPCHECK(hipHostGetDevicePointer((void**)&dc.errorFlag, c->errorFlag, 0));
+  dc.spinTimeoutTicks = (uint64_t)param_int("SPIN_TIMEOUT_S", 60) * 100000000ull;
+  HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
+  HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));
+
+  if (n > 1) {
+    std::vector<char*> fifoOf(n), flagOf(n);
+    for (int r = 0; r < n; r++) {
+      if (r == c->rank) {
+        fifoOf[r] = c->fifoBuf;
+        flagOf[r] = c->flagBuf;
+        continue;
+      }
+      NCCLCHECK(map_peer(c, me, c->peers[r], true, &fifoOf[r]));
+      NCCLCHECK(map_peer(c, me, c->peers[r], false, &flagOf[r]));
+    }
+    std::vector<DevChannel> chans(c->nChannels);
+    const size_t fifoPerCh = (size_t)kSteps * c->slotBytes;
+    for (int ch = 0; ch < c->nChannels; ch++) {
+      const auto& ring = rings[ch % nRings];
+      int pos = (int)(std::find(ring.begin(), ring.end(), c->rank) - ring.begin());
+      int next = ring[(pos + 1) % n], prev = ring[(pos + n - 1) % n];
+      DevChannel& d = chans[ch];
+      memset(&d, 0, sizeof(d));
+      for (int k = 0; k < n; k++) d.ringRanks[k] = ring[(pos + k) % n];
+      d.ringPos = pos;
+      auto flag = [&](int r, int which) {
+        return (uint64_t*)(flagOf[r] + ((size_t)ch * 2 + which) * kFlagStride);
+      };
+      d.recvFifo = c->fifoBuf + ch * fifoPerCh;
+      d.recvTail = flag(c->rank, 0);
+      d.prevSendHead = flag(prev, 1);
+      d.sendFifo = fifoOf[next] + ch * fifoPerCh;
+      d.nextRecvTail = flag(next, 0);
+      d.sendHead = flag(c->rank, 1);
+      d.recvStep = d.sendStep = 0;
+    }
+    HIPCHECK(hipMalloc((void**)&c->devChannels, sizeof(DevChannel) * c->nChannels));
+    HIPCHECK(hipMemcpy(c->devChannels, chans.data(), sizeof(DevChannel) * c->nChannels,
+                       hipMemcpyHostToDevice));
+  }
+  NCCLCHECK(bootstrap_barrier(c->bootstrap));
+  VINFO("comm %p rank %d/%d dev %d: %d channels x %d threads, slot %d B", (void*)c, c->rank, n,
+        c->device, c->nChannels, c->nThreads, c->slotBytes);
+  return ncclSuccess;
+}
+
+ncclResult_t comm_init_rank(ncclComm_t* out, int nranks, const ncclUniqueId* id, int rank,
+                            int device) {
+  if (!out) return ncclInvalidArgument;
+  *out = nullptr;
+  if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) {
+    VWARN("ncclCommInitRank : invalid rank %d / nranks %d", rank, nranks);
+    return ncclInvalidArgument;
+  }
+  auto* c = new ncclComm();
+  c->magic = kCommMagic;
+  c->rank = rank;
+  c->nRanks = nranks;
+  c->device = device;
+  c->userOpFreeHead = 0;
+  ncclResult_t r = init_rank(c, id);
+  if (r != ncclSuccess) {
+    free_resources(c);
+    bootstrap_close(c->bootstrap);
+    c->magic = 0;
+    delete c;
+    return r;
+  }
+  *out = c;
+  return ncclSuccess;
+}
+
+ncclResult_t comm_destroy(ncclComm* c, bool abort) {
+  int old = -1;
+  (void)hipGetDevice(&old);
+  (void)hipSetDevice(c->device);
+  if (abort && c->abortFlag) *c->abortFlag = 1;
+  (void)hipDeviceSynchronize();
+  // Peers may still be reading our FIFOs until they finish: rendezvous first.
+  if (!abort && c->bootstrap && c->nRanks > 1) (void)bootstrap_barrier(c->bootstrap);
+  free_resources(c);
+  bootstrap_close(c->bootstrap);
+  c->bootstrap = nullptr;
+  c->destroyed = true;
+  c->magic = 0;
+  if (old >= 0) (void)hipSetDevice(old);
+  delete c;
+  return ncclSuccess;
+}
+
+}  // namespace vccl
+
+using namespace vccl;
+
+#define VCCL_EXPORT extern "C" __attribute__((visibility("default")))
+#define VCCL_ALIAS(name) __attribute__((alias(#name), visibility("default")))
+
+VCCL_EXPORT ncclResult_t ncclGetVersion(int* version) {
+  if (!version) return ncclInvalidArgument;
+  *version = NCCL_VERSION_CODE;
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t ncclGetUniqueId(ncclUniqueId* uniqueId) {
+  return bootstrap_get_unique_id(uniqueId);
+}
+
+VCCL_EXPORT ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
+                                          int rank) {
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  return comm_init_rank(comm, nranks, &commId, rank, dev);
+}
+
+VCCL_EXPORT ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks,
+                                                ncclUniqueId commId, int rank,
+                                                ncclConfig_t* config) {
+  if (config) {
+    if (config->magic != 0xcafebeef) {
+      VWARN("ncclCommInitRankConfig: config not initialised with NCCL_CONFIG_INITIALIZER");
+      return ncclInvalidArgument;
+    }
+    if (config->blocking != NCCL_CONFIG_UNDEF_INT && config->blocking == 0)
+      VINFO("non-blocking comm requested: this build always initialises blocking");
+  }
+  return ncclCommInitRank(comm, nranks, commId, rank);
+}
+
+VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
+  if (!comms || ndev < 1) return ncclInvalidArgument;
+  int ndevices = 0;
+  HIPCHECK(hipGetDeviceCount(&ndevices));
+  for (int i = 0; i < ndev; i++) {
+    int d = devlist ? devlist[i] : i;
+    if (d < 0 || d >= ndevices) {
+      VWARN("ncclCommInitAll : invalid device %d", d);
+      return ncclInvalidArgument;
+    }
+  }
+  ncclUniqueId id;
+  NCCLCHECK(bootstrap_get_unique_id(&id));
+  std::vector<ncclResult_t> res(ndev, ncclSuccess);
+  std::vector<std::thread> th;
+  for (int i = 0; i < ndev; i++) {
+    th.emplace_back([&, i] {
+      int d = devlist ? devlist[i] : i;
+      if (hipSetDevice(d) != hipSuccess) {
+        res[i] = ncclUnhandledCudaError;
+        return;
+      }
+      res[i] = comm_init_rank(&comms[i], ndev, &id, i, d);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int i = 0; i < ndev; i++) {
+    if (res[i] != ncclSuccess) {
+      for (int j = 0; j < ndev; j++)
+        if (comms[j]) comm_destroy(comms[j], true), comms[j] = nullptr;
+      return res[i];
+    }
+  }
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
+  NCCLCHECK(comm_check(comm, "ncclCommFinalize"));
+  int old = -1;
+  (void)hipGetDevice(&old);
+  (void)hipSetDevice(comm->device);
+  hipError_t e = hipDeviceSynchronize();
+  if (old >= 0) (void)hipSetDevice(old);
+  return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+}
+
+VCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;  // init.cc: destroying NULL is a no-op
+  NCCLCHECK(comm_check(comm, "ncclCommDestroy"));
+  return comm_destroy(comm, false);
+}
+
+VCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;
+  NCCLCHECK(comm_check(comm, "ncclCommAbort"));
+  return comm_destroy(comm, true);
+}
+
+VCCL_EXPORT const char* ncclGetErrorString(ncclResult_t r) {
+  switch (r) {  // src/init.cc ncclGetErrorString wording
+    case ncclSuccess: return "no error";
+    case ncclUnhandledCudaError: return "unhandled cuda error (run with NCCL_DEBUG=INFO for details)";
+    case ncclSystemError: return "unhandled system error (run with NCCL_DEBUG=INFO for details)";
+    case ncclInternalError: return "internal error - please report this issue to the NCCL developers";
+    case ncclInvalidArgument: return "invalid argument (run with NCCL_DEBUG=WARN for details)";
+    case ncclInvalidUsage: return "invalid usage (run with NCCL_DEBUG=WARN for details)";
+    case ncclRemoteError: return "remote process exited or there was a network error";
+    case ncclInProgress: return "NCCL operation in progress";
+    default: return "unknown result code";
+  }
+}
+
+VCCL_EXPORT const char* ncclGetLastError(ncclComm_t) { return ""; }
+
+VCCL_EXPORT ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
+  NCCLCHECK(comm_check(comm, "ncclCommGetAsyncError"));
+  if (!asyncError) return ncclInvalidArgument;
+  int e = comm->asyncError.load();
+  if (e == 0 && comm->errorFlag && *(volatile int*)comm->errorFlag) {
+    comm->asyncError = ncclRemoteError;  // a peer stopped making progress
+    e = ncclRemoteError;
+  }
+  *asyncError = (ncclResult_t)e;
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  NCCLCHECK(comm_check(comm, "ncclCommCount"));
+  if (!count) return ncclInvalidArgument;
+  *count = comm->nRanks;
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
+  NCCLCHECK(comm_check(comm, "ncclCommCuDevice"));
+  if (!device) return ncclInvalidArgument;
+  *device = comm->device;
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+  NCCLCHECK(comm_check(comm, "ncclCommUserRank"));
+  if (!rank) return ncclInvalidArgument;
+  *rank = comm->rank;
+  return ncclSuccess;
+}
+
+// pnccl* profiling aliases (src/include/core.h:18-31)
+extern "C" {
+ncclResult_t pncclGetVersion(int*) VCCL_ALIAS(ncclGetVersion);
+ncclResult_t pncclGetUniqueId(ncclUniqueId*) VCCL_ALIAS(ncclGetUniqueId);
+ncclResult_t pncclCommInitRank(ncclComm_t*, int, ncclUniqueId, int) VCCL_ALIAS(ncclCommInitRank);
+ncclResult_t pncclCommInitRankConfig(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*)
+    VCCL_ALIAS(ncclCommInitRankConfig);
+ncclResult_t pncclCommInitAll(ncclComm_t*, int, const int*) VCCL_ALIAS(ncclCommInitAll);
+ncclResult_t pncclCommFinalize(ncclComm_t) VCCL_ALIAS(ncclCommFinalize);
+ncclResult_t pncclCommDestroy(ncclComm_t) VCCL_ALIAS(ncclCommDestroy);
+ncclResult_t pncclCommAbort(ncclComm_t) VCCL_ALIAS(ncclCommAbort);
+const char* pncclGetErrorString(ncclResult_t) VCCL_ALIAS(ncclGetErrorString);
+const char* pncclGetLastError(ncclComm_t) VCCL_ALIAS(ncclGetLastError);
+ncclResult_t pncclCommGetAsyncError(ncclComm_t, ncclResult_t*) VCCL_ALIAS(ncclCommGetAsyncError);
+ncclResult_t pncclCommCount(const ncclComm_t, int*) VCCL_ALIAS(ncclCommCount);
+ncclResult_t pncclCommCuDevice(const ncclComm_t, int*) VCCL_ALIAS(ncclCommCuDevice);
+ncclResult_t pncclCommUserRank(const ncclComm_t, int*) VCCL_ALIAS(ncclCommUserRank);
+}

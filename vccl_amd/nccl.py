@@ -1,0 +1,242 @@
+"""ctypes binding of libvccl.so's C ABI (include/nccl.h, include/vccl_device.h).
+
+This is the binding a Python caller of the reference would write against
+libnccl (same function names, enum values, argument order and error codes —
+see INTEGRATION.md).  It loads the in-tree ``vccl_amd/lib/libvccl.so`` and
+raises ``VcclError`` if the library is missing: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libvccl.so")
+
+# ncclResult_t (nccl.h.in:40-48)
+ncclSuccess, ncclUnhandledCudaError, ncclSystemError, ncclInternalError = 0, 1, 2, 3
+ncclInvalidArgument, ncclInvalidUsage, ncclRemoteError, ncclInProgress = 4, 5, 6, 7
+# ncclRedOp_t (nccl.h.in:221-236)
+ncclSum, ncclProd, ncclMax, ncclMin, ncclAvg = 0, 1, 2, 3, 4
+# ncclDataType_t (nccl.h.in:239-252)
+ncclInt8, ncclUint8, ncclInt32, ncclUint32, ncclInt64, ncclUint64 = 0, 1, 2, 3, 4, 5
+ncclFloat16, ncclFloat32, ncclFloat64, ncclBfloat16 = 6, 7, 8, 9
+ncclFloat8e4m3, ncclFloat8e5m2, ncclNumTypes = 10, 11, 12
+# ncclScalarResidence_t
+ncclScalarDevice, ncclScalarHostImmediate = 0, 1
+# vcclDevRedOp_t (include/vccl_device.h)
+vcclDevSum, vcclDevProd, vcclDevMinMax, vcclDevPreMulSum, vcclDevSumPostDiv = 0, 1, 2, 3, 4
+vcclDevCopy = 15
+
+TYPE_SIZE = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2, 10: 1, 11: 1}
+
+# Every symbol include/*.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "ncclGetVersion", "ncclGetUniqueId", "ncclCommInitRankConfig", "ncclCommInitRank",
+    "ncclCommInitAll", "ncclCommFinalize", "ncclCommDestroy", "ncclCommAbort",
+    "ncclGetErrorString", "ncclGetLastError", "ncclCommGetAsyncError", "ncclCommCount",
+    "ncclCommCuDevice", "ncclCommUserRank", "ncclRedOpCreatePreMulSum", "ncclRedOpDestroy",
+    "ncclAllReduce", "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
+    "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
+    "vcclBuildInfo",
+]
+
+
+class VcclError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = lib().ncclGetErrorString(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} (ncclResult_t={code})")
+
+
+class ncclUniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+class vcclLaunchConfig(ctypes.Structure):
+    _fields_ = [("blockSize", ctypes.c_int), ("unroll", ctypes.c_int),
+                ("gridBlocks", ctypes.c_int), ("ntLoads", ctypes.c_int),
+                ("ntStores", ctypes.c_int)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libvccl.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make -j8` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    c_int, c_size, vp, u64 = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint64
+    pcomm = ctypes.POINTER(vp)
+    sig = {
+        "ncclGetVersion": [ctypes.POINTER(c_int)],
+        "ncclGetUniqueId": [ctypes.POINTER(ncclUniqueId)],
+        "ncclCommInitRank": [pcomm, c_int, ncclUniqueId, c_int],
+        "ncclCommInitAll": [pcomm, c_int, ctypes.POINTER(c_int)],
+        "ncclCommFinalize": [vp],
+        "ncclCommDestroy": [vp],
+        "ncclCommAbort": [vp],
+        "ncclCommGetAsyncError": [vp, ctypes.POINTER(c_int)],
+        "ncclCommCount": [vp, ctypes.POINTER(c_int)],
+        "ncclCommCuDevice": [vp, ctypes.POINTER(c_int)],
+        "ncclCommUserRank": [vp, ctypes.POINTER(c_int)],
+        "ncclRedOpCreatePreMulSum": [ctypes.POINTER(c_int), vp, c_int, c_int, vp],
+        "ncclRedOpDestroy": [c_int, vp],
+        "ncclAllReduce": [vp, vp, c_size, c_int, c_int, vp, vp],
+        "ncclReduceScatter": [vp, vp, c_size, c_int, c_int, vp, vp],
+        "ncclAllGather": [vp, vp, c_size, c_int, vp, vp],
+        "ncclGroupStart": [],
+        "ncclGroupEnd": [],
+        "vcclReduceCopy": [c_int, c_int, u64, c_int, c_int, c_int, ctypes.POINTER(vp), c_int,
+                           ctypes.POINTER(vp), c_size, vp],
+        "vcclReduceCopyEx": [c_int, c_int, u64, c_int, c_int, c_int, ctypes.POINTER(vp), c_int,
+                             ctypes.POINTER(vp), c_size, vp, ctypes.POINTER(vcclLaunchConfig)],
+        "vcclHostToDevRedOp": [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(u64)],
+        "vcclKernelTypeOf": [c_int, c_int],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = c_int
+    L.ncclGetErrorString.argtypes = [c_int]
+    L.ncclGetErrorString.restype = ctypes.c_char_p
+    L.vcclBuildInfo.argtypes = []
+    L.vcclBuildInfo.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != ncclSuccess:
+        raise VcclError(rc, what)
+
+
+def get_version() -> int:
+    v = ctypes.c_int()
+    check(lib().ncclGetVersion(ctypes.byref(v)), "ncclGetVersion")
+    return v.value
+
+
+def get_unique_id() -> ncclUniqueId:
+    uid = ncclUniqueId()
+    check(lib().ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+    return uid
+
+
+def unique_id_to_bytes(uid: ncclUniqueId) -> bytes:
+    return ctypes.string_at(ctypes.addressof(uid), 128)  # .internal stops at the first NUL
+
+
+def unique_id_from_bytes(b: bytes) -> ncclUniqueId:
+    uid = ncclUniqueId()
+    ctypes.memmove(ctypes.byref(uid), b, 128)
+    return uid
+
+
+def host_to_dev_redop(op: int, dtype: int, nranks: int) -> tuple[int, int]:
+    d, a = ctypes.c_int(), ctypes.c_uint64()
+    check(lib().vcclHostToDevRedOp(op, dtype, nranks, ctypes.byref(d), ctypes.byref(a)),
+          "vcclHostToDevRedOp")
+    return d.value, a.value
+
+
+def kernel_type_of(dev_op: int, dtype: int) -> int:
+    return lib().vcclKernelTypeOf(dev_op, dtype)
+
+
+def reduce_copy(dev_op: int, dtype: int, red_arg: int, srcs, dsts, n_elts: int, stream: int = 0,
+                pre_op_srcs: int = 0, post_op: bool = False, config: dict | None = None) -> None:
+    """vcclReduceCopy on raw device pointers (ints)."""
+    s = (ctypes.c_void_p * len(srcs))(*srcs)
+    d = (ctypes.c_void_p * len(dsts))(*dsts)
+    if config:
+        cfg = vcclLaunchConfig(**config)
+        rc = lib().vcclReduceCopyEx(dev_op, dtype, red_arg, pre_op_srcs, int(post_op), len(srcs),
+                                    s, len(dsts), d, n_elts, stream, ctypes.byref(cfg))
+    else:
+        rc = lib().vcclReduceCopy(dev_op, dtype, red_arg, pre_op_srcs, int(post_op), len(srcs), s,
+                                  len(dsts), d, n_elts, stream)
+    check(rc, "vcclReduceCopy")
+
+
+class Comm:
+    """Owning wrapper over ncclComm_t."""
+
+    def __init__(self, handle: int):
+        self.handle = ctypes.c_void_p(handle)
+
+    @classmethod
+    def init_rank(cls, nranks: int, uid: ncclUniqueId, rank: int) -> "Comm":
+        h = ctypes.c_void_p()
+        check(lib().ncclCommInitRank(ctypes.byref(h), nranks, uid, rank), "ncclCommInitRank")
+        return cls(h.value)
+
+    @classmethod
+    def init_all(cls, devices: list[int]) -> list["Comm"]:
+        n = len(devices)
+        hs = (ctypes.c_void_p * n)()
+        dl = (ctypes.c_int * n)(*devices)
+        check(lib().ncclCommInitAll(hs, n, dl), "ncclCommInitAll")
+        return [cls(hs[i]) for i in range(n)]
+
+    def _q(self, fn, what):
+        v = ctypes.c_int()
+        check(fn(self.handle, ctypes.byref(v)), what)
+        return v.value
+
+    @property
+    def count(self) -> int:
+        return self._q(lib().ncclCommCount, "ncclCommCount")
+
+    @property
+    def rank(self) -> int:
+        return self._q(lib().ncclCommUserRank, "ncclCommUserRank")
+
+    @property
+    def device(self) -> int:
+        return self._q(lib().ncclCommCuDevice, "ncclCommCuDevice")
+
+    def async_error(self) -> int:
+        return self._q(lib().ncclCommGetAsyncError, "ncclCommGetAsyncError")
+
+    def all_reduce(self, send: int, recv: int, count: int, dtype: int, op: int, stream: int = 0):
+        check(lib().ncclAllReduce(send, recv, count, dtype, op, self.handle, stream), "ncclAllReduce")
+
+    def reduce_scatter(self, send: int, recv: int, recvcount: int, dtype: int, op: int,
+                       stream: int = 0):
+        check(lib().ncclReduceScatter(send, recv, recvcount, dtype, op, self.handle, stream),
+              "ncclReduceScatter")
+
+    def all_gather(self, send: int, recv: int, sendcount: int, dtype: int, stream: int = 0):
+        check(lib().ncclAllGather(send, recv, sendcount, dtype, self.handle, stream), "ncclAllGather")
+
+    def create_premulsum(self, scalar_ptr: int, dtype: int, residence: int) -> int:
+        op = ctypes.c_int()
+        check(lib().ncclRedOpCreatePreMulSum(ctypes.byref(op), scalar_ptr, dtype, residence,
+                                             self.handle), "ncclRedOpCreatePreMulSum")
+        return op.value
+
+    def destroy_op(self, op: int):
+        check(lib().ncclRedOpDestroy(op, self.handle), "ncclRedOpDestroy")
+
+    def destroy(self):
+        if self.handle:
+            check(lib().ncclCommDestroy(self.handle), "ncclCommDestroy")
+            self.handle = ctypes.c_void_p()
+
+    def abort(self):
+        if self.handle:
+            check(lib().ncclCommAbort(self.handle), "ncclCommAbort")
+            self.handle = ctypes.c_void_p()
+
+
+def group_start():
+    check(lib().ncclGroupStart(), "ncclGroupStart")
+
+
+def group_end():
+    check(lib().ncclGroupEnd(), "ncclGroupEnd")
