@@ -1,0 +1,111 @@
+"""Test-side restatement of the ring data partition, to compute the exact
+expected result of a ring collective with the CPU oracle.
+
+Mirrors vccl_amd/csrc/host/init.cc (ring_orders, channel count) and
+vccl_amd/csrc/device/ring.hpp (channel_part, the all-reduce round/chunk
+layout of all_reduce.h:32-82).  The oracle's ring_fold then reproduces the
+fold order element by element, so multi-rank fp results are checked
+bit-exactly against OUR partition, and with the §8c tolerance against any
+other partition (e.g. the reference's, which differs).
+"""
+import numpy as np
+
+from oracle import oracle as O
+
+RINGS = {
+    8: [[0, 1, 2, 3, 4, 5, 6, 7], [0, 2, 1, 3, 5, 4, 7, 6], [0, 3, 1, 4, 6, 2, 7, 5],
+        [0, 4, 1, 5, 7, 2, 6, 3], [0, 5, 3, 6, 1, 7, 4, 2], [0, 6, 5, 2, 4, 3, 7, 1],
+        [0, 7, 3, 2, 5, 1, 6, 4]],
+    4: [[0, 1, 2, 3], [0, 1, 3, 2], [0, 2, 1, 3], [0, 2, 3, 1], [0, 3, 1, 2], [0, 3, 2, 1]],
+}
+
+
+def ring_orders(n):
+    return RINGS.get(n, [list(range(n))])
+
+
+def n_channels(n, per_ring=None, nch=None):
+    rings = ring_orders(n)
+    if per_ring is None:
+        per_ring = 4 if n in (4, 8) else 16
+    c = nch if nch is not None else per_ring * len(rings)
+    return max(1, min(c, 64))
+
+
+def _align_up(x, a):
+    return (x + a - 1) // a * a
+
+
+def _div_up(x, a):
+    return (x + a - 1) // a
+
+
+def channel_part(count, nch, c, elt_align):
+    per = _align_up(_div_up(count, nch), elt_align)
+    lo = min(per * c, count)
+    hi = min(per * (c + 1), count)
+    return lo, hi - lo
+
+
+def allreduce_owner(count, n, nch, slot_bytes, elt_size):
+    """(channel, owner ring position) per element for the ring all-reduce."""
+    elt_align = max(1, 16 // elt_size)
+    chan = np.zeros(count, np.int32)
+    owner = np.zeros(count, np.int32)
+    for c in range(nch):
+        off, length = channel_part(count, nch, c, elt_align)
+        chunk = slot_bytes // elt_size
+        loop = n * chunk
+        eo = 0
+        while eo < length:
+            rem = length - eo
+            if rem < loop:
+                chunk = _align_up(_div_up(rem, n), elt_align)
+            for k in range(n):
+                lo = eo + k * chunk
+                hi = min(eo + (k + 1) * chunk, length)
+                if hi > lo:
+                    chan[off + lo:off + hi] = c
+                    owner[off + lo:off + hi] = k
+            eo += loop
+    return chan, owner
+
+
+def expected_allreduce(op, dtype, inputs, nch, slot_bytes):
+    """Exact expected output (identical on every rank)."""
+    n = len(inputs)
+    dev_op, arg = O.host_to_dev_redop(op, dtype, n)
+    pre = dev_op == O.DEV_PREMULSUM
+    count = inputs[0].size
+    chan, owner = allreduce_owner(count, n, nch, slot_bytes, inputs[0].dtype.itemsize)
+    out = np.empty_like(inputs[0])
+    rings = ring_orders(n)
+    for c in range(nch):
+        idx = np.nonzero(chan == c)[0]
+        if idx.size == 0:
+            continue
+        ring = rings[c % len(rings)]
+        ins = [inputs[r][idx] for r in ring]
+        out[idx] = O.ring_fold(dev_op, dtype, arg, pre, ins, owner[idx])
+    return out
+
+
+def expected_reducescatter(op, dtype, inputs, nch):
+    """Per-rank expected outputs; inputs[r] has n*recvcount elements."""
+    n = len(inputs)
+    dev_op, arg = O.host_to_dev_redop(op, dtype, n)
+    pre = dev_op == O.DEV_PREMULSUM
+    count = inputs[0].size // n
+    elt_align = max(1, 16 // inputs[0].dtype.itemsize)
+    rings = ring_orders(n)
+    outs = [np.empty(count, inputs[0].dtype) for _ in range(n)]
+    for c in range(nch):
+        off, length = channel_part(count, nch, c, elt_align)
+        if length == 0:
+            continue
+        ring = rings[c % len(rings)]
+        for r in range(n):
+            ins = [inputs[q][r * count + off:r * count + off + length] for q in ring]
+            own = np.full(length, ring.index(r), np.int32)
+            outs[r][off:off + length] = O.ring_fold(dev_op, dtype, arg, pre, ins, own)
+    return outs

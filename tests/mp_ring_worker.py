@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""One rank of a multi-process ring test (spawned by tests/test_gpu_collectives.py).
+
+argv: rank nranks device uid_hex outdir
+Runs every case of tests/ring_cases.py through ncclAllReduce /
+ncclReduceScatter / ncclAllGather and saves its outputs to outdir/rank<r>.npz.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tests import ring_cases as RC  # noqa: E402
+from vccl_amd import nccl  # noqa: E402
+
+
+def main():
+    rank, nranks, device = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[4]))
+    outdir = sys.argv[5]
+    torch.cuda.set_device(device)
+    comm = nccl.Comm.init_rank(nranks, uid, rank)
+    s = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for ci, (name, coll, op, dt, count) in enumerate(RC.CASES):
+        x = RC.gen_input(ci, rank, nranks)
+        xb = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+        nout = RC.out_count(ci, nranks)
+        yb = torch.empty(nout * x.dtype.itemsize, dtype=torch.uint8, device="cuda")
+        if coll == "ar":
+            comm.all_reduce(xb.data_ptr(), yb.data_ptr(), count, dt, op, s)
+        elif coll == "ar_inplace":
+            comm.all_reduce(xb.data_ptr(), xb.data_ptr(), count, dt, op, s)
+            yb = xb
+        elif coll == "rs":
+            comm.reduce_scatter(xb.data_ptr(), yb.data_ptr(), count, dt, op, s)
+        else:
+            comm.all_gather(xb.data_ptr(), yb.data_ptr(), count, dt, s)
+        torch.cuda.synchronize()
+        res[name] = yb.cpu().numpy().view(x.dtype)
+    err = comm.async_error()
+    comm.destroy()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)
+    sys.exit(0 if err == 0 else 3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,105 @@
+"""Ring all-reduce / reduce-scatter / all-gather parity on MI355X.
+
+The box has one GPU, so the multi-rank protocol is exercised with several
+ranks sharing device 0: (a) one process driving n comms from
+ncclCommInitAll([0]*n) inside ncclGroupStart/End, one stream per rank;
+(b) 8 (and 2) separate processes joined through ncclGetUniqueId /
+ncclCommInitRank, FIFOs mapped with hipIpcOpenMemHandle.  Expected outputs
+come from the CPU oracle's ring fold over OUR channel partition
+(tests/_ring.py), so every type/op is checked bit-exactly (min/max: +0 == -0).
+Spins are bounded (VCCL_SPIN_TIMEOUT_S) so a protocol bug fails the test
+instead of hanging the GPU.
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from tests import _ring
+from tests import ring_cases as RC
+from tests._util import assert_bitexact
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from vccl_amd import nccl  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SLOT = 256 << 10
+os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+
+
+def _check(ci, n, outs):
+    name, coll, op, dt, count = RC.CASES[ci]
+    exp = RC.expected(ci, n, _ring.n_channels(n), SLOT)
+    for r in range(n):
+        assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_single_process_ranks(n):
+    comms = nccl.Comm.init_all([0] * n)
+    try:
+        assert [c.rank for c in comms] == list(range(n)) and comms[0].count == n
+        streams = [torch.cuda.Stream() for _ in range(n)]
+        for ci, (name, coll, op, dt, count) in enumerate(RC.CASES):
+            xs = [RC.gen_input(ci, r, n) for r in range(n)]
+            xb = [torch.from_numpy(x.view(np.uint8).copy()).cuda() for x in xs]
+            nout = RC.out_count(ci, n)
+            yb = [torch.empty(nout * xs[0].dtype.itemsize, dtype=torch.uint8, device="cuda")
+                  for _ in range(n)]
+            torch.cuda.synchronize()
+            nccl.group_start()
+            for r, c in enumerate(comms):
+                sp = streams[r].cuda_stream
+                if coll == "ar":
+                    c.all_reduce(xb[r].data_ptr(), yb[r].data_ptr(), count, dt, op, sp)
+                elif coll == "ar_inplace":
+                    c.all_reduce(xb[r].data_ptr(), xb[r].data_ptr(), count, dt, op, sp)
+                elif coll == "rs":
+                    c.reduce_scatter(xb[r].data_ptr(), yb[r].data_ptr(), count, dt, op, sp)
+                else:
+                    c.all_gather(xb[r].data_ptr(), yb[r].data_ptr(), count, dt, sp)
+            nccl.group_end()
+            torch.cuda.synchronize()
+            for c in comms:
+                assert c.async_error() == 0, f"{name}: spin timeout (protocol hang)"
+            outs = [(xb[r] if coll == "ar_inplace" else yb[r]).cpu().numpy().view(xs[0].dtype)
+                    for r in range(n)]
+            _check(ci, n, outs)
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_multi_process_ranks(n):
+    uid = nccl.get_unique_id()  # root thread lives in this process
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
+                                   str(r), str(n), "0", hexid, d], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                 for r in range(n)]
+        logs = []
+        for p in procs:
+            try:
+                out, _ = p.communicate(timeout=420)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            logs.append(out.decode(errors="replace")[-2000:])
+        codes = [p.returncode for p in procs]
+        assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
+        res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
+        for ci, case in enumerate(RC.CASES):
+            _check(ci, n, [res[r][case[0]] for r in range(n)])

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Interleaved launch-geometry sweep of the reduce-copy kernel (config 2 shape).
+
+All variants run in ONE process, round-robin, each launch timed with its own
+HIP event pair on the launch stream (cdna_hip_programming.md §5.4 rule 24).
+Prints median / min GB/s per variant as JSON lines.
+"""
+import itertools
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vccl_amd import nccl  # noqa: E402
+
+
+def main():
+    n = int(os.environ.get("SWEEP_ELEMS", 1 << 26))
+    rounds = int(os.environ.get("SWEEP_ROUNDS", 8))
+    reps = int(os.environ.get("SWEEP_REPS", 10))
+    a = torch.rand(n, device="cuda") * 2 - 1
+    b = torch.rand(n, device="cuda") * 2 - 1
+    d = torch.empty_like(a)
+    ref = a + b
+    s = torch.cuda.current_stream()
+    sp = s.cuda_stream
+    variants = []
+    for block, unroll, mult, ntl, nts in itertools.product(
+            (256, 512, 1024), (2, 4, 8), (4, 8, 16, 0), (0, 1), (0, 1)):
+        if unroll == 2 and (ntl or nts):
+            continue  # only the plain flavour is instantiated at unroll 2
+        hunk = block * unroll * 16
+        full = (n * 4 + hunk - 1) // hunk
+        grid = full if mult == 0 else min(full, 256 * mult)
+        variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
+                         "ntLoads": ntl, "ntStores": nts})
+    variants.append(None)  # library default
+    variants.append("torch_add")  # known-good reference on the same hardware: torch.add(a, b, out=d)
+    times = {i: [] for i in range(len(variants))}
+    for r in range(rounds):
+        order = list(range(len(variants)))
+        np.random.default_rng(r).shuffle(order)
+        for i in order:
+            cfg = variants[i]
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(reps)]
+            for e0, e1 in ev:
+                e0.record(s)
+                if cfg == "torch_add":
+                    torch.add(a, b, out=d)
+                else:
+                    nccl.reduce_copy(0, 7, 0, [a.data_ptr(), b.data_ptr()], [d.data_ptr()], n, sp,
+                                     config=cfg)
+                e1.record(s)
+            torch.cuda.synchronize()
+            times[i] += [e0.elapsed_time(e1) for e0, e1 in ev]
+            if r == 0:
+                assert torch.equal(d, ref), cfg
+    rows = []
+    for i, cfg in enumerate(variants):
+        t = np.array(times[i][reps:])  # drop the first round (warm-up)
+        gbs = 3 * n * 4 / (t / 1e3) / 1e9
+        rows.append({"cfg": cfg or "default", "median_gbs": round(float(np.median(gbs)), 1),
+                     "max_gbs": round(float(gbs.max()), 1), "median_us": round(float(np.median(t)) * 1e3, 2)})
+    rows.sort(key=lambda x: -x["median_gbs"])
+    for row in rows:
+        print(json.dumps(row))
+
+
+if __name__ == "__main__":
+    main()

@@ -8,10 +8,15 @@
 
 namespace vccl {
 
-// Library defaults for the grid-wide reduce-copy.
+// Library defaults for the grid-wide reduce-copy, from the interleaved sweep
+// of tools/sweep_rc.py on MI355X (profiles/r01_sweep_rc.log):
+// 256 threads, 4 x 16 B per thread per source, one hunk per workgroup (no
+// grid-stride below kRcMaxGrid), nontemporal loads, plain stores.
 constexpr int kRcDefBlock = 256;
 constexpr int kRcDefUnroll = 4;
-constexpr int kRcDefBlocksPerCU = 8;
+constexpr int kRcMaxGrid = 65536;
+constexpr int kRcDefLd = kLdNT;
+constexpr int kRcDefSt = kStPlain;
 
 // Internal entry used by both the C ABI and the one-rank path.  `a` holds the
 // pointers; geometry from cfg (nullptr = defaults).

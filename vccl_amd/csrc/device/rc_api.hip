@@ -9,19 +9,6 @@
 
 using namespace vccl;
 
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      n = v;
-    else
-      n = 256;
-  }
-  return n;
-}
-
 static int elt_size_of_kt(int k) {
   switch (k) {
     case K_U8: return 1;
@@ -41,14 +28,14 @@ hipError_t reduce_copy_launch(int devOp, int datatype, uint64_t redArg, RCArgs a
   lg.unroll = (cfg && cfg->unroll) ? cfg->unroll : kRcDefUnroll;
   if (lg.block != 256 && lg.block != 512 && lg.block != 1024) return hipErrorInvalidValue;
   if (lg.unroll != 2 && lg.unroll != 4 && lg.unroll != 8) return hipErrorInvalidValue;
-  lg.ntLoads = cfg ? cfg->ntLoads : 0;
-  lg.ntStores = cfg ? cfg->ntStores : 0;
+  lg.ntLoads = cfg ? cfg->ntLoads : (kRcDefLd == kLdNT);
+  lg.ntStores = cfg ? cfg->ntStores : (kRcDefSt == kStNT);
   const int64_t bytes = nElts * elt_size_of_kt(k);
   const int64_t hunk = (int64_t)lg.block * lg.unroll * 16;
   const int64_t want = (bytes + hunk - 1) / hunk;
   lg.grid = (cfg && cfg->gridBlocks)
                 ? cfg->gridBlocks
-                : (int)std::min<int64_t>(want, (int64_t)num_cus() * kRcDefBlocksPerCU);
+                : (int)std::min<int64_t>(want, (int64_t)kRcMaxGrid);
   if (lg.grid < 1) lg.grid = 1;
   a.argBytes = elt_size_of_kt(k);
   switch (k) {

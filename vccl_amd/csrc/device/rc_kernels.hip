@@ -31,7 +31,7 @@ static hipError_t launch_nsnd(const RCArgs& a, int64_t nElts, uint64_t redArg,
   hipLaunchKernelGGL((k_reduce_copy<Fn, NS, ND, U, L, S>), g, b, 0, s, a, nElts, redArg); \
   return hipGetLastError();
   if constexpr (!kSweep) {
-    VCCL_RC_LAUNCH(kRcDefUnroll, kLdPlain, kStPlain)
+    VCCL_RC_LAUNCH(kRcDefUnroll, kRcDefLd, kRcDefSt)
   } else {
     const int ntl = lg.ntLoads, nts = lg.ntStores;
     if (lg.unroll == 8) {
