@@ -114,6 +114,7 @@ static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, b
 }
 
 static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
+  VINFO("rank %d/%d dev %d: bootstrap", c->rank, c->nRanks, c->device);
   NCCLCHECK(bootstrap_init(id, c->rank, c->nRanks, &c->bootstrap));
   const int n = c->nRanks;
   const auto rings = ring_orders(n);
@@ -144,6 +145,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   if (n > 1) {
     const size_t fifoBytes = (size_t)c->nChannels * kSteps * c->slotBytes;
     const size_t flagBytes = (size_t)c->nChannels * 2 * kFlagStride;
+    VINFO("rank %d: alloc fifo %zu B", c->rank, fifoBytes);
     NCCLCHECK(alloc_uncached((void**)&c->fifoBuf, fifoBytes));
     NCCLCHECK(alloc_uncached((void**)&c->flagBuf, flagBytes));
     HIPCHECK(hipMemset(c->flagBuf, 0, flagBytes));
@@ -152,6 +154,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     me.fifoPtr = c->fifoBuf;
     me.flagPtr = c->flagBuf;
   }
+  VINFO("rank %d: exchange peer info", c->rank);
   c->peers.assign(n, PeerMap{});
   c->peers[c->rank] = me;
   NCCLCHECK(bootstrap_allgather(c->bootstrap, c->peers.data(), sizeof(PeerMap)));
@@ -173,6 +176,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));
 
+  VINFO("rank %d: map peers", c->rank);
   if (n > 1) {
     std::vector<char*> fifoOf(n), flagOf(n);
     for (int r = 0; r < n; r++) {
@@ -209,6 +213,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     HIPCHECK(hipMemcpy(c->devChannels, chans.data(), sizeof(DevChannel) * c->nChannels,
                        hipMemcpyHostToDevice));
   }
+  VINFO("rank %d: final barrier", c->rank);
   NCCLCHECK(bootstrap_barrier(c->bootstrap));
   VINFO("comm %p rank %d/%d dev %d: %d channels x %d threads, slot %d B", (void*)c, c->rank, n,
         c->device, c->nChannels, c->nThreads, c->slotBytes);
@@ -247,8 +252,14 @@ ncclResult_t comm_destroy(ncclComm* c, bool abort) {
   (void)hipSetDevice(c->device);
   if (abort && c->abortFlag) *c->abortFlag = 1;
   (void)hipDeviceSynchronize();
-  // Peers may still be reading our FIFOs until they finish: rendezvous first.
-  if (!abort && c->bootstrap && c->nRanks > 1) (void)bootstrap_barrier(c->bootstrap);
+  // Peers in OTHER processes may still post a last credit into our flags:
+  // rendezvous before freeing.  Comms of one process (ncclCommInitAll) are
+  // legitimately destroyed one after another by a single thread (as with the
+  // reference), so a barrier there would deadlock; their kernels are already
+  // complete once the owning devices have synchronised.
+  bool remotePeers = false;
+  for (const auto& p : c->peers) remotePeers |= p.pid != (int)getpid();
+  if (!abort && remotePeers && c->bootstrap && c->nRanks > 1) (void)bootstrap_barrier(c->bootstrap);
   free_resources(c);
   bootstrap_close(c->bootstrap);
   c->bootstrap = nullptr;
