@@ -137,7 +137,9 @@ def _dist_setup():
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    torch.cuda.set_device(local)
+    # one process per GPU; on a box with fewer GPUs than ranks (rehearsal),
+    # ranks share devices round-robin
+    torch.cuda.set_device(local % torch.cuda.device_count())
     dist.init_process_group("gloo", rank=rank, world_size=world)
     obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
@@ -162,9 +164,67 @@ def _time_coll(dist, fn, steps, warmup):
     return float(t.item())
 
 
+class _HipIpcHandle(ctypes.Structure):
+    _fields_ = [("reserved", ctypes.c_char * 64)]
+
+
+def peer_copy_bench(dist, rank, world, nbytes=256 << 20, steps=10):
+    """xGMI microbench: write a local buffer into the next rank's HBM (one link,
+    one direction) and into all peers at once (every outgoing link), with the
+    library's copy kernel; buffers mapped via hipIpcGetMemHandle/OpenMemHandle.
+    Pins the per-link denominator of the all-reduce roofline."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp = ctypes.c_void_p
+    hip.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(vp), _HipIpcHandle, ctypes.c_uint]
+    hip.hipIpcGetMemHandle.argtypes = [ctypes.POINTER(_HipIpcHandle), vp]
+    local, remote = vp(), vp()
+    assert hip.hipMalloc(ctypes.byref(local), ctypes.c_size_t(nbytes)) == 0
+    assert hip.hipMalloc(ctypes.byref(remote), ctypes.c_size_t(nbytes)) == 0
+    handle = _HipIpcHandle()
+    assert hip.hipIpcGetMemHandle(ctypes.byref(handle), remote) == 0
+    handles = [None] * world
+    dist.all_gather_object(handles, bytes(ctypes.string_at(ctypes.addressof(handle), 64)))
+    peers = {}
+    res = {}
+    try:
+        for r in range(world):
+            if r == rank:
+                continue
+            p = vp()
+            h = _HipIpcHandle()
+            ctypes.memmove(ctypes.addressof(h), handles[r], 64)
+            rc = hip.hipIpcOpenMemHandle(ctypes.byref(p), h, 1)
+            if rc != 0:
+                raise RuntimeError(f"hipIpcOpenMemHandle -> {rc}")
+            peers[r] = p.value
+        ok = 1
+    except RuntimeError as e:
+        res["error"] = str(e)
+        ok = 0
+    t = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    sp = torch.cuda.current_stream().cuda_stream
+    if t.item() == 1:
+        nxt = (rank + 1) % world
+        for name, dsts in (("one_peer", [peers[nxt]]), ("all_peers", list(peers.values()))):
+            def fn(d=dsts):
+                nccl.reduce_copy(nccl.vcclDevCopy, nccl.ncclUint8, 0, [local.value], d, nbytes, sp)
+            dt = _time_coll(dist, fn, steps, 2)
+            res[name + "_GBs"] = round(nbytes * len(dsts) * steps / dt / 1e9, 2)
+    torch.cuda.synchronize()
+    dist.barrier()
+    for p in peers.values():
+        hip.hipIpcCloseMemHandle(vp(p))
+    hip.hipFree(local)
+    hip.hipFree(remote)
+    res["bytes"] = nbytes
+    return res
+
+
 def bench_allreduce(args):
     dist, rank, world, comm = _dist_setup()
     sp = torch.cuda.current_stream().cuda_stream
+    xgmi = peer_copy_bench(dist, rank, world) if not args.no_peer else None
     sizes = [1 << p for p in range(3, 31)] if args.sweep else [args.bytes or (1 << 30)]
     rows = []
     for S in sizes:
@@ -200,7 +260,8 @@ def bench_allreduce(args):
                       "async_error": err},
            "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": peak,
                         "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
-                        "note": f"per-rank busbw vs {links} links x {XGMI_LINK_GBS} GB/s/direction (spec)"}}
+                        "note": f"per-rank busbw vs {links} links x {XGMI_LINK_GBS} GB/s/direction (spec)",
+                        "measured_peer_copy": xgmi}}
     if args.sweep:
         out["sweep"] = [{k: round(v, 3) if isinstance(v, float) else v for k, v in r.items()} for r in rows]
     dist.destroy_process_group()
@@ -251,6 +312,7 @@ def main():
     ap.add_argument("--workload", default="")
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-peer", action="store_true")
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)

@@ -20,6 +20,7 @@
 #include <random>
 #include <thread>
 
+#include "../../../include/vccl_bootstrap.h"
 #include "core.h"
 
 namespace vccl {
@@ -231,3 +232,14 @@ void bootstrap_close(Bootstrap* b) {
 }
 
 }  // namespace vccl
+
+extern "C" __attribute__((visibility("default"))) ncclResult_t vcclBootstrapAllGather(
+    const ncclUniqueId* id, int rank, int nranks, void* buf, size_t bytesPerRank) {
+  if (!id || !buf || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+  vccl::Bootstrap* b = nullptr;
+  ncclResult_t r = vccl::bootstrap_init(id, rank, nranks, &b);
+  if (r != ncclSuccess) return r;
+  r = vccl::bootstrap_allgather(b, buf, bytesPerRank);
+  vccl::bootstrap_close(b);
+  return r;
+}

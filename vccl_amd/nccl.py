@@ -38,7 +38,7 @@ EXPORTED = [
     "ncclCommCuDevice", "ncclCommUserRank", "ncclRedOpCreatePreMulSum", "ncclRedOpDestroy",
     "ncclAllReduce", "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
-    "vcclBuildInfo",
+    "vcclBuildInfo", "vcclBootstrapAllGather",
 ]
 
 
@@ -97,6 +97,7 @@ def lib() -> ctypes.CDLL:
                              ctypes.POINTER(vp), c_size, vp, ctypes.POINTER(vcclLaunchConfig)],
         "vcclHostToDevRedOp": [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(u64)],
         "vcclKernelTypeOf": [c_int, c_int],
+        "vcclBootstrapAllGather": [ctypes.POINTER(ncclUniqueId), c_int, c_int, vp, c_size],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -135,6 +136,17 @@ def unique_id_from_bytes(b: bytes) -> ncclUniqueId:
     uid = ncclUniqueId()
     ctypes.memmove(ctypes.byref(uid), b, 128)
     return uid
+
+
+def bootstrap_allgather(uid: ncclUniqueId, rank: int, nranks: int, mine: bytes) -> list[bytes]:
+    """One all-gather round over the TCP rendezvous (host only)."""
+    n = len(mine)
+    buf = ctypes.create_string_buffer(n * nranks)
+    ctypes.memmove(ctypes.addressof(buf) + rank * n, mine, n)
+    check(lib().vcclBootstrapAllGather(ctypes.byref(uid), rank, nranks, buf, n),
+          "vcclBootstrapAllGather")
+    raw = buf.raw
+    return [raw[i * n:(i + 1) * n] for i in range(nranks)]
 
 
 def host_to_dev_redop(op: int, dtype: int, nranks: int) -> tuple[int, int]:
