@@ -221,10 +221,32 @@ def peer_copy_bench(dist, rank, world, nbytes=256 << 20, steps=10):
     return res
 
 
+def allreduce_check(dist, comm, rank, world, nbytes=64 << 20):
+    """Exactness check on the real topology: integer-valued fp32 inputs
+    (sums exact in any fold order), every rank regenerates all inputs."""
+    sp = torch.cuda.current_stream().cuda_stream
+    n = nbytes // 4
+    ref = torch.zeros(n, device="cuda")
+    mine = None
+    for r in range(world):
+        g = torch.Generator(device="cuda").manual_seed(4242 + r)
+        v = torch.randint(-64, 64, (n,), device="cuda", generator=g).float()
+        ref += v
+        if r == rank:
+            mine = v
+    out = torch.empty_like(ref)
+    comm.all_reduce(mine.data_ptr(), out.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+    torch.cuda.synchronize()
+    ok = torch.tensor([1 if torch.equal(out, ref) and comm.async_error() == 0 else 0])
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return bool(ok.item())
+
+
 def bench_allreduce(args):
     dist, rank, world, comm = _dist_setup()
     sp = torch.cuda.current_stream().cuda_stream
     xgmi = peer_copy_bench(dist, rank, world) if not args.no_peer else None
+    correct = allreduce_check(dist, comm, rank, world)
     sizes = [1 << p for p in range(3, 31)] if args.sweep else [args.bytes or (1 << 30)]
     rows = []
     for S in sizes:
@@ -257,7 +279,7 @@ def bench_allreduce(args):
                                   "(BASELINE config 3), value = aggregate busbw over ranks",
                       "bytes_per_rank": last["bytes"], "busbw_per_rank": round(last["busbw"], 2),
                       "algbw": round(last["algbw"], 2), "parallelism": f"ring x{world}",
-                      "async_error": err},
+                      "async_error": err, "correct": correct},
            "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": peak,
                         "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
                         "note": f"per-rank busbw vs {links} links x {XGMI_LINK_GBS} GB/s/direction (spec)",

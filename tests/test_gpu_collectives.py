@@ -31,19 +31,25 @@ if not torch.cuda.is_available():
 from vccl_amd import nccl  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SLOT = 256 << 10
 os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+# Several ranks share ONE GPU here, so every rank's channel workgroups must be
+# co-resident: the tests pin a geometry that fits (library defaults are sized
+# for one rank per GPU and are exercised by the 2-process default case).
+TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10)}
 
 
-def _check(ci, n, outs):
+def _check(ci, n, outs, nch, slot):
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, _ring.n_channels(n), SLOT)
+    exp = RC.expected(ci, n, nch, slot)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
 
 
 @pytest.mark.parametrize("n", [2, 3, 4])
-def test_single_process_ranks(n):
+def test_single_process_ranks(n, monkeypatch):
+    for k, v in TEST_GEOM.items():
+        monkeypatch.setenv(k, v)
+    nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
     comms = nccl.Comm.init_all([0] * n)
     try:
         assert [c.rank for c in comms] == list(range(n)) and comms[0].count == n
@@ -72,18 +78,25 @@ def test_single_process_ranks(n):
                 assert c.async_error() == 0, f"{name}: spin timeout (protocol hang)"
             outs = [(xb[r] if coll == "ar_inplace" else yb[r]).cpu().numpy().view(xs[0].dtype)
                     for r in range(n)]
-            _check(ci, n, outs)
+            _check(ci, n, outs, nch, slot)
     finally:
         for c in comms:
             c.destroy()
 
 
-@pytest.mark.parametrize("n", [2, 8])
-def test_multi_process_ranks(n):
+@pytest.mark.parametrize("n,geom", [(2, "default"), (8, "test")])
+def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    if geom == "test":
+        env.update(TEST_GEOM)
+        nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+    else:
+        for k in TEST_GEOM:
+            env.pop(k, None)
+        nch, slot = _ring.n_channels(n), 512 << 10
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
                                    str(r), str(n), "0", hexid, d], env=env,
@@ -102,4 +115,4 @@ def test_multi_process_ranks(n):
         assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
-            _check(ci, n, [res[r][case[0]] for r in range(n)])
+            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot)

@@ -16,7 +16,7 @@ namespace vccl {
 template <class Fn, int NS, int ND, int UNROLL, int LD, int ST>
 __global__ __launch_bounds__(1024) void k_reduce_copy(RCArgs a, int64_t nElts, uint64_t redArg) {
   Fn fn(load_op_arg(a.argPtr, a.argBytes, redArg));
-  reduce_copy<Fn, NS, ND, UNROLL, LD, ST>(fn, a, nElts, blockIdx.x, gridDim.x, threadIdx.x,
+  reduce_copy<Fn, NS, ND, UNROLL, uniform_pol(LD, ST)>(fn, a, nElts, blockIdx.x, gridDim.x, threadIdx.x,
                                           blockDim.x);
 }
 

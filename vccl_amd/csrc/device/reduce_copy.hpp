@@ -12,7 +12,15 @@
 // UNROLL*NSRC 16-byte loads in flight before its first reduce.  Hunks are
 // dealt to "workers" (workgroups for a grid-wide copy, one for an in-ring
 // slice) round-robin.  No LDS: there is no data reuse, so staging through LDS
-// would add traffic, not remove it (DESIGN.md §Kernels).
+// would add traffic, not remove it (DESIGN.md §4).
+//
+// Memory policy per operand (POLS template word, 2 bits per operand):
+//   kPlain  global_load/store
+//   kNT     nontemporal (streamed once; the tuned default for user buffers)
+//   kSys    buffer_load/store ... sc0 sc1: system-coherent, write-through —
+//           used for ring FIFO slots shared with a peer GPU over xGMI, so a
+//           drained store is visible at the peer without an L2 writeback and
+//           a load never hits a stale cached line (no acquire/release fence).
 #pragma once
 #include "ops.hpp"
 
@@ -21,19 +29,69 @@ namespace vccl {
 constexpr int kMaxSrcs = 8;
 constexpr int kMaxDsts = 8;
 
-// Memory flavours for the pack path.
-enum : int { kLdPlain = 0, kLdNT = 1 };
-enum : int { kStPlain = 0, kStNT = 1 };
+enum : int { kPlain = 0, kNT = 1, kSys = 2 };
+// Legacy names used by the launch sweep.
+enum : int { kLdPlain = kPlain, kLdNT = kNT };
+enum : int { kStPlain = kPlain, kStNT = kNT };
 
-template <int LD>
-__device__ __forceinline__ u32x4 ld16(const char* p) {
-  if constexpr (LD == kLdNT) return __builtin_nontemporal_load((const u32x4*)p);
-  else return *(const u32x4*)p;
+// Policy word: bits [2s, 2s+1] = source s (s < 4), bits [8+2d, 9+2d] = dest d
+// (d < 4); operands beyond index 3 use the policy of index 3.
+constexpr int mkpol(int s0, int s1, int s2, int s3, int d0, int d1, int d2, int d3) {
+  return s0 | s1 << 2 | s2 << 4 | s3 << 6 | d0 << 8 | d1 << 10 | d2 << 12 | d3 << 14;
 }
-template <int ST>
-__device__ __forceinline__ void st16(char* p, u32x4 v) {
-  if constexpr (ST == kStNT) __builtin_nontemporal_store(v, (u32x4*)p);
-  else *(u32x4*)p = v;
+constexpr int uniform_pol(int ld, int st) { return mkpol(ld, ld, ld, ld, st, st, st, st); }
+constexpr int src_pol(int POLS, int s) { return (POLS >> (2 * (s < 3 ? s : 3))) & 3; }
+constexpr int dst_pol(int POLS, int d) { return (POLS >> (8 + 2 * (d < 3 ? d : 3))) & 3; }
+
+constexpr int kSysAux = 1 | 16;  // cache-policy bits sc0 | sc1 (gfx940+ CPol)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const char* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+}
+
+template <int P>
+__device__ __forceinline__ u32x4 ld16(const char* base, int64_t off) {
+  if constexpr (P == kNT) return __builtin_nontemporal_load((const u32x4*)(base + off));
+  else if constexpr (P == kSys)
+    return __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base), (int)off, 0, kSysAux);
+  else return *(const u32x4*)(base + off);
+}
+template <int P>
+__device__ __forceinline__ void st16(char* base, int64_t off, u32x4 v) {
+  if constexpr (P == kNT) __builtin_nontemporal_store(v, (u32x4*)(base + off));
+  else if constexpr (P == kSys) __builtin_amdgcn_raw_buffer_store_b128(v, sys_rsrc(base), (int)off, 0, kSysAux);
+  else *(u32x4*)(base + off) = v;
+}
+
+// Element-sized accesses (T = 1, 2, 4 or 8 bytes), same policies.
+template <int P, typename T>
+__device__ __forceinline__ T ldT(const char* base, int64_t i) {
+  if constexpr (P == kSys) {
+    auto r = sys_rsrc(base);
+    const int off = (int)(i * (int64_t)sizeof(T));
+    if constexpr (sizeof(T) == 1) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, kSysAux));
+    else if constexpr (sizeof(T) == 2) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, kSysAux));
+    else if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSysAux));
+    else return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kSysAux));
+  } else {
+    return ((const T*)base)[i];
+  }
+}
+template <int P, typename T>
+__device__ __forceinline__ void stT(char* base, int64_t i, T v) {
+  if constexpr (P == kSys) {
+    auto r = sys_rsrc(base);
+    const int off = (int)(i * (int64_t)sizeof(T));
+    if constexpr (sizeof(T) == 1) __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), r, off, 0, kSysAux);
+    else if constexpr (sizeof(T) == 2) __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, v), r, off, 0, kSysAux);
+    else if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, kSysAux);
+    else {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, kSysAux);
+    }
+  } else {
+    ((T*)base)[i] = v;
+  }
 }
 
 struct RCArgs {
@@ -57,21 +115,60 @@ __device__ __forceinline__ uint64_t load_op_arg(const void* p, int bytes, uint64
   }
 }
 
-// One pass over `nPacks` 16-byte packs starting at byte offset `base`.
-// NS/ND: compile-time source/destination counts (0 = runtime, <= kMax*).
-template <class Fn, int NS, int ND, int UNROLL, int LD, int ST>
-__device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t base,
-                                         int64_t nPacks, int64_t worker, int64_t nWorkers,
-                                         int tid, int nthreads) {
+// Runtime-index dispatch onto the compile-time policy of operand s / d.
+template <int POLS>
+__device__ __forceinline__ u32x4 ld16_src(const RCArgs& a, int s, int64_t off) {
+  switch (s) {
+    case 0: return ld16<src_pol(POLS, 0)>(a.srcs[0], off);
+    case 1: return ld16<src_pol(POLS, 1)>(a.srcs[1], off);
+    case 2: return ld16<src_pol(POLS, 2)>(a.srcs[2], off);
+    default: return ld16<src_pol(POLS, 3)>(a.srcs[s], off);
+  }
+}
+template <int POLS>
+__device__ __forceinline__ void st16_dst(const RCArgs& a, int d, int64_t off, u32x4 v) {
+  switch (d) {
+    case 0: st16<dst_pol(POLS, 0)>(a.dsts[0], off, v); return;
+    case 1: st16<dst_pol(POLS, 1)>(a.dsts[1], off, v); return;
+    case 2: st16<dst_pol(POLS, 2)>(a.dsts[2], off, v); return;
+    default: st16<dst_pol(POLS, 3)>(a.dsts[d], off, v); return;
+  }
+}
+template <int POLS, typename T>
+__device__ __forceinline__ T ldT_src(const RCArgs& a, int s, int64_t i) {
+  switch (s) {
+    case 0: return ldT<src_pol(POLS, 0), T>(a.srcs[0], i);
+    case 1: return ldT<src_pol(POLS, 1), T>(a.srcs[1], i);
+    case 2: return ldT<src_pol(POLS, 2), T>(a.srcs[2], i);
+    default: return ldT<src_pol(POLS, 3), T>(a.srcs[s], i);
+  }
+}
+template <int POLS, typename T>
+__device__ __forceinline__ void stT_dst(const RCArgs& a, int d, int64_t i, T v) {
+  switch (d) {
+    case 0: stT<dst_pol(POLS, 0), T>(a.dsts[0], i, v); return;
+    case 1: stT<dst_pol(POLS, 1), T>(a.dsts[1], i, v); return;
+    case 2: stT<dst_pol(POLS, 2), T>(a.dsts[2], i, v); return;
+    default: stT<dst_pol(POLS, 3), T>(a.dsts[d], i, v); return;
+  }
+}
+
+// Full hunks over [0, nPacks) packs.  NS/ND: compile-time source/destination
+// counts (0 = runtime, <= kMax*).
+template <class Fn, int NS, int ND, int UNROLL, int POLS>
+__device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t nPacks,
+                                         int64_t worker, int64_t nWorkers, int tid,
+                                         int nthreads) {
   const int nS = NS ? NS : a.nSrcs;
   const int nD = ND ? ND : a.nDsts;
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t nHunks = nPacks / hunkPacks;
   for (int64_t h = worker; h < nHunks; h += nWorkers) {
-    const int64_t off = base + (h * hunkPacks + tid) * 16;
+    const int64_t off = (h * hunkPacks + tid) * 16;
+    const int64_t ustride = (int64_t)nthreads * 16;
     u32x4 acc[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; u++) acc[u] = ld16<LD>(a.srcs[0] + off + (int64_t)u * nthreads * 16);
+    for (int u = 0; u < UNROLL; u++) acc[u] = ld16<src_pol(POLS, 0)>(a.srcs[0], off + u * ustride);
     if (Fn::kPreOp && a.preOpSrcs > 0) {
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) acc[u] = pack_preop(fn, acc[u]);
@@ -79,7 +176,7 @@ __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t 
     auto fold_src = [&](int s) __attribute__((always_inline)) {
       u32x4 tmp[UNROLL];
 #pragma unroll
-      for (int u = 0; u < UNROLL; u++) tmp[u] = ld16<LD>(a.srcs[s] + off + (int64_t)u * nthreads * 16);
+      for (int u = 0; u < UNROLL; u++) tmp[u] = ld16_src<POLS>(a, s, off + u * ustride);
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) {
         if (Fn::kPreOp && s < a.preOpSrcs) tmp[u] = pack_preop(fn, tmp[u]);
@@ -99,7 +196,7 @@ __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t 
     }
     auto store_dst = [&](int d) __attribute__((always_inline)) {
 #pragma unroll
-      for (int u = 0; u < UNROLL; u++) st16<ST>(a.dsts[d] + off + (int64_t)u * nthreads * 16, acc[u]);
+      for (int u = 0; u < UNROLL; u++) st16_dst<POLS>(a, d, off + u * ustride, acc[u]);
     };
     if constexpr (ND > 0) {
 #pragma unroll
@@ -115,20 +212,20 @@ __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t 
 
 // Element-granular path (misaligned pointers and the < 16 B tail),
 // reduceCopyPacks<BytePerPack=sizeof(T)> equivalent.
-template <class Fn>
+template <class Fn, int POLS>
 __device__ __forceinline__ void rc_elems(const Fn& fn, const RCArgs& a, int64_t eBegin,
                                          int64_t eEnd, int64_t gtid, int64_t gthreads) {
   using T = typename Fn::EltType;
   for (int64_t i = eBegin + gtid; i < eEnd; i += gthreads) {
-    T acc = ((const T*)a.srcs[0])[i];
+    T acc = ldT<src_pol(POLS, 0), T>(a.srcs[0], i);
     if (Fn::kPreOp && a.preOpSrcs > 0) acc = fn.preOp(acc);
     for (int s = 1; s < a.nSrcs; s++) {
-      T v = ((const T*)a.srcs[s])[i];
+      T v = ldT_src<POLS, T>(a, s, i);
       if (Fn::kPreOp && s < a.preOpSrcs) v = fn.preOp(v);
       acc = fn.reduce(acc, v);
     }
     if (Fn::kPostOp && a.postOp) acc = fn.postOp(acc);
-    for (int d = 0; d < a.nDsts; d++) ((T*)a.dsts[d])[i] = acc;
+    for (int d = 0; d < a.nDsts; d++) stT_dst<POLS, T>(a, d, i, acc);
   }
 }
 
@@ -142,7 +239,7 @@ __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
 // Full reduce-copy of nElts elements by `nWorkers` cooperating workgroups of
 // `nthreads` threads (this workgroup = `worker`).  Pointers in `a` are the
 // element-0 addresses.  Wave-uniform control flow throughout.
-template <class Fn, int NS, int ND, int UNROLL, int LD, int ST>
+template <class Fn, int NS, int ND, int UNROLL, int POLS>
 __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
                                             int64_t worker, int64_t nWorkers, int tid,
                                             int nthreads) {
@@ -150,30 +247,29 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
   const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
   if (nElts <= 0) return;
   if (!rc_all_aligned16(a)) {
-    rc_elems(fn, a, 0, nElts, gtid, gthreads);
+    rc_elems<Fn, POLS>(fn, a, 0, nElts, gtid, gthreads);
     return;
   }
-  const int64_t nBytes = nElts * (int64_t)sizeof(T);
-  const int64_t nPacks = nBytes / 16;
+  const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t fullPacks = (nPacks / hunkPacks) * hunkPacks;
-  rc_hunks<Fn, NS, ND, UNROLL, LD, ST>(fn, a, 0, fullPacks, worker, nWorkers, tid, nthreads);
+  rc_hunks<Fn, NS, ND, UNROLL, POLS>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
   // Remaining packs (< one hunk): one pack per thread, grid-strided.
   for (int64_t p = fullPacks + gtid; p < nPacks; p += gthreads) {
     const int64_t off = p * 16;
-    u32x4 acc = ld16<LD>(a.srcs[0] + off);
+    u32x4 acc = ld16<src_pol(POLS, 0)>(a.srcs[0], off);
     if (Fn::kPreOp && a.preOpSrcs > 0) acc = pack_preop(fn, acc);
     for (int s = 1; s < a.nSrcs; s++) {
-      u32x4 v = ld16<LD>(a.srcs[s] + off);
+      u32x4 v = ld16_src<POLS>(a, s, off);
       if (Fn::kPreOp && s < a.preOpSrcs) v = pack_preop(fn, v);
       acc = pack_reduce(fn, acc, v);
     }
     if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
-    for (int d = 0; d < a.nDsts; d++) st16<ST>(a.dsts[d] + off, acc);
+    for (int d = 0; d < a.nDsts; d++) st16_dst<POLS>(a, d, off, acc);
   }
   // Element tail (< 16 bytes).
   const int64_t eDone = nPacks * 16 / (int64_t)sizeof(T);
-  if (eDone < nElts) rc_elems(fn, a, eDone, nElts, gtid, gthreads);
+  if (eDone < nElts) rc_elems<Fn, POLS>(fn, a, eDone, nElts, gtid, gthreads);
 }
 
 }  // namespace vccl

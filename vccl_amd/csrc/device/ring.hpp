@@ -67,14 +67,21 @@ struct RingCtx {
       if (RECV) ok = spin_ge(ch->recvTail, recvStep + 1);
       if (SEND && ok && sendStep + 1 > (uint64_t)kSteps) ok = spin_ge(ch->sendHead, sendStep + 1 - kSteps);
       if (!ok) *shAbort = 1;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
-      drain_vmem();
+      if (comm->useFences) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
+        drain_vmem();
+      }
     }
     __syncthreads();
     if (aborted()) return;
     if (nelem > 0) {
+      // Operand order and memory policy: own input streamed once (nt), FIFO
+      // slots system-coherent write-through (sc0 sc1), own output plain.
       constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
       constexpr int ND = (SEND ? 1 : 0) + (DST ? 1 : 0);
+      constexpr int S0 = SRC ? kNT : kSys, S1 = kSys;
+      constexpr int D0 = SEND ? kSys : kPlain, D1 = kPlain;
+      constexpr int POLS = mkpol(S0, S1, S1, S1, D0, D1, D1, D1);
       RCArgs a;
       int s = 0, d = 0;
       if (SRC) a.srcs[s++] = (const char*)src;
@@ -85,13 +92,15 @@ struct RingCtx {
       a.nDsts = ND;
       a.preOpSrcs = SRC ? 1 : 0;
       a.postOp = postOp ? 1 : 0;
-      reduce_copy<Fn, NS, ND, UNROLL, kLdNT, kStPlain>(fn, a, nelem, 0, 1, tid, nthreads);
+      reduce_copy<Fn, NS, ND, UNROLL, POLS>(fn, a, nelem, 0, 1, tid, nthreads);
     }
-    drain_vmem();  // every storing wave: its payload stores are complete
+    drain_vmem();  // every storing wave: its write-through payload stores are complete
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system-scope release
-      drain_vmem();
+      if (comm->useFences) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system-scope release (L2 writeback)
+        drain_vmem();
+      }
       if (SEND) st_sys(ch->nextRecvTail, sendStep + 1);
       if (RECV) st_sys(ch->prevSendHead, recvStep + 1);
     }

@@ -47,6 +47,7 @@ struct DevComm {
   volatile int* abortFlag;           // host-pinned, mapped (ncclCommAbort)
   int* errorFlag;                    // host-pinned, mapped: 1 = spin timeout
   uint64_t spinTimeoutTicks;         // s_memrealtime ticks (100 MHz)
+  int useFences;                     // 1: system acquire/release around each slot
 };
 
 // Per-launch work descriptor (kernel argument, by value).

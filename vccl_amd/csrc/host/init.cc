@@ -120,17 +120,21 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   const auto rings = ring_orders(n);
   const int nRings = (int)rings.size();
   // Channel count: NCCL_NCHANNELS total, else VCCL_CHANNELS_PER_RING x rings.
-  int perRing = (int)param_int("CHANNELS_PER_RING", n == 8 ? 4 : (n == 4 ? 4 : 16));
+  // Defaults from tools/sweep_ring.py (profiles/r01_sweep_ring*.log): a
+  // channel is one workgroup whose throughput is bounded by the per-slot
+  // credit round trip, so bandwidth scales with channels: 8 per ring for the
+  // 8- and 4-GPU ring sets (56 / 48 workgroups), 32 for 2 GPUs.
+  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : 32);
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
   nch = std::max(1, std::min(nch, kMaxChannels));
   c->nChannels = n > 1 ? nch : 0;
-  c->slotBytes = (int)param_int("SLOT_BYTES", 256 << 10);
-  if (c->slotBytes < 4096 || c->slotBytes % 4096) {
-    VWARN("NCCL_SLOT_BYTES must be a multiple of 4096, using 262144");
-    c->slotBytes = 256 << 10;
+  c->slotBytes = (int)param_int("SLOT_BYTES", 512 << 10);
+  if (c->slotBytes < 4096 || c->slotBytes % 4096 || c->slotBytes > (64 << 20)) {
+    VWARN("NCCL_SLOT_BYTES must be a multiple of 4096 up to 64 MiB, using 524288");
+    c->slotBytes = 512 << 10;
   }
-  c->nThreads = (int)param_int("NTHREADS", 512);
-  if (c->nThreads != 256 && c->nThreads != 512 && c->nThreads != 1024) c->nThreads = 512;
+  c->nThreads = (int)param_int("NTHREADS", 1024);
+  if (c->nThreads != 256 && c->nThreads != 512 && c->nThreads != 1024) c->nThreads = 1024;
 
   HIPCHECK(hipHostMalloc((void**)&c->abortFlag, sizeof(int), hipHostMallocMapped));
   HIPCHECK(hipHostMalloc((void**)&c->errorFlag, sizeof(int), hipHostMallocMapped));
@@ -173,6 +177,10 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   HIPCHECK(hipHostGetDevicePointer((void**)&dc.abortFlag, (void*)c->abortFlag, 0));
   HIPCHECK(hipHostGetDevicePointer((void**)&dc.errorFlag, c->errorFlag, 0));
   dc.spinTimeoutTicks = (uint64_t)param_int("SPIN_TIMEOUT_S", 60) * 100000000ull;
+  // FIFO payload moves with sc0 sc1 write-through accesses, so no L2
+  // writeback / invalidate is needed per slot; VCCL_FENCES=1 adds the
+  // system-scope release/acquire fences back (A/B and safety valve).
+  dc.useFences = (int)param_int("FENCES", 0);
   HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));
 
