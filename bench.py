@@ -140,6 +140,8 @@ def _dist_setup():
     # one process per GPU; on a box with fewer GPUs than ranks (rehearsal),
     # ranks share devices round-robin
     torch.cuda.set_device(local % torch.cuda.device_count())
+    if world > torch.cuda.device_count():  # rehearsal on a smaller box only
+        os.environ["VCCL_ALLOW_SHARED_DEVICE"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)

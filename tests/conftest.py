@@ -3,11 +3,6 @@ import sys
 
 import pytest
 
-# One process drives up to 4 ranks on one GPU in the single-process ring tests;
-# each rank's stream needs its own hardware queue for the kernels to be
-# co-resident (HIP default is 4 queues per process).  Read at HIP init.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -35,7 +35,8 @@ os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
 # Several ranks share ONE GPU here, so every rank's channel workgroups must be
 # co-resident: the tests pin a geometry that fits (library defaults are sized
 # for one rank per GPU and are exercised by the 2-process default case).
-TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10)}
+TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10),
+             "VCCL_ALLOW_SHARED_DEVICE": "1"}
 
 
 def _check(ci, n, outs, nch, slot):
@@ -45,7 +46,17 @@ def _check(ci, n, outs, nch, slot):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
 
 
-@pytest.mark.parametrize("n", [2, 3, 4])
+def test_duplicate_device_rejected():
+    # reference init.cc:1782-1786 / :732-735: two ranks on one GPU
+    with pytest.raises(nccl.VcclError) as e:
+        nccl.Comm.init_all([0, 0])
+    assert e.value.code == nccl.ncclInvalidUsage
+
+
+# One process drives n ranks on the single GPU: each rank's stream needs its
+# own hardware queue (HIP default: 4 per process, one taken by the null
+# stream), so n <= 3 here; larger n run as separate processes below.
+@pytest.mark.parametrize("n", [2, 3])
 def test_single_process_ranks(n, monkeypatch):
     for k, v in TEST_GEOM.items():
         monkeypatch.setenv(k, v)
@@ -84,7 +95,7 @@ def test_single_process_ranks(n, monkeypatch):
             c.destroy()
 
 
-@pytest.mark.parametrize("n,geom", [(2, "default"), (8, "test")])
+@pytest.mark.parametrize("n,geom", [(2, "default"), (4, "test"), (8, "test")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
@@ -93,9 +104,10 @@ def test_multi_process_ranks(n, geom):
     if geom == "test":
         env.update(TEST_GEOM)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
-    else:
+    else:  # library defaults (2 ranks x 32 channels x 1024 threads fit on one GPU)
         for k in TEST_GEOM:
             env.pop(k, None)
+        env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         nch, slot = _ring.n_channels(n), 512 << 10
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),

@@ -7,6 +7,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
+os.environ["VCCL_ALLOW_SHARED_DEVICE"] = "1"  # ranks share the one GPU
+
 from vccl_amd import nccl  # noqa: E402
 
 def log(*a):

@@ -23,6 +23,8 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count())
     dist.init_process_group("gloo")
+    if world > torch.cuda.device_count():
+        os.environ["VCCL_ALLOW_SHARED_DEVICE"] = "1"
     nbytes = int(os.environ.get("SWEEP_BYTES", 256 << 20))
     steps = int(os.environ.get("SWEEP_STEPS", 10))
     n = nbytes // 4

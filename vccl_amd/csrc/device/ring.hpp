@@ -35,9 +35,18 @@ struct RingCtx {
 
   // Bounded spin on `flag` until pred(value); returns false on abort/timeout.
   // The timeout is per wait (no progress for spinTimeoutTicks), not per call.
+  __device__ uint64_t poll(const uint64_t* flag) const {
+    // pollMode 1: atomic RMW (resolved at the point of coherence, never a
+    // cached copy); 0: relaxed system-scope load.
+    if (comm->pollMode == 1)
+      return __hip_atomic_fetch_add((uint64_t*)flag, (uint64_t)0, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_SYSTEM);
+    return ld_sys(flag);
+  }
+
   __device__ bool spin_ge(const uint64_t* flag, uint64_t target) {
     uint64_t spins = 0, start = 0;
-    while (ld_sys(flag) < target) {
+    while (poll(flag) < target) {
       __builtin_amdgcn_s_sleep(1);
       if ((++spins & 255) == 0) {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();

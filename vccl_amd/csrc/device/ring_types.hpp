@@ -48,6 +48,7 @@ struct DevComm {
   int* errorFlag;                    // host-pinned, mapped: 1 = spin timeout
   uint64_t spinTimeoutTicks;         // s_memrealtime ticks (100 MHz)
   int useFences;                     // 1: system acquire/release around each slot
+  int pollMode;                      // 0: system-scope load, 1: atomic RMW poll
 };
 
 // Per-launch work descriptor (kernel argument, by value).

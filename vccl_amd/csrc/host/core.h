@@ -68,6 +68,7 @@ struct PeerMap {               // what one rank published about itself
   int pid;
   int device;
   uint64_t hostHash;
+  int64_t busId;               // PCI domain/bus/device: the GPU's identity across processes
   hipIpcMemHandle_t fifoHandle;
   hipIpcMemHandle_t flagHandle;
   char* fifoPtr;               // raw pointers (valid only in the owner process)

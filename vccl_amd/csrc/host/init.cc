@@ -146,6 +146,13 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   me.pid = (int)getpid();
   me.device = c->device;
   me.hostHash = host_hash();
+  {
+    int dom = 0, bus = 0, dev = 0;
+    HIPCHECK(hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device));
+    HIPCHECK(hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device));
+    HIPCHECK(hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, c->device));
+    me.busId = ((int64_t)dom << 16) | (bus << 8) | dev;
+  }
   if (n > 1) {
     const size_t fifoBytes = (size_t)c->nChannels * kSteps * c->slotBytes;
     const size_t flagBytes = (size_t)c->nChannels * 2 * kFlagStride;
@@ -167,6 +174,13 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       VWARN("rank %d is on another node: inter-node transport is out of scope", r);
       return ncclInvalidUsage;
     }
+    // init.cc:732-735: two ranks on one GPU is invalid usage.  The escape
+    // hatch exists for protocol tests on a 1-GPU machine only.
+    if (r != c->rank && c->peers[r].busId == me.busId && !param_int("ALLOW_SHARED_DEVICE", 0)) {
+      VWARN("Duplicate GPU detected : rank %d and rank %d both on device %lx", c->rank, r,
+            (long)me.busId);
+      return ncclInvalidUsage;
+    }
   }
 
   DevComm dc{};
@@ -181,6 +195,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   // writeback / invalidate is needed per slot; VCCL_FENCES=1 adds the
   // system-scope release/acquire fences back (A/B and safety valve).
   dc.useFences = (int)param_int("FENCES", 0);
+  dc.pollMode = (int)param_int("POLL_MODE", 0);
   HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));
 
@@ -320,12 +335,14 @@ VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
   if (!comms || ndev < 1) return ncclInvalidArgument;
   int ndevices = 0;
   HIPCHECK(hipGetDeviceCount(&ndevices));
+  std::vector<int> seen(ndevices, 0);
   for (int i = 0; i < ndev; i++) {
     int d = devlist ? devlist[i] : i;
     if (d < 0 || d >= ndevices) {
-      VWARN("ncclCommInitAll : invalid device %d", d);
+      VWARN("ncclCommInitAll : invalid device %d (totalnDev=%d)", d, ndevices);
       return ncclInvalidArgument;
     }
+    if (seen[d]++ && !param_int("ALLOW_SHARED_DEVICE", 0)) return ncclInvalidUsage;  // init.cc:1782-1786
   }
   ncclUniqueId id;
   NCCLCHECK(bootstrap_get_unique_id(&id));
