@@ -17,6 +17,8 @@ CASES = [
     ("ar_i32_avg", "ar", 4, 2, 40_000),
     ("ar_f64_sum", "ar", 0, 8, 30_001),
     ("ar_f32_sum_inplace", "ar_inplace", 0, 7, 1 << 21),
+    ("ar_f16_sum_inplace_small", "ar_inplace", 0, 6, 4097),
+    ("ar_bf16_sum_ll_edge", "ar", 0, 9, (1 << 19) - 3),
     ("rs_f32_sum", "rs", 0, 7, 65_537),
     ("rs_bf16_avg", "rs", 4, 9, 20_000),
     ("rs_u32_min", "rs", 3, 3, 9_999),
@@ -39,12 +41,18 @@ def gen_input(case_idx, rank, n_ranks):
     return rng.uniform(-1, 1, total).astype(O.NP_DTYPE[dt])
 
 
-def expected(case_idx, n_ranks, nch, slot_bytes):
-    """Per-rank expected outputs."""
+def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0):
+    """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
+    bytes take the one-shot LL path, whose fold is the chain-tree order
+    (oracle ref_chain_fold); larger ones the ring (owner-map ring fold)."""
     name, coll, op, dt, count = CASES[case_idx]
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace"):
-        e = _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
+        if count * ins[0].dtype.itemsize <= ll_max:
+            dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
+            e = O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
+        else:
+            e = _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
         return [e] * n_ranks
     if coll == "rs":
         return _ring.expected_reducescatter(op, dt, ins, nch)

@@ -36,12 +36,13 @@ os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
 # co-resident: the tests pin a geometry that fits (library defaults are sized
 # for one rank per GPU and are exercised by the 2-process default case).
 TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10),
-             "VCCL_ALLOW_SHARED_DEVICE": "1"}
+             "VCCL_ALLOW_SHARED_DEVICE": "1", "VCCL_LL_THRESHOLD": str(1 << 20)}
+LL_DEFAULT = 1 << 20
 
 
-def _check(ci, n, outs, nch, slot):
+def _check(ci, n, outs, nch, slot, ll_max):
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, nch, slot)
+    exp = RC.expected(ci, n, nch, slot, ll_max)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
 
@@ -53,10 +54,11 @@ def test_duplicate_device_rejected():
     assert e.value.code == nccl.ncclInvalidUsage
 
 
-# One process drives n ranks on the single GPU: each rank's stream needs its
-# own hardware queue (HIP default: 4 per process, one taken by the null
-# stream), so n <= 3 here; larger n run as separate processes below.
-@pytest.mark.parametrize("n", [2, 3])
+# One process drives n ranks on the single GPU: the ranks' kernels are only
+# co-resident if their streams land on distinct hardware queues (HIP: 4 per
+# process, assigned round-robin over every stream the process has created),
+# so the single-process case is kept at n = 2; n >= 3 run as processes below.
+@pytest.mark.parametrize("n", [2])
 def test_single_process_ranks(n, monkeypatch):
     for k, v in TEST_GEOM.items():
         monkeypatch.setenv(k, v)
@@ -89,21 +91,26 @@ def test_single_process_ranks(n, monkeypatch):
                 assert c.async_error() == 0, f"{name}: spin timeout (protocol hang)"
             outs = [(xb[r] if coll == "ar_inplace" else yb[r]).cpu().numpy().view(xs[0].dtype)
                     for r in range(n)]
-            _check(ci, n, outs, nch, slot)
+            _check(ci, n, outs, nch, slot, LL_DEFAULT)
     finally:
         for c in comms:
             c.destroy()
 
 
-@pytest.mark.parametrize("n,geom", [(2, "default"), (4, "test"), (8, "test")])
+@pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (8, "test"),
+                                    (8, "ring_only")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
-    if geom == "test":
+    ll_max = LL_DEFAULT
+    if geom in ("test", "ring_only"):
         env.update(TEST_GEOM)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+        if geom == "ring_only":  # NCCL_ALGO forces the ring for every size
+            env["NCCL_ALGO"] = "Ring"
+            ll_max = 0
     else:  # library defaults (2 ranks x 32 channels x 1024 threads fit on one GPU)
         for k in TEST_GEOM:
             env.pop(k, None)
@@ -127,4 +134,4 @@ def test_multi_process_ranks(n, geom):
         assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
-            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot)
+            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max)

@@ -128,3 +128,18 @@ def test_functable_signed_maps_to_unsigned():
                 assert (r1["id"] == r2["id"]) == (kt(r1) == kt(r2)), (r1, r2)
                 checked += 1
     assert checked > 500
+
+
+def test_oracle_chain_fold_order():
+    """Chain-tree LL fold (all_reduce.h:148-229, prims_ll.h:258-266):
+    x_0 (+) (x_1 (+) (... (+) x_{n-1})) with peer (+) own at every hop —
+    restated with numpy's IEEE f32/f16 adds, element by element."""
+    rng = np.random.default_rng(9)
+    for dt, npdt in ((7, np.float32), (6, np.float16)):
+        for n in (2, 3, 8):
+            xs = [rng.uniform(-1, 1, 777).astype(npdt) for _ in range(n)]
+            exp = xs[n - 1].copy()
+            for p in range(n - 2, -1, -1):
+                exp = (exp + xs[p]).astype(npdt)
+            got = O.chain_fold(O.DEV_SUM, dt, 0, False, xs)
+            assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (dt, n)

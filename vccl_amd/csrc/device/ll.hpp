@@ -1,0 +1,153 @@
+// Low-latency (LL) all-reduce for small buckets, MI355X-native.
+//
+// Reference: the intra-node "tree" all-reduce over the LL protocol
+// (all_reduce.h:148-229 runTreeSplit, prims_ll.h:89-128, 224-298): the tree is
+// a chain (graph/connect.cc:64-65), data moves in 16-byte lines carrying two
+// {4 B data, 4 B flag} halves (device.h:46-59), flag = step+1, the receiver
+// polls the line itself (no separate flag / fence), each hop computes
+// peer (+) own, the root applies postOp and the result is broadcast back down.
+//
+// MI355X design: the 8 GPUs are fully connected by xGMI, so instead of
+// 2(n-1) dependent hops the bucket moves ONE hop: every rank writes its input,
+// as LL lines tagged with the call's epoch, into its slot of every peer's LL
+// buffer (sc0 sc1 write-through 16-byte stores; each 8-byte half is one
+// granule), then every rank folds all n inputs locally in the reference's
+// chain order — x_0 (+) (x_1 (+) (... (+) x_{n-1})), preOp on every input,
+// postOp once — so every rank produces the chain-tree result bit-identically.
+// Buffers are double-buffered by epoch parity: a peer can only run one call
+// ahead of us (it needs our contribution to finish), so parity reuse is safe
+// and no buffer is ever cleared.
+#pragma once
+#include "reduce_copy.hpp"
+#include "ring_types.hpp"
+
+namespace vccl {
+
+struct LLWork {
+  DevComm* comm;
+  const void* sendbuff;
+  void* recvbuff;
+  uint64_t count;          // elements
+  uint64_t redArg;
+  const void* redArgPtr;
+  int redArgBytes;
+  int preOp;
+  int nRanks, rank;
+  uint32_t epoch;          // flag value of this call (never 0)
+  int linesPerSlot;        // capacity of one (parity, source) slot
+  char* localBuf;          // my LL buffer: [2 parities][nRanks sources][linesPerSlot] lines
+  char* peerBuf[kMaxRanks];  // every rank's LL buffer mapped here (peerBuf[rank] = local)
+};
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Byte offset of the (parity, source rank) slot inside an LL buffer.
+__host__ __device__ __forceinline__ size_t ll_slot_off(int parity, int src, int nRanks,
+                                                       int linesPerSlot) {
+  return ((size_t)parity * nRanks + src) * (size_t)linesPerSlot * 16;
+}
+
+// 8 data bytes of element stream `p` (bytes [8*line, 8*line+8)), zero padded.
+__device__ __forceinline__ uint64_t ll_load8(const char* p, int64_t line, int64_t nbytes) {
+  const int64_t b = line * 8;
+  if (b + 8 <= nbytes && (((uintptr_t)p + b) & 7) == 0) return *(const uint64_t*)(p + b);
+  uint64_t v = 0;
+  for (int k = 0; k < 8 && b + k < nbytes; k++) v |= (uint64_t)(uint8_t)p[b + k] << (8 * k);
+  return v;
+}
+__device__ __forceinline__ void ll_store8(char* p, int64_t line, int64_t nbytes, uint64_t v) {
+  const int64_t b = line * 8;
+  if (b + 8 <= nbytes && (((uintptr_t)p + b) & 7) == 0) {
+    *(uint64_t*)(p + b) = v;
+    return;
+  }
+  for (int k = 0; k < 8 && b + k < nbytes; k++) p[b + k] = (char)(v >> (8 * k));
+}
+
+template <class Fn>
+__device__ __forceinline__ uint64_t ll_apply(const Fn& fn, uint64_t acc, uint64_t x, int mode) {
+  using T = typename Fn::EltType;
+  union U { uint64_t u; T e[8 / sizeof(T)]; } a, b;
+  a.u = acc;
+  b.u = x;
+#pragma unroll
+  for (int i = 0; i < (int)(8 / sizeof(T)); i++) {
+    if (mode == 0) a.e[i] = fn.reduce(a.e[i], b.e[i]);
+    else if (mode == 1) a.e[i] = fn.preOp(b.e[i]);
+    else a.e[i] = fn.postOp(a.e[i]);
+  }
+  return a.u;
+}
+
+// Poll one LL line until both halves carry `epoch`; returns the 8 data bytes.
+__device__ __forceinline__ bool ll_read_line(const char* line, uint32_t epoch, const DevComm* comm,
+                                             uint64_t* out) {
+  const __amdgpu_buffer_rsrc_t r = sys_rsrc(line);
+  uint64_t spins = 0, start = 0;
+  for (;;) {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, kSysAux);
+    if (v.y == epoch && v.w == epoch) {
+      *out = (uint64_t)v.x | ((uint64_t)v.z << 32);
+      return true;
+    }
+    if ((++spins & 63) == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (start == 0) start = now;
+      if (*comm->abortFlag) return false;
+      if (__hip_atomic_load(comm->errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
+      if (now - start > comm->spinTimeoutTicks) {
+        __hip_atomic_store(comm->errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
+  }
+}
+
+template <class Fn>
+__device__ void ll_allreduce(const LLWork& w) {
+  const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
+  using T = typename Fn::EltType;
+  const int64_t nbytes = (int64_t)w.count * (int64_t)sizeof(T);
+  const int64_t nLines = (nbytes + 7) / 8;
+  const int parity = (int)(w.epoch & 1);
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gthreads = (int64_t)gridDim.x * blockDim.x;
+  const char* in = (const char*)w.sendbuff;
+  const uint32_t e = w.epoch;
+  // Phase 1: publish my input to every peer (one hop over xGMI).
+  for (int64_t l = gtid; l < nLines; l += gthreads) {
+    const uint64_t v = ll_load8(in, l, nbytes);
+    u32x4 line;
+    line.x = (uint32_t)v;
+    line.y = e;
+    line.z = (uint32_t)(v >> 32);
+    line.w = e;
+    for (int k = 1; k < w.nRanks; k++) {
+      const int peer = w.rank + k < w.nRanks ? w.rank + k : w.rank + k - w.nRanks;
+      char* dst = w.peerBuf[peer] + ll_slot_off(parity, w.rank, w.nRanks, w.linesPerSlot) + l * 16;
+      __builtin_amdgcn_raw_buffer_store_b128(line, sys_rsrc(dst), 0, 0, kSysAux);
+    }
+  }
+  // Phase 2: fold all inputs in chain order, x_0 (+) (x_1 (+) (... x_{n-1})).
+  char* out = (char*)w.recvbuff;
+  bool ok = true;
+  for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
+    uint64_t acc = 0;
+    for (int p = w.nRanks - 1; p >= 0 && ok; p--) {
+      uint64_t x;
+      if (p == w.rank) {
+        x = ll_load8(in, l, nbytes);
+      } else {
+        ok = ll_read_line(w.localBuf + ll_slot_off(parity, p, w.nRanks, w.linesPerSlot) + l * 16, e, w.comm, &x);
+        if (!ok) break;
+      }
+      if (Fn::kPreOp && w.preOp) x = ll_apply(fn, 0, x, 1);
+      acc = (p == w.nRanks - 1) ? x : ll_apply(fn, acc, x, 0);  // LL order: peer (+) own
+    }
+    if (!ok) break;
+    if (Fn::kPostOp) acc = ll_apply(fn, acc, 0, 2);
+    ll_store8(out, l, nbytes, acc);
+  }
+}
+
+}  // namespace vccl

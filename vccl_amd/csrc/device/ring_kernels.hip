@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dispatch.hpp"
+#include "ll.hpp"
 #include "ring.hpp"
 #include "ring_launch.hpp"
 
@@ -37,6 +38,24 @@ __global__ __launch_bounds__(1024) void k_ring(RingWork w) {
     ch->recvStep = r.recvStep;
     ch->sendStep = r.sendStep;
   }
+}
+
+template <class Fn>
+__global__ __launch_bounds__(256) void k_ll_allreduce(LLWork w) {
+  ll_allreduce<Fn>(w);
+}
+
+template <>
+hipError_t ll_launch<VCCL_KT>(int devOp, const LLWork& w, int grid, hipStream_t stream) {
+  using T = typename KTypeOf<VCCL_KT>::T;
+  hipError_t err = hipErrorInvalidValue;
+  dispatch_op<T>(devOp, [&]<class Fn>() {
+    if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
+      hipLaunchKernelGGL((k_ll_allreduce<Fn>), dim3(grid), dim3(256), 0, stream, w);
+      err = hipGetLastError();
+    }
+  });
+  return err;
 }
 
 template <>

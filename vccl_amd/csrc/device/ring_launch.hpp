@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "ll.hpp"
 #include "ring_types.hpp"
 
 namespace vccl {
@@ -12,5 +13,9 @@ constexpr int kRingUnroll = 8;
 
 template <int K>
 hipError_t ring_launch(int coll, int devOp, const RingWork& w, int nthreads, hipStream_t stream);
+
+// One-shot LL all-reduce (ll.hpp): 256-thread workgroups, `grid` of them.
+template <int K>
+hipError_t ll_launch(int devOp, const LLWork& w, int grid, hipStream_t stream);
 
 }  // namespace vccl

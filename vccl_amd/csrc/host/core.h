@@ -71,8 +71,10 @@ struct PeerMap {               // what one rank published about itself
   int64_t busId;               // PCI domain/bus/device: the GPU's identity across processes
   hipIpcMemHandle_t fifoHandle;
   hipIpcMemHandle_t flagHandle;
+  hipIpcMemHandle_t llHandle;
   char* fifoPtr;               // raw pointers (valid only in the owner process)
   char* flagPtr;
+  char* llPtr;
 };
 
 struct UserRedOp {             // ncclRedOpCreatePreMulSum state (enqueue.cc:2528-2567)
@@ -93,6 +95,13 @@ struct ncclComm {
   // device resources
   char* fifoBuf = nullptr;     // nChannels * kSteps * slotBytes, uncached
   char* flagBuf = nullptr;     // nChannels * 2 flags * kFlagStride, uncached
+  // one-shot LL all-reduce (ll.hpp): [2 parities][nRanks][llLines] 16 B lines
+  char* llBuf = nullptr;
+  int llLines = 0;             // lines per (parity, source) slot = llMaxBytes / 8
+  size_t llMaxBytes = 0;       // largest all-reduce carried by LL
+  uint32_t llEpoch = 0;
+  std::vector<char*> llPeer;   // every rank's LL buffer mapped into this process
+  int algoForce = 0;           // NCCL_ALGO/NCCL_PROTO: 0 auto, 1 ring/SIMPLE, 2 tree/LL
   vccl::DevComm* devComm = nullptr;
   vccl::DevChannel* devChannels = nullptr;
   volatile int* abortFlag = nullptr;  // host pinned, mapped

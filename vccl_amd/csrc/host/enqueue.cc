@@ -9,6 +9,7 @@
 // done on the device (ring.hpp channel_part).  Group semantics
 // (group.cc:92-110, :393-506): calls between ncclGroupStart/End are queued
 // per thread and launched, in call order, at the outermost ncclGroupEnd.
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -228,6 +229,56 @@ static ncclResult_t launch_ring(const Task& t) {
   return ncclSuccess;
 }
 
+// One-shot LL all-reduce for small buckets (ll.hpp); the chain-tree fold.
+static ncclResult_t launch_ll(const Task& t) {
+  ncclComm* comm = t.comm;
+  LLWork w{};
+  w.comm = comm->devComm;
+  w.sendbuff = t.sendbuff;
+  w.recvbuff = t.recvbuff;
+  w.count = t.count;
+  w.redArg = t.arg;
+  w.redArgPtr = t.argPtr;
+  w.redArgBytes = type_size(t.datatype);
+  w.preOp = t.devOp == OP_PREMULSUM;
+  w.nRanks = comm->nRanks;
+  w.rank = comm->rank;
+  if (++comm->llEpoch == 0) ++comm->llEpoch;  // flag 0 is the cleared state
+  w.epoch = comm->llEpoch;
+  w.linesPerSlot = comm->llLines;
+  w.localBuf = comm->llBuf;
+  for (int r = 0; r < comm->nRanks; r++) w.peerBuf[r] = comm->llPeer[r];
+  const int kt = kernel_type_of(t.devOp, (int)t.datatype);
+  if (kt < 0) return ncclInvalidArgument;
+  const int64_t lines = ((int64_t)t.count * type_size(t.datatype) + 7) / 8;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((lines + 255) / 256, 256));
+  hipError_t e = hipErrorInvalidValue;
+  switch (kt) {
+    case K_U8: e = ll_launch<K_U8>(t.devOp, w, grid, t.stream); break;
+    case K_U32: e = ll_launch<K_U32>(t.devOp, w, grid, t.stream); break;
+    case K_U64: e = ll_launch<K_U64>(t.devOp, w, grid, t.stream); break;
+    case K_F16: e = ll_launch<K_F16>(t.devOp, w, grid, t.stream); break;
+    case K_F32: e = ll_launch<K_F32>(t.devOp, w, grid, t.stream); break;
+    case K_F64: e = ll_launch<K_F64>(t.devOp, w, grid, t.stream); break;
+    case K_BF16: e = ll_launch<K_BF16>(t.devOp, w, grid, t.stream); break;
+  }
+  if (e != hipSuccess) {
+    VWARN("LL kernel launch failed: %s", hipGetErrorString(e));
+    return ncclUnhandledCudaError;
+  }
+  return ncclSuccess;
+}
+
+// Algorithm choice (topoGetAlgoInfo, enqueue.cc:1805-1945, reduced to one
+// node): all-reduce buckets up to llMaxBytes take the one-shot LL path unless
+// NCCL_ALGO / NCCL_PROTO force the ring; everything else takes the ring.
+static bool use_ll(const Task& t) {
+  const ncclComm* c = t.comm;
+  if (t.coll != kAllReduce || c->nRanks < 2 || !c->llBuf || c->algoForce == 1) return false;
+  const size_t bytes = t.count * (size_t)type_size(t.datatype);
+  return bytes <= c->llMaxBytes;
+}
+
 static ncclResult_t launch_task(const Task& t) {
   int old = -1;
   HIPCHECK(hipGetDevice(&old));
@@ -243,6 +294,8 @@ static ncclResult_t launch_task(const Task& t) {
       }
     } else if (t.comm->nRanks == 1) {
       r = launch_one_rank(t);
+    } else if (use_ll(t)) {
+      r = launch_ll(t);
     } else {
       r = launch_ring(t);
     }

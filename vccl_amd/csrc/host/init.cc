@@ -71,6 +71,8 @@ static void free_resources(ncclComm* c) {
   c->ipcOpened.clear();
   if (c->fifoBuf) (void)hipFree(c->fifoBuf);
   if (c->flagBuf) (void)hipFree(c->flagBuf);
+  if (c->llBuf) (void)hipFree(c->llBuf);
+  c->llBuf = nullptr;
   if (c->devComm) (void)hipFree(c->devComm);
   if (c->devChannels) (void)hipFree(c->devChannels);
   if (c->abortFlag) (void)hipHostFree((void*)c->abortFlag);
@@ -85,9 +87,12 @@ static void free_resources(ncclComm* c) {
 }
 
 // Map a peer's buffer into this process/device.
-static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, bool fifo,
+enum { kMapFifo = 0, kMapFlag = 1, kMapLL = 2 };
+static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, int which,
                              char** out) {
-  char* raw = fifo ? p.fifoPtr : p.flagPtr;
+  char* raw = which == kMapFifo ? p.fifoPtr : which == kMapFlag ? p.flagPtr : p.llPtr;
+  const hipIpcMemHandle_t& handle =
+      which == kMapFifo ? p.fifoHandle : which == kMapFlag ? p.flagHandle : p.llHandle;
   if (p.pid == me.pid && p.hostHash == me.hostHash) {
     if (p.device != c->device) {
       hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
@@ -102,8 +107,7 @@ static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, b
     return ncclSuccess;
   }
   void* ptr = nullptr;
-  hipError_t e = hipIpcOpenMemHandle(&ptr, fifo ? p.fifoHandle : p.flagHandle,
-                                     hipIpcMemLazyEnablePeerAccess);
+  hipError_t e = hipIpcOpenMemHandle(&ptr, handle, hipIpcMemLazyEnablePeerAccess);
   if (e != hipSuccess) {
     VWARN("hipIpcOpenMemHandle failed: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
@@ -132,6 +136,13 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   if (c->slotBytes < 4096 || c->slotBytes % 4096 || c->slotBytes > (64 << 20)) {
     VWARN("NCCL_SLOT_BYTES must be a multiple of 4096 up to 64 MiB, using 524288");
     c->slotBytes = 512 << 10;
+  }
+  {
+    const char* algo = getenv("NCCL_ALGO");
+    const char* proto = getenv("NCCL_PROTO");
+    auto has = [](const char* s, const char* w) { return s && strcasestr(s, w) != nullptr; };
+    if (has(proto, "LL") || has(algo, "tree")) c->algoForce = 2;
+    if (has(proto, "simple") || (has(algo, "ring") && !has(algo, "tree"))) c->algoForce = 1;
   }
   c->nThreads = (int)param_int("NTHREADS", 1024);
   if (c->nThreads != 256 && c->nThreads != 512 && c->nThreads != 1024) c->nThreads = 1024;
@@ -164,6 +175,17 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     HIPCHECK(hipIpcGetMemHandle(&me.flagHandle, c->flagBuf));
     me.fifoPtr = c->fifoBuf;
     me.flagPtr = c->flagBuf;
+    // LL buffers for the one-shot small-bucket all-reduce.
+    c->llMaxBytes = (size_t)param_int("LL_THRESHOLD", 1 << 20);
+    c->llMaxBytes = (c->llMaxBytes + 7) / 8 * 8;
+    if (c->llMaxBytes > 0) {
+      c->llLines = (int)(c->llMaxBytes / 8);
+      const size_t llBytes = (size_t)2 * n * c->llLines * 16;
+      NCCLCHECK(alloc_uncached((void**)&c->llBuf, llBytes));
+      HIPCHECK(hipMemset(c->llBuf, 0, llBytes));
+      HIPCHECK(hipIpcGetMemHandle(&me.llHandle, c->llBuf));
+      me.llPtr = c->llBuf;
+    }
   }
   VINFO("rank %d: exchange peer info", c->rank);
   c->peers.assign(n, PeerMap{});
@@ -208,8 +230,15 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
         flagOf[r] = c->flagBuf;
         continue;
       }
-      NCCLCHECK(map_peer(c, me, c->peers[r], true, &fifoOf[r]));
-      NCCLCHECK(map_peer(c, me, c->peers[r], false, &flagOf[r]));
+      NCCLCHECK(map_peer(c, me, c->peers[r], kMapFifo, &fifoOf[r]));
+      NCCLCHECK(map_peer(c, me, c->peers[r], kMapFlag, &flagOf[r]));
+    }
+    c->llPeer.assign(n, nullptr);
+    if (c->llBuf) {
+      for (int r = 0; r < n; r++) {
+        if (r == c->rank) c->llPeer[r] = c->llBuf;
+        else NCCLCHECK(map_peer(c, me, c->peers[r], kMapLL, &c->llPeer[r]));
+      }
     }
     std::vector<DevChannel> chans(c->nChannels);
     const size_t fifoPerCh = (size_t)kSteps * c->slotBytes;
