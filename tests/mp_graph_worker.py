@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""One rank of the HIP-graph capture/replay test (tests/test_gpu_collectives.py).
+
+argv: rank nranks uid_hex
+Captures [LL all-reduce (small), ring all-reduce (large), ring reduce-scatter]
+into one graph, replays it 4 times with new integer-valued inputs (exact in any
+fold order) and checks every output; exit code 0 = all replays correct."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from vccl_amd import nccl  # noqa: E402
+
+
+def main():
+    rank, n = int(sys.argv[1]), int(sys.argv[2])
+    uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
+    torch.cuda.set_device(0)
+    comm = nccl.Comm.init_rank(n, uid, rank)
+    small, large, rc = 10_001, 3 << 20, 100_003
+    xs = torch.empty(small, device="cuda")
+    xl = torch.empty(large, device="cuda")
+    xr = torch.empty(rc * n, device="cuda")
+    ys, yl, yr = torch.empty_like(xs), torch.empty_like(xl), torch.empty(rc, device="cuda")
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s):
+        sp = s.cuda_stream
+        comm.all_reduce(xs.data_ptr(), ys.data_ptr(), small, nccl.ncclFloat32, nccl.ncclSum, sp)
+        comm.all_reduce(xl.data_ptr(), yl.data_ptr(), large, nccl.ncclFloat32, nccl.ncclSum, sp)
+        comm.reduce_scatter(xr.data_ptr(), yr.data_ptr(), rc, nccl.ncclFloat32, nccl.ncclSum, sp)
+    ok = True
+    for it in range(4):
+        def val(r, m):
+            return ((torch.arange(m, device="cuda") * (r + 3) + 7 * it) % 97).float()
+        xs.copy_(val(rank, small))
+        xl.copy_(val(rank, large))
+        xr.copy_(val(rank, rc * n))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        ok &= torch.equal(ys, sum(val(r, small) for r in range(n)))
+        ok &= torch.equal(yl, sum(val(r, large) for r in range(n)))
+        ok &= torch.equal(yr, sum(val(r, rc * n) for r in range(n))[rank * rc:(rank + 1) * rc])
+    ok &= comm.async_error() == 0
+    comm.destroy()
+    sys.exit(0 if ok else 4)
+
+
+if __name__ == "__main__":
+    main()

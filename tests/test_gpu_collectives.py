@@ -135,3 +135,17 @@ def test_multi_process_ranks(n, geom):
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
             _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max)
+
+
+def test_graph_capture_replay():
+    """Collectives captured into a HIP graph replay correctly (device-resident
+    LL epoch and ring step counters; no host state baked into the graph)."""
+    n = 2
+    uid = nccl.get_unique_id()
+    env = dict(os.environ)
+    env.update(TEST_GEOM)
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_graph_worker.py"),
+                               str(r), str(n), nccl.unique_id_to_bytes(uid).hex()], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+    outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+    assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)

@@ -33,7 +33,6 @@ struct LLWork {
   int redArgBytes;
   int preOp;
   int nRanks, rank;
-  uint32_t epoch;          // flag value of this call (never 0)
   int linesPerSlot;        // capacity of one (parity, source) slot
   char* localBuf;          // my LL buffer: [2 parities][nRanks sources][linesPerSlot] lines
   char* peerBuf[kMaxRanks];  // every rank's LL buffer mapped here (peerBuf[rank] = local)
@@ -103,17 +102,36 @@ __device__ __forceinline__ bool ll_read_line(const char* line, uint32_t epoch, c
   }
 }
 
+// Epoch of this call: DevComm::llEpoch + 1 (wrapping past 0, the cleared
+// state).  The last workgroup to finish stores it back for the next call.
+__device__ __forceinline__ uint32_t ll_epoch_of(const DevComm* comm) {
+  uint32_t e = __hip_atomic_load(&comm->llEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  return e == 0 ? 1 : e;
+}
+__device__ __forceinline__ void ll_epoch_retire(DevComm* comm, uint32_t e) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t done = __hip_atomic_fetch_add(&comm->llDone, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(&comm->llDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&comm->llEpoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <class Fn>
 __device__ void ll_allreduce(const LLWork& w) {
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
   using T = typename Fn::EltType;
+  const uint32_t epoch = ll_epoch_of(w.comm);
   const int64_t nbytes = (int64_t)w.count * (int64_t)sizeof(T);
   const int64_t nLines = (nbytes + 7) / 8;
-  const int parity = (int)(w.epoch & 1);
+  const int parity = (int)(epoch & 1);
   const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t gthreads = (int64_t)gridDim.x * blockDim.x;
   const char* in = (const char*)w.sendbuff;
-  const uint32_t e = w.epoch;
+  const uint32_t e = epoch;
   // Phase 1: publish my input to every peer (one hop over xGMI).
   for (int64_t l = gtid; l < nLines; l += gthreads) {
     const uint64_t v = ll_load8(in, l, nbytes);
@@ -148,6 +166,7 @@ __device__ void ll_allreduce(const LLWork& w) {
     if (Fn::kPostOp) acc = ll_apply(fn, acc, 0, 2);
     ll_store8(out, l, nbytes, acc);
   }
+  ll_epoch_retire(w.comm, e);
 }
 
 }  // namespace vccl

@@ -49,6 +49,11 @@ struct DevComm {
   uint64_t spinTimeoutTicks;         // s_memrealtime ticks (100 MHz)
   int useFences;                     // 1: system acquire/release around each slot
   int pollMode;                      // 0: system-scope load, 1: atomic RMW poll
+  // LL call epoch, device-resident so captured graphs replay correctly:
+  // every workgroup reads llEpoch at start; the last one to finish (llDone
+  // ticket) advances it for the next call.
+  uint32_t llEpoch;
+  uint32_t llDone;
 };
 
 // Per-launch work descriptor (kernel argument, by value).

@@ -99,7 +99,6 @@ struct ncclComm {
   char* llBuf = nullptr;
   int llLines = 0;             // lines per (parity, source) slot = llMaxBytes / 8
   size_t llMaxBytes = 0;       // largest all-reduce carried by LL
-  uint32_t llEpoch = 0;
   std::vector<char*> llPeer;   // every rank's LL buffer mapped into this process
   int algoForce = 0;           // NCCL_ALGO/NCCL_PROTO: 0 auto, 1 ring/SIMPLE, 2 tree/LL
   vccl::DevComm* devComm = nullptr;

@@ -243,8 +243,6 @@ static ncclResult_t launch_ll(const Task& t) {
   w.preOp = t.devOp == OP_PREMULSUM;
   w.nRanks = comm->nRanks;
   w.rank = comm->rank;
-  if (++comm->llEpoch == 0) ++comm->llEpoch;  // flag 0 is the cleared state
-  w.epoch = comm->llEpoch;
   w.linesPerSlot = comm->llLines;
   w.localBuf = comm->llBuf;
   for (int r = 0; r < comm->nRanks; r++) w.peerBuf[r] = comm->llPeer[r];
