@@ -53,9 +53,12 @@ typedef struct {
   int blockSize;    /* threads per workgroup: 256, 512 or 1024 */
   int unroll;       /* 16-byte packs in flight per thread per source: 2, 4 or 8 */
   int gridBlocks;   /* workgroups in the grid */
-  int ntLoads;      /* 1 = nontemporal loads */
-  int ntStores;     /* 1 = nontemporal stores */
+  int ntLoads;      /* load policy: 0 plain, 1 nontemporal, 2 sc0 sc1, 3 sc1 nt */
+  int ntStores;     /* store policy: same encoding */
+  int order;        /* hunk order: 0 round-robin, 1 XCD-contiguous */
 } vcclLaunchConfig;
+/* Sweep variants other than the defaults exist only for the 2-source fp32 sum
+ * shape; other shapes always run the tuned default. */
 
 ncclResult_t vcclReduceCopyEx(vcclDevRedOp_t devOp, ncclDataType_t datatype, uint64_t redArg,
                               int preOpSrcs, int postOp, int nSrcs, const void* const* srcs,

@@ -19,7 +19,7 @@ from vccl_amd import nccl  # noqa: E402
 
 def main():
     n = int(os.environ.get("SWEEP_ELEMS", 1 << 26))
-    rounds = int(os.environ.get("SWEEP_ROUNDS", 8))
+    rounds = int(os.environ.get("SWEEP_ROUNDS", 16))
     reps = int(os.environ.get("SWEEP_REPS", 10))
     a = torch.rand(n, device="cuda") * 2 - 1
     b = torch.rand(n, device="cuda") * 2 - 1
@@ -28,15 +28,16 @@ def main():
     s = torch.cuda.current_stream()
     sp = s.cuda_stream
     variants = []
-    for block, unroll, mult, ntl, nts in itertools.product(
-            (256, 512, 1024), (2, 4, 8), (4, 8, 16, 0), (0, 1), (0, 1)):
-        if unroll == 2 and (ntl or nts):
-            continue  # only the plain flavour is instantiated at unroll 2
+    # load/store policy: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1 nt; order 1 = XCD-contiguous hunks
+    for block, unroll, ld, st, order in itertools.product(
+            (256,), (4, 8), (1, 2, 3), (0, 1, 2, 3), (0, 1)):
         hunk = block * unroll * 16
-        full = (n * 4 + hunk - 1) // hunk
-        grid = full if mult == 0 else min(full, 256 * mult)
+        grid = (n * 4 + hunk - 1) // hunk
         variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
-                         "ntLoads": ntl, "ntStores": nts})
+                         "ntLoads": ld, "ntStores": st, "order": order})
+    for grid in (2048, 4096):
+        variants.append({"blockSize": 256, "unroll": 4, "gridBlocks": grid, "ntLoads": 1,
+                          "ntStores": 0, "order": 0})
     variants.append(None)  # library default
     variants.append("torch_add")  # known-good reference on the same hardware: torch.add(a, b, out=d)
     times = {i: [] for i in range(len(variants))}

@@ -65,7 +65,7 @@ inline bool dispatch_op(int devOp, F&& f) {
 
 // Launch geometry shared by the launchers.
 struct LaunchGeom {
-  int block, unroll, grid, ntLoads, ntStores;
+  int block, unroll, grid, ntLoads, ntStores, order;
 };
 
 }  // namespace vccl

@@ -17,11 +17,12 @@ constexpr int kRcDefUnroll = 4;
 constexpr int kRcMaxGrid = 65536;
 constexpr int kRcDefLd = kLdNT;
 constexpr int kRcDefSt = kStPlain;
+constexpr int kRcDefOrder = 0;
 
 // Internal entry used by both the C ABI and the one-rank path.  `a` holds the
 // pointers; geometry from cfg (nullptr = defaults).
 struct vcclLaunchConfigLite {
-  int blockSize, unroll, gridBlocks, ntLoads, ntStores;
+  int blockSize, unroll, gridBlocks, ntLoads, ntStores, order;
 };
 hipError_t reduce_copy_launch(int devOp, int datatype, uint64_t redArg, RCArgs a, int64_t nElts,
                               const vcclLaunchConfigLite* cfg, hipStream_t stream);

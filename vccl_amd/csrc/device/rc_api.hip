@@ -28,8 +28,10 @@ hipError_t reduce_copy_launch(int devOp, int datatype, uint64_t redArg, RCArgs a
   lg.unroll = (cfg && cfg->unroll) ? cfg->unroll : kRcDefUnroll;
   if (lg.block != 256 && lg.block != 512 && lg.block != 1024) return hipErrorInvalidValue;
   if (lg.unroll != 2 && lg.unroll != 4 && lg.unroll != 8) return hipErrorInvalidValue;
-  lg.ntLoads = cfg ? cfg->ntLoads : (kRcDefLd == kLdNT);
-  lg.ntStores = cfg ? cfg->ntStores : (kRcDefSt == kStNT);
+  lg.ntLoads = cfg ? cfg->ntLoads : kRcDefLd;
+  lg.ntStores = cfg ? cfg->ntStores : kRcDefSt;
+  lg.order = cfg ? cfg->order : kRcDefOrder;
+  if (lg.ntLoads < 0 || lg.ntLoads > 3 || lg.ntStores < 0 || lg.ntStores > 3) return hipErrorInvalidValue;
   const int64_t bytes = nElts * elt_size_of_kt(k);
   const int64_t hunk = (int64_t)lg.block * lg.unroll * 16;
   const int64_t want = (bytes + hunk - 1) / hunk;
@@ -75,7 +77,8 @@ extern "C" ncclResult_t vcclReduceCopyEx(vcclDevRedOp_t devOp, ncclDataType_t da
   a.postOp = postOp ? 1 : 0;
   a.argPtr = nullptr;
   vcclLaunchConfigLite lite;
-  if (cfg) lite = {cfg->blockSize, cfg->unroll, cfg->gridBlocks, cfg->ntLoads, cfg->ntStores};
+  if (cfg) lite = {cfg->blockSize, cfg->unroll, cfg->gridBlocks, cfg->ntLoads, cfg->ntStores,
+                   cfg->order};
   hipError_t err = reduce_copy_launch((int)devOp, (int)datatype, redArg, a, (int64_t)nElts,
                                       cfg ? &lite : nullptr, stream);
   if (err == hipErrorInvalidValue) return ncclInvalidArgument;

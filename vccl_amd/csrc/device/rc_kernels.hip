@@ -13,40 +13,61 @@
 
 namespace vccl {
 
-template <class Fn, int NS, int ND, int UNROLL, int LD, int ST>
+template <class Fn, int NS, int ND, int UNROLL, int LD, int ST, int ORDER>
 __global__ __launch_bounds__(1024) void k_reduce_copy(RCArgs a, int64_t nElts, uint64_t redArg) {
   Fn fn(load_op_arg(a.argPtr, a.argBytes, redArg));
-  reduce_copy<Fn, NS, ND, UNROLL, uniform_pol(LD, ST)>(fn, a, nElts, blockIdx.x, gridDim.x, threadIdx.x,
-                                          blockDim.x);
+  reduce_copy<Fn, NS, ND, UNROLL, uniform_pol(LD, ST), ORDER>(fn, a, nElts, blockIdx.x, gridDim.x,
+                                                           threadIdx.x, blockDim.x);
+}
+
+// Launch one instantiation.
+template <class Fn, int NS, int ND, int U, int L, int S, int O>
+static hipError_t launch_one(const RCArgs& a, int64_t nElts, uint64_t redArg, const LaunchGeom& lg,
+                             hipStream_t s) {
+  hipLaunchKernelGGL((k_reduce_copy<Fn, NS, ND, U, L, S, O>), dim3(lg.grid), dim3(lg.block), 0, s,
+                     a, nElts, redArg);
+  return hipGetLastError();
+}
+
+// Sweep dispatch (benchmark shape only): unroll {2,4,8} x load policy
+// {plain, nt, sys, sc1nt} x store policy {plain, nt, sys, sc1nt} x order {0,1}.
+template <class Fn, int NS, int ND, int U>
+static hipError_t sweep_ls(const RCArgs& a, int64_t n, uint64_t r, const LaunchGeom& lg,
+                           hipStream_t s) {
+  auto by_order = [&]<int L, int S>() -> hipError_t {
+    if (lg.order == 1) return launch_one<Fn, NS, ND, U, L, S, 1>(a, n, r, lg, s);
+    return launch_one<Fn, NS, ND, U, L, S, 0>(a, n, r, lg, s);
+  };
+  auto by_store = [&]<int L>() -> hipError_t {
+    switch (lg.ntStores) {
+      case 1: return by_order.template operator()<L, kNT>();
+      case 2: return by_order.template operator()<L, kSys>();
+      case 3: return by_order.template operator()<L, kSc1NT>();
+      default: return by_order.template operator()<L, kPlain>();
+    }
+  };
+  switch (lg.ntLoads) {
+    case 1: return by_store.template operator()<kNT>();
+    case 2: return by_store.template operator()<kSys>();
+    case 3: return by_store.template operator()<kSc1NT>();
+    default: return by_store.template operator()<kPlain>();
+  }
 }
 
 template <class Fn, int NS, int ND>
 static hipError_t launch_nsnd(const RCArgs& a, int64_t nElts, uint64_t redArg,
                               const LaunchGeom& lg, hipStream_t s) {
-  dim3 g(lg.grid), b(lg.block);
   // Only the benchmark shape (2-src f32 sum) carries the full sweep set; every
-  // other functor gets the default geometry (keeps the code object small).
+  // other functor gets the tuned default (keeps the code object small).
   constexpr bool kSweep = std::is_same<Fn, FnSum<float>>::value && NS == 2 && ND == 1;
-#define VCCL_RC_LAUNCH(U, L, S)                                                             \
-  hipLaunchKernelGGL((k_reduce_copy<Fn, NS, ND, U, L, S>), g, b, 0, s, a, nElts, redArg); \
-  return hipGetLastError();
   if constexpr (!kSweep) {
-    VCCL_RC_LAUNCH(kRcDefUnroll, kRcDefLd, kRcDefSt)
+    return launch_one<Fn, NS, ND, kRcDefUnroll, kRcDefLd, kRcDefSt, kRcDefOrder>(a, nElts, redArg,
+                                                                                 lg, s);
   } else {
-    const int ntl = lg.ntLoads, nts = lg.ntStores;
-    if (lg.unroll == 8) {
-      if (ntl && nts) { VCCL_RC_LAUNCH(8, kLdNT, kStNT) }
-      if (ntl) { VCCL_RC_LAUNCH(8, kLdNT, kStPlain) }
-      if (nts) { VCCL_RC_LAUNCH(8, kLdPlain, kStNT) }
-      VCCL_RC_LAUNCH(8, kLdPlain, kStPlain)
-    }
-    if (lg.unroll == 2) { VCCL_RC_LAUNCH(2, kLdPlain, kStPlain) }
-    if (ntl && nts) { VCCL_RC_LAUNCH(4, kLdNT, kStNT) }
-    if (ntl) { VCCL_RC_LAUNCH(4, kLdNT, kStPlain) }
-    if (nts) { VCCL_RC_LAUNCH(4, kLdPlain, kStNT) }
-    VCCL_RC_LAUNCH(4, kLdPlain, kStPlain)
+    if (lg.unroll == 8) return sweep_ls<Fn, NS, ND, 8>(a, nElts, redArg, lg, s);
+    if (lg.unroll == 2) return sweep_ls<Fn, NS, ND, 2>(a, nElts, redArg, lg, s);
+    return sweep_ls<Fn, NS, ND, 4>(a, nElts, redArg, lg, s);
   }
-#undef VCCL_RC_LAUNCH
 }
 
 template <>

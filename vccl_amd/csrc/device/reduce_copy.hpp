@@ -29,7 +29,7 @@ namespace vccl {
 constexpr int kMaxSrcs = 8;
 constexpr int kMaxDsts = 8;
 
-enum : int { kPlain = 0, kNT = 1, kSys = 2 };
+enum : int { kPlain = 0, kNT = 1, kSys = 2, kSc1NT = 3 };
 // Legacy names used by the launch sweep.
 enum : int { kLdPlain = kPlain, kLdNT = kNT };
 enum : int { kStPlain = kPlain, kStNT = kNT };
@@ -44,6 +44,7 @@ constexpr int src_pol(int POLS, int s) { return (POLS >> (2 * (s < 3 ? s : 3))) 
 constexpr int dst_pol(int POLS, int d) { return (POLS >> (8 + 2 * (d < 3 ? d : 3))) & 3; }
 
 constexpr int kSysAux = 1 | 16;  // cache-policy bits sc0 | sc1 (gfx940+ CPol)
+constexpr int kSc1NTAux = 2 | 16;  // nt | sc1: streamed, L1-bypassing
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const char* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
@@ -54,12 +55,15 @@ __device__ __forceinline__ u32x4 ld16(const char* base, int64_t off) {
   if constexpr (P == kNT) return __builtin_nontemporal_load((const u32x4*)(base + off));
   else if constexpr (P == kSys)
     return __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base), (int)off, 0, kSysAux);
+  else if constexpr (P == kSc1NT)
+    return __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base), (int)off, 0, kSc1NTAux);
   else return *(const u32x4*)(base + off);
 }
 template <int P>
 __device__ __forceinline__ void st16(char* base, int64_t off, u32x4 v) {
   if constexpr (P == kNT) __builtin_nontemporal_store(v, (u32x4*)(base + off));
   else if constexpr (P == kSys) __builtin_amdgcn_raw_buffer_store_b128(v, sys_rsrc(base), (int)off, 0, kSysAux);
+  else if constexpr (P == kSc1NT) __builtin_amdgcn_raw_buffer_store_b128(v, sys_rsrc(base), (int)off, 0, kSc1NTAux);
   else *(u32x4*)(base + off) = v;
 }
 
@@ -155,10 +159,16 @@ __device__ __forceinline__ void stT_dst(const RCArgs& a, int d, int64_t i, T v) 
 
 // Full hunks over [0, nPacks) packs.  NS/ND: compile-time source/destination
 // counts (0 = runtime, <= kMax*).
-template <class Fn, int NS, int ND, int UNROLL, int POLS>
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0>
 __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t nPacks,
                                          int64_t worker, int64_t nWorkers, int tid,
                                          int nthreads) {
+  // ORDER 1: workgroups b, b+8, b+16, ... (one XCD under round-robin
+  // dispatch) take consecutive hunks, so each XCD streams one contiguous
+  // eighth of the buffer (speed only: any placement is correct).
+  if constexpr (ORDER == 1) {
+    if (nWorkers % 8 == 0) worker = (worker % 8) * (nWorkers / 8) + worker / 8;
+  }
   const int nS = NS ? NS : a.nSrcs;
   const int nD = ND ? ND : a.nDsts;
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
@@ -239,7 +249,7 @@ __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
 // Full reduce-copy of nElts elements by `nWorkers` cooperating workgroups of
 // `nthreads` threads (this workgroup = `worker`).  Pointers in `a` are the
 // element-0 addresses.  Wave-uniform control flow throughout.
-template <class Fn, int NS, int ND, int UNROLL, int POLS>
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0>
 __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
                                             int64_t worker, int64_t nWorkers, int tid,
                                             int nthreads) {
@@ -253,7 +263,7 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
   const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t fullPacks = (nPacks / hunkPacks) * hunkPacks;
-  rc_hunks<Fn, NS, ND, UNROLL, POLS>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
+  rc_hunks<Fn, NS, ND, UNROLL, POLS, ORDER>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
   // Remaining packs (< one hunk): one pack per thread, grid-strided.
   for (int64_t p = fullPacks + gtid; p < nPacks; p += gthreads) {
     const int64_t off = p * 16;

@@ -56,7 +56,7 @@ class ncclUniqueId(ctypes.Structure):
 class vcclLaunchConfig(ctypes.Structure):
     _fields_ = [("blockSize", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("gridBlocks", ctypes.c_int), ("ntLoads", ctypes.c_int),
-                ("ntStores", ctypes.c_int)]
+                ("ntStores", ctypes.c_int), ("order", ctypes.c_int)]
 
 
 _lib = None
