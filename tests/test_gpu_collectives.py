@@ -116,6 +116,7 @@ def test_multi_process_ranks(n, geom):
             env.pop(k, None)
         env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         nch, slot = _ring.n_channels(n), 512 << 10
+        ll_max = (256 << 10) if n <= 2 else (1 << 20)
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
                                    str(r), str(n), "0", hexid, d], env=env,

@@ -176,7 +176,9 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     me.fifoPtr = c->fifoBuf;
     me.flagPtr = c->flagBuf;
     // LL buffers for the one-shot small-bucket all-reduce.
-    c->llMaxBytes = (size_t)param_int("LL_THRESHOLD", 1 << 20);
+    // LL vs ring crossover (profiles/r01_sweep_ar_2rank_*.log): the ring pays
+    // 2(n-1) dependent hops, LL one hop but (n-1)x the bytes per rank.
+    c->llMaxBytes = (size_t)param_int("LL_THRESHOLD", n <= 2 ? (256 << 10) : (1 << 20));
     c->llMaxBytes = (c->llMaxBytes + 7) / 8 * 8;
     if (c->llMaxBytes > 0) {
       c->llLines = (int)(c->llMaxBytes / 8);
