@@ -28,16 +28,21 @@ def main():
     s = torch.cuda.current_stream()
     sp = s.cuda_stream
     variants = []
-    # load/store policy: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1 nt; order 1 = XCD-contiguous hunks
-    for block, unroll, ld, st, order in itertools.product(
-            (256,), (4, 8), (1, 2, 3), (0, 1, 2, 3), (0, 1)):
-        hunk = block * unroll * 16
-        grid = (n * 4 + hunk - 1) // hunk
-        variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
-                         "ntLoads": ld, "ntStores": st, "order": order})
-    for grid in (2048, 4096):
-        variants.append({"blockSize": 256, "unroll": 4, "gridBlocks": grid, "ntLoads": 1,
-                          "ntStores": 0, "order": 0})
+    mode = os.environ.get("SWEEP_MODE", "policies")
+    if mode == "policies":
+        # load/store policy: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1 nt; order 1 = XCD-contiguous hunks
+        for block, unroll, ld, st, order in itertools.product(
+                (256,), (4, 8), (1, 2, 3), (0, 1, 2, 3), (0, 1)):
+            hunk = block * unroll * 16
+            grid = (n * 4 + hunk - 1) // hunk
+            variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
+                             "ntLoads": ld, "ntStores": st, "order": order})
+    else:  # geometry around the tuned policies (nt loads, sc0 sc1 stores)
+        for block, unroll, per in itertools.product((256, 512, 1024), (2, 4, 8), (1, 2, 4)):
+            hunk = block * unroll * 16
+            grid = max(1, (n * 4 + hunk - 1) // hunk // per)
+            variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
+                             "ntLoads": 1, "ntStores": 2, "order": 0})
     variants.append(None)  # library default
     variants.append("torch_add")  # known-good reference on the same hardware: torch.add(a, b, out=d)
     times = {i: [] for i in range(len(variants))}

@@ -10,11 +10,11 @@ namespace vccl {
 
 // Library defaults for the grid-wide reduce-copy, from the interleaved sweeps
 // of tools/sweep_rc.py on MI355X (profiles/r01_sweep_rc*.log):
-// 256 threads, 4 x 16 B per thread per source, one hunk per workgroup (no
+// 256 threads, 2 x 16 B per thread per source, one hunk per workgroup (no
 // grid-stride below kRcMaxGrid), nontemporal loads, sc0 sc1 write-through
 // stores (the destination line is not kept in L2: +6.6 % over plain stores).
 constexpr int kRcDefBlock = 256;
-constexpr int kRcDefUnroll = 4;
+constexpr int kRcDefUnroll = 2;
 constexpr int kRcMaxGrid = 65536;
 constexpr int kRcDefLd = kLdNT;
 constexpr int kRcDefSt = kSys;
