@@ -147,20 +147,41 @@ __device__ void ll_allreduce(const LLWork& w) {
     }
   }
   // Phase 2: fold all inputs in chain order, x_0 (+) (x_1 (+) (... x_{n-1})).
+  // Loads for up to kLLBatch sources of a line are issued together (their
+  // latencies overlap); a source whose line has not arrived yet is re-polled.
+  constexpr int kLLBatch = 8;
   char* out = (char*)w.recvbuff;
   bool ok = true;
   for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
     uint64_t acc = 0;
-    for (int p = w.nRanks - 1; p >= 0 && ok; p--) {
-      uint64_t x;
-      if (p == w.rank) {
-        x = ll_load8(in, l, nbytes);
-      } else {
-        ok = ll_read_line(w.localBuf + ll_slot_off(parity, p, w.nRanks, w.linesPerSlot) + l * 16, e, w.comm, &x);
-        if (!ok) break;
+    for (int hi = w.nRanks - 1; hi >= 0 && ok; hi -= kLLBatch) {
+      const int lo = hi - kLLBatch + 1 > 0 ? hi - kLLBatch + 1 : 0;
+      u32x4 v[kLLBatch];
+#pragma unroll
+      for (int b = 0; b < kLLBatch; b++) {
+        const int p = hi - b;
+        if (p >= lo && p != w.rank)
+          v[b] = __builtin_amdgcn_raw_buffer_load_b128(
+              sys_rsrc(w.localBuf + ll_slot_off(parity, p, w.nRanks, w.linesPerSlot) + l * 16), 0, 0,
+              kSysAux);
       }
-      if (Fn::kPreOp && w.preOp) x = ll_apply(fn, 0, x, 1);
-      acc = (p == w.nRanks - 1) ? x : ll_apply(fn, acc, x, 0);  // LL order: peer (+) own
+#pragma unroll
+      for (int b = 0; b < kLLBatch; b++) {
+        const int p = hi - b;
+        if (p < lo) break;
+        uint64_t x;
+        if (p == w.rank) {
+          x = ll_load8(in, l, nbytes);
+        } else if (v[b].y == e && v[b].w == e) {
+          x = (uint64_t)v[b].x | ((uint64_t)v[b].z << 32);
+        } else {
+          ok = ll_read_line(w.localBuf + ll_slot_off(parity, p, w.nRanks, w.linesPerSlot) + l * 16, e,
+                            w.comm, &x);
+          if (!ok) break;
+        }
+        if (Fn::kPreOp && w.preOp) x = ll_apply(fn, 0, x, 1);
+        acc = (p == w.nRanks - 1) ? x : ll_apply(fn, acc, x, 0);  // LL order: peer (+) own
+      }
     }
     if (!ok) break;
     if (Fn::kPostOp) acc = ll_apply(fn, acc, 0, 2);

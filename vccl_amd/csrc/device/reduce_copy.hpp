@@ -119,6 +119,24 @@ __device__ __forceinline__ uint64_t load_op_arg(const void* p, int bytes, uint64
   }
 }
 
+// Operand pointers by runtime index, through constant indices only: a dynamic
+// index into the by-value kernel argument would force a private (scratch)
+// copy of RCArgs.
+__device__ __forceinline__ const char* src_ptr(const RCArgs& a, int s) {
+  switch (s) {
+    case 0: return a.srcs[0]; case 1: return a.srcs[1]; case 2: return a.srcs[2];
+    case 3: return a.srcs[3]; case 4: return a.srcs[4]; case 5: return a.srcs[5];
+    case 6: return a.srcs[6]; default: return a.srcs[7];
+  }
+}
+__device__ __forceinline__ char* dst_ptr(const RCArgs& a, int d) {
+  switch (d) {
+    case 0: return a.dsts[0]; case 1: return a.dsts[1]; case 2: return a.dsts[2];
+    case 3: return a.dsts[3]; case 4: return a.dsts[4]; case 5: return a.dsts[5];
+    case 6: return a.dsts[6]; default: return a.dsts[7];
+  }
+}
+
 // Runtime-index dispatch onto the compile-time policy of operand s / d.
 template <int POLS>
 __device__ __forceinline__ u32x4 ld16_src(const RCArgs& a, int s, int64_t off) {
@@ -126,7 +144,7 @@ __device__ __forceinline__ u32x4 ld16_src(const RCArgs& a, int s, int64_t off) {
     case 0: return ld16<src_pol(POLS, 0)>(a.srcs[0], off);
     case 1: return ld16<src_pol(POLS, 1)>(a.srcs[1], off);
     case 2: return ld16<src_pol(POLS, 2)>(a.srcs[2], off);
-    default: return ld16<src_pol(POLS, 3)>(a.srcs[s], off);
+    default: return ld16<src_pol(POLS, 3)>(src_ptr(a, s), off);
   }
 }
 template <int POLS>
@@ -135,7 +153,7 @@ __device__ __forceinline__ void st16_dst(const RCArgs& a, int d, int64_t off, u3
     case 0: st16<dst_pol(POLS, 0)>(a.dsts[0], off, v); return;
     case 1: st16<dst_pol(POLS, 1)>(a.dsts[1], off, v); return;
     case 2: st16<dst_pol(POLS, 2)>(a.dsts[2], off, v); return;
-    default: st16<dst_pol(POLS, 3)>(a.dsts[d], off, v); return;
+    default: st16<dst_pol(POLS, 3)>(dst_ptr(a, d), off, v); return;
   }
 }
 template <int POLS, typename T>
@@ -144,7 +162,7 @@ __device__ __forceinline__ T ldT_src(const RCArgs& a, int s, int64_t i) {
     case 0: return ldT<src_pol(POLS, 0), T>(a.srcs[0], i);
     case 1: return ldT<src_pol(POLS, 1), T>(a.srcs[1], i);
     case 2: return ldT<src_pol(POLS, 2), T>(a.srcs[2], i);
-    default: return ldT<src_pol(POLS, 3), T>(a.srcs[s], i);
+    default: return ldT<src_pol(POLS, 3), T>(src_ptr(a, s), i);
   }
 }
 template <int POLS, typename T>
@@ -153,7 +171,7 @@ __device__ __forceinline__ void stT_dst(const RCArgs& a, int d, int64_t i, T v) 
     case 0: stT<dst_pol(POLS, 0), T>(a.dsts[0], i, v); return;
     case 1: stT<dst_pol(POLS, 1), T>(a.dsts[1], i, v); return;
     case 2: stT<dst_pol(POLS, 2), T>(a.dsts[2], i, v); return;
-    default: stT<dst_pol(POLS, 3), T>(a.dsts[d], i, v); return;
+    default: stT<dst_pol(POLS, 3), T>(dst_ptr(a, d), i, v); return;
   }
 }
 
@@ -241,8 +259,8 @@ __device__ __forceinline__ void rc_elems(const Fn& fn, const RCArgs& a, int64_t 
 
 __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
   uintptr_t bits = 0;
-  for (int s = 0; s < a.nSrcs; s++) bits |= (uintptr_t)a.srcs[s];
-  for (int d = 0; d < a.nDsts; d++) bits |= (uintptr_t)a.dsts[d];
+  for (int s = 0; s < a.nSrcs; s++) bits |= (uintptr_t)src_ptr(a, s);
+  for (int d = 0; d < a.nDsts; d++) bits |= (uintptr_t)dst_ptr(a, d);
   return (bits & 15) == 0;
 }
 
