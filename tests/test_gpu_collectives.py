@@ -36,7 +36,8 @@ os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
 # co-resident: the tests pin a geometry that fits (library defaults are sized
 # for one rank per GPU and are exercised by the 2-process default case).
 TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10),
-             "VCCL_ALLOW_SHARED_DEVICE": "1", "VCCL_LL_THRESHOLD": str(1 << 20)}
+             "VCCL_ALLOW_SHARED_DEVICE": "1", "VCCL_LL_THRESHOLD": str(1 << 20),
+             "VCCL_LL_MAX_BLOCKS": "32"}
 LL_DEFAULT = 1 << 20
 
 

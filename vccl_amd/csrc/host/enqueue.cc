@@ -249,11 +249,11 @@ static ncclResult_t launch_ll(const Task& t) {
   const int kt = kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
   const int64_t lines = ((int64_t)t.count * type_size(t.datatype) + 7) / 8;
-  // A small persistent grid (<= VCCL_LL_MAX_BLOCKS workgroups, each thread
+  // A bounded grid (<= VCCL_LL_MAX_BLOCKS 256-thread workgroups, each thread
   // looping over lines): every rank's LL workgroups must be resident at once
-  // for the peers' spins to complete, so the grid stays far below a GPU's
-  // residency even beside concurrent compute kernels.
-  const int maxBlocks = (int)std::max<int64_t>(1, param_int("LL_MAX_BLOCKS", 64));
+  // for the peers' spins to complete; 256 x 4 waves is 1/8 of a GPU's
+  // residency.  Tests that put 8 ranks on ONE GPU lower it.
+  const int maxBlocks = (int)std::max<int64_t>(1, param_int("LL_MAX_BLOCKS", 256));
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((lines + 255) / 256, maxBlocks));
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
