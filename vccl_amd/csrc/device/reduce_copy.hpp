@@ -238,6 +238,64 @@ __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t 
   (void)nD;
 }
 
+// Software-pipelined variant for compile-time source counts: the loads of
+// hunk h + nWorkers are issued BEFORE the stores of hunk h.  vmcnt counts
+// loads and stores in issue order, so waiting for the next hunk's loads then
+// leaves this hunk's stores in flight instead of draining them — which
+// matters when stores are slow to acknowledge (write-through sc0 sc1 stores
+// to a peer GPU's FIFO over xGMI): without it every iteration pays a full
+// store round trip.
+template <class Fn, int NS, int ND, int UNROLL, int POLS>
+__device__ __forceinline__ void rc_hunks_pipelined(const Fn& fn, const RCArgs& a, int64_t nPacks,
+                                                   int64_t worker, int64_t nWorkers, int tid,
+                                                   int nthreads) {
+  static_assert(NS >= 1 && ND >= 1, "compile-time operand counts only");
+  const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
+  const int64_t nHunks = nPacks / hunkPacks;
+  const int64_t ustride = (int64_t)nthreads * 16;
+  int64_t h = worker;
+  if (h >= nHunks) return;
+  u32x4 cur[NS][UNROLL];
+  auto load_hunk = [&](u32x4 (&v)[NS][UNROLL], int64_t hh) __attribute__((always_inline)) {
+    const int64_t off = (hh * hunkPacks + tid) * 16;
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) v[s][u] = ld16_src<POLS>(a, s, off + u * ustride);
+  };
+  load_hunk(cur, h);
+  for (;;) {
+    const int64_t hn = h + nWorkers;
+    const bool more = hn < nHunks;
+    u32x4 nxt[NS][UNROLL];
+    if (more) load_hunk(nxt, hn);
+    u32x4 acc[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      acc[u] = cur[0][u];
+      if (Fn::kPreOp && a.preOpSrcs > 0) acc[u] = pack_preop(fn, acc[u]);
+#pragma unroll
+      for (int s = 1; s < NS; s++) {
+        u32x4 t = cur[s][u];
+        if (Fn::kPreOp && s < a.preOpSrcs) t = pack_preop(fn, t);
+        acc[u] = pack_reduce(fn, acc[u], t);
+      }
+      if (Fn::kPostOp && a.postOp) acc[u] = pack_postop(fn, acc[u]);
+    }
+    const int64_t off = (h * hunkPacks + tid) * 16;
+#pragma unroll
+    for (int d = 0; d < ND; d++)
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) st16_dst<POLS>(a, d, off + u * ustride, acc[u]);
+    if (!more) break;
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) cur[s][u] = nxt[s][u];
+    h = hn;
+  }
+}
+
 // Element-granular path (misaligned pointers and the < 16 B tail),
 // reduceCopyPacks<BytePerPack=sizeof(T)> equivalent.
 template <class Fn, int POLS>
@@ -267,7 +325,7 @@ __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
 // Full reduce-copy of nElts elements by `nWorkers` cooperating workgroups of
 // `nthreads` threads (this workgroup = `worker`).  Pointers in `a` are the
 // element-0 addresses.  Wave-uniform control flow throughout.
-template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0>
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false>
 __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
                                             int64_t worker, int64_t nWorkers, int tid,
                                             int nthreads) {
@@ -281,7 +339,10 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
   const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t fullPacks = (nPacks / hunkPacks) * hunkPacks;
-  rc_hunks<Fn, NS, ND, UNROLL, POLS, ORDER>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
+  if constexpr (PIPE && NS >= 1 && ND >= 1)
+    rc_hunks_pipelined<Fn, NS, ND, UNROLL, POLS>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
+  else
+    rc_hunks<Fn, NS, ND, UNROLL, POLS, ORDER>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
   // Remaining packs (< one hunk): one pack per thread, grid-strided.
   for (int64_t p = fullPacks + gtid; p < nPacks; p += gthreads) {
     const int64_t off = p * 16;

@@ -101,7 +101,7 @@ struct RingCtx {
       a.nDsts = ND;
       a.preOpSrcs = SRC ? 1 : 0;
       a.postOp = postOp ? 1 : 0;
-      reduce_copy<Fn, NS, ND, UNROLL, POLS>(fn, a, nelem, 0, 1, tid, nthreads);
+      reduce_copy<Fn, NS, ND, UNROLL, POLS, 0, true>(fn, a, nelem, 0, 1, tid, nthreads);
     }
     drain_vmem();  // every storing wave: its write-through payload stores are complete
     __syncthreads();

@@ -9,7 +9,7 @@
 namespace vccl {
 
 enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2 };
-constexpr int kRingUnroll = 4;
+constexpr int kRingUnroll = 2;
 
 template <int K>
 hipError_t ring_launch(int coll, int devOp, const RingWork& w, int nthreads, hipStream_t stream);
