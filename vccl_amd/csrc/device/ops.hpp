@@ -245,6 +245,53 @@ __device__ __forceinline__ u32x4 pack_reduce(const Fn& fn, u32x4 a, u32x4 b) {
   for (int i = 0; i < (int)(16 / sizeof(T)); i++) x.e[i] = fn.reduce(x.e[i], y.e[i]);
   return x.v;
 }
+// u8 sum on whole 32-bit words (SWAR): add the low 7 bits of every byte, then
+// restore each byte's top bit by XOR — per-byte wrap-around, no cross-byte
+// carry (reduce_kernel.h:200-211 computes the same per-byte sum).
+__device__ __forceinline__ uint32_t swar_add_u8(uint32_t a, uint32_t b) {
+  return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnSum<uint8_t>&, u32x4 a, u32x4 b) {
+  return u32x4{swar_add_u8(a.x, b.x), swar_add_u8(a.y, b.y), swar_add_u8(a.z, b.z),
+               swar_add_u8(a.w, b.w)};
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnPreMulSum<uint8_t>&, u32x4 a, u32x4 b) {
+  return pack_reduce(FnSum<uint8_t>(), a, b);
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnSumPostDiv<uint8_t>&, u32x4 a, u32x4 b) {
+  return pack_reduce(FnSum<uint8_t>(), a, b);
+}
+// u8 product / min / max on 16-bit lanes: even and odd bytes are widened into
+// the two halves of a word and run through v_pk_{mul_lo,min}_u16, two bytes
+// per instruction (per-element semantics unchanged: product mod 256, and the
+// xormask-transformed unsigned min of FnMinMax).
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t swar_mul_u8(uint32_t a, uint32_t b) {
+  uint32_t lo = as_u32(as_u16x2(a & 0x00ff00ffu) * as_u16x2(b & 0x00ff00ffu)) & 0x00ff00ffu;
+  uint32_t hi = as_u32(as_u16x2((a >> 8) & 0x00ff00ffu) * as_u16x2((b >> 8) & 0x00ff00ffu));
+  return lo | ((hi & 0x00ff00ffu) << 8);
+}
+__device__ __forceinline__ uint32_t swar_min_u8(uint32_t a, uint32_t b) {
+  uint32_t lo = as_u32(__builtin_elementwise_min(as_u16x2(a & 0x00ff00ffu), as_u16x2(b & 0x00ff00ffu)));
+  uint32_t hi = as_u32(__builtin_elementwise_min(as_u16x2(a & 0xff00ff00u), as_u16x2(b & 0xff00ff00u)));
+  return lo | hi;
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnProd<uint8_t>&, u32x4 a, u32x4 b) {
+  return u32x4{swar_mul_u8(a.x, b.x), swar_mul_u8(a.y, b.y), swar_mul_u8(a.z, b.z),
+               swar_mul_u8(a.w, b.w)};
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnMinMax<uint8_t>& fn, u32x4 a, u32x4 b) {
+  uint32_t m = 0x01010101u * fn.xormask;
+  u32x4 r;
+  r.x = swar_min_u8(a.x ^ m, b.x ^ m) ^ m;
+  r.y = swar_min_u8(a.y ^ m, b.y ^ m) ^ m;
+  r.z = swar_min_u8(a.z ^ m, b.z ^ m) ^ m;
+  r.w = swar_min_u8(a.w ^ m, b.w ^ m) ^ m;
+  return r;
+}
+
 template <class Fn>
 __device__ __forceinline__ u32x4 pack_preop(const Fn& fn, u32x4 a) {
   using T = typename Fn::EltType;
@@ -253,6 +300,10 @@ __device__ __forceinline__ u32x4 pack_preop(const Fn& fn, u32x4 a) {
 #pragma unroll
   for (int i = 0; i < (int)(16 / sizeof(T)); i++) x.e[i] = fn.preOp(x.e[i]);
   return x.v;
+}
+__device__ __forceinline__ u32x4 pack_preop(const FnPreMulSum<uint8_t>& fn, u32x4 a) {
+  uint32_t s = 0x01010101u * fn.scalar;
+  return u32x4{swar_mul_u8(a.x, s), swar_mul_u8(a.y, s), swar_mul_u8(a.z, s), swar_mul_u8(a.w, s)};
 }
 template <class Fn>
 __device__ __forceinline__ u32x4 pack_postop(const Fn& fn, u32x4 a) {
