@@ -3,9 +3,12 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CXXFLAGS := -std=c++20 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
-            --offload-arch=$(ARCH) -I include
-OBJ := build/obj
-LIB := vccl_amd/lib/libvccl.so
+            --offload-arch=$(ARCH) -I include $(DEFS)
+# Experiment builds: `make VARIANT=_x DEFS=-DVCCL_RING_SRC_POL=2` builds
+# vccl_amd/lib/libvccl_x.so (selected at run time with VCCL_LIB=...).
+VARIANT ?=
+OBJ := build/obj$(VARIANT)
+LIB := vccl_amd/lib/libvccl$(VARIANT).so
 DEV := vccl_amd/csrc/device
 HOST := vccl_amd/csrc/host
 KTS := 0 1 2 3 4 5 6

@@ -15,6 +15,10 @@
 #include "reduce_copy.hpp"
 #include "ring_types.hpp"
 
+#ifndef VCCL_RING_SRC_POL
+#define VCCL_RING_SRC_POL kNT  // load policy of the rank's own input in ring steps
+#endif
+
 namespace vccl {
 
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
@@ -88,7 +92,7 @@ struct RingCtx {
       // slots system-coherent write-through (sc0 sc1), own output plain.
       constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
       constexpr int ND = (SEND ? 1 : 0) + (DST ? 1 : 0);
-      constexpr int S0 = SRC ? kNT : kSys, S1 = kSys;
+      constexpr int S0 = SRC ? VCCL_RING_SRC_POL : kSys, S1 = kSys;
       constexpr int D0 = SEND ? kSys : kPlain, D1 = kPlain;
       constexpr int POLS = mkpol(S0, S1, S1, S1, D0, D1, D1, D1);
       RCArgs a;

@@ -11,7 +11,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libvccl.so")
+LIB_PATH = os.environ.get("VCCL_LIB") or os.path.join(_HERE, "lib", "libvccl.so")
 
 # ncclResult_t (nccl.h.in:40-48)
 ncclSuccess, ncclUnhandledCudaError, ncclSystemError, ncclInternalError = 0, 1, 2, 3
