@@ -11,10 +11,12 @@ N > 1 (torch.distributed.run, one process per GPU): BASELINE config 3 at a
   own ring over xGMI peer memory; no RCCL).  value = aggregate bus bandwidth
   = sum over ranks of busbw, busbw = (S/t) * 2(n-1)/n (nccl-tests convention).
   torch.distributed (gloo, CPU tensors) only ships the unique id, barriers and
-  the max-over-ranks time.
+  the max-over-ranks time.  The same run adds `extras` (not `value`): config 3
+  at a few sizes, config 5 (fp16 LL sizes) and config 4 (RS + AG bf16, 4 GiB
+  bucket) — skip with --no-extras.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--bytes S]
-       [--workload reduce_copy|allreduce|rs_ag] [--sweep]
+       [--workload reduce_copy|allreduce|rs_ag] [--sweep] [--no-extras]
 """
 import argparse
 import ctypes
@@ -244,7 +246,12 @@ def peer_copy_bench(dist, rank, world, nbytes=256 << 20, steps=10):
 
 def allreduce_check(dist, comm, rank, world, nbytes=64 << 20):
     """Exactness check on the real topology: integer-valued fp32 inputs
-    (sums exact in any fold order), every rank regenerates all inputs."""
+    (sums exact in any fold order), every rank regenerates all inputs.
+    Checks one LL-protocol size (64 KiB) and one ring size (``nbytes``)."""
+    return all(_allreduce_check_one(dist, comm, rank, world, b) for b in (64 << 10, nbytes))
+
+
+def _allreduce_check_one(dist, comm, rank, world, nbytes):
     sp = torch.cuda.current_stream().cuda_stream
     n = nbytes // 4
     ref = torch.zeros(n, device="cuda")
@@ -286,6 +293,7 @@ def bench_allreduce(args):
         if rank == 0 and args.sweep:
             print(f"# allreduce {n*4:>12d} B  {dt/steps*1e6:10.1f} us  algbw {algbw:8.2f}  "
                   f"busbw {busbw:8.2f} GB/s", file=sys.stderr, flush=True)
+    extras = None if args.sweep or args.no_extras else bench_extras(dist, comm, rank, world, args)
     err = comm.async_error()
     comm.destroy()
     last = rows[-1]
@@ -305,17 +313,52 @@ def bench_allreduce(args):
                         "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
                         "note": f"per-rank busbw vs {links} links x {XGMI_LINK_GBS} GB/s/direction (spec)",
                         "measured_peer_copy": xgmi}}
+    if extras is not None:
+        out["extras"] = extras
     if args.sweep:
         out["sweep"] = [{k: round(v, 3) if isinstance(v, float) else v for k, v in r.items()} for r in rows]
     dist.destroy_process_group()
     return out if rank == 0 else None
 
 
-def bench_rs_ag(args):
-    """BASELINE config 4: reduce-scatter + all-gather bf16 bucket."""
-    dist, rank, world, comm = _dist_setup()
+def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
     sp = torch.cuda.current_stream().cuda_stream
-    S = args.bytes or (4 << 30)
+    tdt, code = {"f32": (torch.float32, nccl.ncclFloat32), "f16": (torch.float16, nccl.ncclFloat16)}[dtype]
+    esz = torch.tensor([], dtype=tdt).element_size()
+    n = max(1, S // esz)
+    g = torch.Generator(device="cuda").manual_seed((1000 if dtype == "f32" else 3000) + rank)
+    x = (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt)
+    y = torch.empty_like(x)
+    dt = _time_coll(dist, lambda: comm.all_reduce(x.data_ptr(), y.data_ptr(), n, code, nccl.ncclSum, sp),
+                    steps, warmup)
+    algbw = n * esz * steps / dt / 1e9
+    return {"bytes": n * esz, "us": round(dt / steps * 1e6, 2),
+            "busbw": round(algbw * 2 * (world - 1) / world, 3)}
+
+
+def bench_extras(dist, comm, rank, world, args):
+    """Secondary BASELINE configs measured in the same multi-GPU run (reported
+    beside the headline, never as ``value``): config 3 at a few sizes (fp32,
+    SIMPLE ring and LL), config 5 (fp16, LL sizes) and config 4 (RS + AG bf16,
+    4 GiB bucket).  Each part records its own error instead of aborting."""
+    ex = {}
+    try:
+        ex["allreduce_f32_sizes"] = [_ar_size_row(dist, comm, rank, world, S, "f32", 20, 5)
+                                     for S in (8, 1 << 10, 8 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20)]
+        ex["allreduce_f16_ll"] = [_ar_size_row(dist, comm, rank, world, S, "f16", 50, 5)
+                                  for S in (8, 1 << 10, 16 << 10, 128 << 10)]
+    except Exception as e:  # noqa: BLE001 - reported, not fatal to the headline
+        ex["allreduce_error"] = repr(e)
+    try:
+        ex["rs_ag_bf16"] = _rs_ag(dist, comm, rank, world, args.rs_ag_bytes, min(args.steps, 10), 2)
+    except Exception as e:  # noqa: BLE001
+        ex["rs_ag_error"] = repr(e)
+    ex["async_error"] = comm.async_error()
+    return ex
+
+
+def _rs_ag(dist, comm, rank, world, S, steps, warmup):
+    sp = torch.cuda.current_stream().cuda_stream
     n = S // 2
     rc = n // world
     g = torch.Generator(device="cuda").manual_seed(2000 + rank)
@@ -328,22 +371,31 @@ def bench_rs_ag(args):
 
     def ag():
         comm.all_gather(shard.data_ptr(), y.data_ptr(), rc, nccl.ncclBfloat16, sp)
-    t_rs = _time_coll(dist, rs, args.steps, args.warmup)
-    t_ag = _time_coll(dist, ag, args.steps, args.warmup)
+    t_rs = _time_coll(dist, rs, steps, warmup)
+    t_ag = _time_coll(dist, ag, steps, warmup)
     frac = (world - 1) / world
-    bw_rs = S * args.steps / t_rs / 1e9 * frac
-    bw_ag = S * args.steps / t_ag / 1e9 * frac
+    del x, y, shard
+    torch.cuda.empty_cache()
+    return {"bytes": S, "steps": steps, "rs_busbw": round(S * steps / t_rs / 1e9 * frac, 2),
+            "ag_busbw": round(S * steps / t_ag / 1e9 * frac, 2),
+            "ms_per_rs_ag": round((t_rs + t_ag) / steps * 1e3, 3)}
+
+
+def bench_rs_ag(args):
+    """BASELINE config 4: reduce-scatter + all-gather bf16 bucket."""
+    dist, rank, world, comm = _dist_setup()
+    r = _rs_ag(dist, comm, rank, world, args.bytes or (4 << 30), args.steps, args.warmup)
     comm.destroy()
     dist.destroy_process_group()
     if rank:
         return None
     return {"metric": "reduce-scatter + all-gather busbw (BASELINE config 4)",
-            "value": round((bw_rs + bw_ag) / 2 * world, 2), "unit": "GB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round((t_rs + t_ag) / args.steps * 1e3, 3), "higher_is_better": True,
+            "value": round((r["rs_busbw"] + r["ag_busbw"]) / 2 * world, 2), "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": r["ms_per_rs_ag"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"workload": f"RS+AG bf16 {S} B bucket", "rs_busbw": round(bw_rs, 2),
-                       "ag_busbw": round(bw_ag, 2)}}
+            "config": {"workload": f"RS+AG bf16 {r['bytes']} B bucket", "rs_busbw": r["rs_busbw"],
+                       "ag_busbw": r["ag_busbw"]}}
 
 
 def main():
@@ -356,6 +408,8 @@ def main():
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-peer", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--rs-ag-bytes", type=int, default=4 << 30)
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)

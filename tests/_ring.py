@@ -110,3 +110,22 @@ def expected_reducescatter(op, dtype, inputs, nch):
             own = np.full(length, ring.index(r), np.int32)
             outs[r][off:off + length] = O.ring_fold(dev_op, dtype, arg, pre, ins, own)
     return outs
+
+
+def direct_shard_elts(count, n, elt_size):
+    """Shard length of the two-shot direct all-reduce (host/enqueue.cc
+    launch_direct): ceil(count / n) rounded up to 16 bytes."""
+    return _align_up(_div_up(count, n), max(1, 16 // elt_size))
+
+
+def expected_direct(op, dtype, inputs):
+    """Direct all-reduce: shard o (owned by rank o) is folded in the ring order
+    of the identity ring, x_{o+1} (+) ... (+) x_o — the ring all-reduce fold
+    with chunk o finishing at ring index o (all_reduce.h:42-64)."""
+    n = len(inputs)
+    dev_op, arg = O.host_to_dev_redop(op, dtype, n)
+    pre = dev_op == O.DEV_PREMULSUM
+    count = inputs[0].size
+    shard = direct_shard_elts(count, n, inputs[0].dtype.itemsize)
+    owner = (np.arange(count) // shard).astype(np.int32)
+    return O.ring_fold(dev_op, dtype, arg, pre, list(inputs), owner)

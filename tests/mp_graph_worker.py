@@ -2,7 +2,8 @@
 """One rank of the HIP-graph capture/replay test (tests/test_gpu_collectives.py).
 
 argv: rank nranks uid_hex
-Captures [LL all-reduce (small), ring all-reduce (large), ring reduce-scatter]
+Captures [LL all-reduce (small), direct all-reduce (mid), ring all-reduce
+(large), ring reduce-scatter]
 into one graph, replays it 4 times with new integer-valued inputs (exact in any
 fold order) and checks every output; exit code 0 = all replays correct."""
 import os
@@ -21,8 +22,10 @@ def main():
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
     torch.cuda.set_device(0)
     comm = nccl.Comm.init_rank(n, uid, rank)
-    small, large, rc = 10_001, 3 << 20, 100_003
+    small, mid, large, rc = 10_001, 600_001, 3 << 20, 100_003
     xs = torch.empty(small, device="cuda")
+    xm = torch.empty(mid, device="cuda")
+    ym = torch.empty_like(xm)
     xl = torch.empty(large, device="cuda")
     xr = torch.empty(rc * n, device="cuda")
     ys, yl, yr = torch.empty_like(xs), torch.empty_like(xl), torch.empty(rc, device="cuda")
@@ -32,6 +35,7 @@ def main():
     with torch.cuda.graph(g, stream=s):
         sp = s.cuda_stream
         comm.all_reduce(xs.data_ptr(), ys.data_ptr(), small, nccl.ncclFloat32, nccl.ncclSum, sp)
+        comm.all_reduce(xm.data_ptr(), ym.data_ptr(), mid, nccl.ncclFloat32, nccl.ncclSum, sp)
         comm.all_reduce(xl.data_ptr(), yl.data_ptr(), large, nccl.ncclFloat32, nccl.ncclSum, sp)
         comm.reduce_scatter(xr.data_ptr(), yr.data_ptr(), rc, nccl.ncclFloat32, nccl.ncclSum, sp)
     ok = True
@@ -39,12 +43,14 @@ def main():
         def val(r, m):
             return ((torch.arange(m, device="cuda") * (r + 3) + 7 * it) % 97).float()
         xs.copy_(val(rank, small))
+        xm.copy_(val(rank, mid))
         xl.copy_(val(rank, large))
         xr.copy_(val(rank, rc * n))
         torch.cuda.synchronize()
         g.replay()
         torch.cuda.synchronize()
         ok &= torch.equal(ys, sum(val(r, small) for r in range(n)))
+        ok &= torch.equal(ym, sum(val(r, mid) for r in range(n)))
         ok &= torch.equal(yl, sum(val(r, large) for r in range(n)))
         ok &= torch.equal(yr, sum(val(r, rc * n) for r in range(n))[rank * rc:(rank + 1) * rc])
     ok &= comm.async_error() == 0

@@ -19,6 +19,13 @@ CASES = [
     ("ar_f32_sum_inplace", "ar_inplace", 0, 7, 1 << 21),
     ("ar_f16_sum_inplace_small", "ar_inplace", 0, 6, 4097),
     ("ar_bf16_sum_ll_edge", "ar", 0, 9, (1 << 19) - 3),
+    # two-shot direct range under the test geometry (1 MiB < bytes <= 4 MiB)
+    ("ar_f32_sum_direct", "ar", 0, 7, 786_433),
+    ("ar_bf16_avg_direct", "ar", 4, 9, 1_200_001),
+    ("ar_i8_max_direct", "ar", 2, 0, 3_000_001),
+    ("ar_f16_sum_inplace_direct", "ar_inplace", 0, 6, 1_000_003),
+    ("ar_i64_sum_direct", "ar", 0, 4, 300_001),
+    ("ar_u32_avg_direct", "ar", 4, 3, 500_007),
     ("rs_f32_sum", "rs", 0, 7, 65_537),
     ("rs_bf16_avg", "rs", 4, 9, 20_000),
     ("rs_u32_min", "rs", 3, 3, 9_999),
@@ -41,16 +48,19 @@ def gen_input(case_idx, rank, n_ranks):
     return rng.uniform(-1, 1, total).astype(O.NP_DTYPE[dt])
 
 
-def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0):
+def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0):
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
-    (oracle ref_chain_fold); larger ones the ring (owner-map ring fold)."""
+    (oracle ref_chain_fold); up to `direct_max` the two-shot direct path
+    (identity-ring fold per shard); larger ones the ring (owner-map ring fold)."""
     name, coll, op, dt, count = CASES[case_idx]
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace"):
         if count * ins[0].dtype.itemsize <= ll_max:
             dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
             e = O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
+        elif count * ins[0].dtype.itemsize <= direct_max:
+            e = _ring.expected_direct(op, dt, ins)
         else:
             e = _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
         return [e] * n_ranks

@@ -1,0 +1,107 @@
+"""CPU simulation of the two-shot direct all-reduce's data movement
+(vccl_amd/csrc/device/direct.hpp, host/enqueue.cc launch_direct).
+
+Replays phases 1-3 with numpy over the same shard / block partition and inbox
+region layout the kernel uses, and checks that (a) every write stays inside
+its inbox region, (b) every output element is produced exactly once per rank,
+and (c) the result equals the oracle fold the GPU parity tests expect
+(tests/_ring.py expected_direct), for ragged counts, every element size and
+n = 2..8.  No GPU needed.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import _ring
+
+MIN_BLK_BYTES = 16 << 10
+
+
+def _geometry(count, n, esz, max_blocks, direct_max):
+    align = max(1, 16 // esz)
+    shard = _ring.direct_shard_elts(count, n, esz)
+    min_blk = MIN_BLK_BYTES // esz
+    nb = max(1, min(-(-shard // min_blk), max_blocks))
+    blk = -(-(-(-shard // nb)) // align) * align
+    n_blocks = -(-shard // blk)
+    region = ((direct_max + n - 1) // n + 16 + 255) // 256 * 256
+    return shard, blk, n_blocks, region
+
+
+def _simulate(op, dtype, inputs, max_blocks=64, direct_max=16 << 20):
+    n = len(inputs)
+    dev_op, arg = O.host_to_dev_redop(op, dtype, n)
+    pre = dev_op == O.DEV_PREMULSUM
+    count = inputs[0].size
+    esz = inputs[0].dtype.itemsize
+    shard, blk, n_blocks, region = _geometry(count, n, esz, max_blocks, direct_max)
+    assert shard * esz <= region and n_blocks <= 128
+    inbox = [[[None] * n for _ in range(2)] for _ in range(n)]  # [rank][phase][src] -> {b: array}
+    for r in range(n):
+        for ph in range(2):
+            for s in range(n):
+                inbox[r][ph][s] = {}
+    outs = [np.zeros_like(inputs[0]) for _ in range(n)]
+    written = [np.zeros(count, np.int32) for _ in range(n)]
+
+    def block_of(o, b):
+        end = min((o + 1) * shard, count)
+        lo = o * shard + b * blk
+        hi = min(lo + blk, end)
+        return lo, max(0, hi - lo)
+
+    for b in range(n_blocks):
+        in_off = b * blk * esz
+        for me in range(n):  # phase 1
+            for k in range(1, n):
+                p = (me + k) % n
+                off, ln = block_of(p, b)
+                assert in_off + ln * esz <= region
+                inbox[p][0][me][b] = inputs[me][off:off + ln].copy()
+        for me in range(n):  # phase 2: srcs x_{me+1}, ..., x_{me-1}, own
+            off, ln = block_of(me, b)
+            ins = [inbox[me][0][(me + j) % n][b] for j in range(1, n)] + [inputs[me][off:off + ln]]
+            if ln:
+                # ring_fold over [x_{me+1}, ..., x_me] with owner = last position
+                own = np.full(ln, n - 1, np.int32)
+                res = O.ring_fold(dev_op, dtype, arg, pre, ins, own)
+            else:
+                res = inputs[me][off:off]
+            outs[me][off:off + ln] = res
+            written[me][off:off + ln] += 1
+            for j in range(1, n):
+                inbox[(me + j) % n][1][me][b] = res.copy()
+        for me in range(n):  # phase 3
+            for k in range(1, n):
+                o = (me + k) % n
+                off, ln = block_of(o, b)
+                outs[me][off:off + ln] = inbox[me][1][o][b]
+                written[me][off:off + ln] += 1
+    for r in range(n):
+        assert (written[r] == 1).all(), "every element produced exactly once"
+    return outs
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("dtype,count", [(7, 786_433), (9, 100_003), (0, 3_001), (4, 5), (6, 70_001)])
+def test_direct_simulation_matches_expected(n, dtype, count):
+    rng = np.random.default_rng(n * 100 + dtype)
+    if dtype in (0, 4):
+        ins = [rng.integers(-100, 100, count).astype(O.NP_DTYPE[dtype]) for _ in range(n)]
+        op = 2  # max
+    elif dtype == 9:
+        ins = [O.f32_to_bf16_bits(rng.uniform(-1, 1, count).astype(np.float32)) for _ in range(n)]
+        op = 0
+    else:
+        ins = [rng.uniform(-1, 1, count).astype(O.NP_DTYPE[dtype]) for _ in range(n)]
+        op = 4 if dtype == 6 else 0  # f16 avg exercises preOp on every input
+    outs = _simulate(op, dtype, ins)
+    exp = _ring.expected_direct(op, dtype, ins)
+    for r in range(n):
+        assert np.array_equal(outs[r].view(np.uint8), exp.view(np.uint8)), f"rank {r}"
+
+
+def test_direct_geometry_small_block_cap():
+    # 16 blocks (the shared-GPU test cap) over an 8-rank 16 MiB bucket
+    shard, blk, nb, region = _geometry((16 << 20) // 4, 8, 4, 16, 16 << 20)
+    assert nb == 16 and shard * 4 <= region and blk % 4 == 0

@@ -37,13 +37,15 @@ os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
 # for one rank per GPU and are exercised by the 2-process default case).
 TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10),
              "VCCL_ALLOW_SHARED_DEVICE": "1", "VCCL_LL_THRESHOLD": str(1 << 20),
-             "VCCL_LL_MAX_BLOCKS": "32"}
+             "VCCL_LL_MAX_BLOCKS": "32", "VCCL_DIRECT_THRESHOLD": str(4 << 20),
+             "VCCL_DIRECT_MAX_BLOCKS": "16"}
 LL_DEFAULT = 1 << 20
+DIRECT_TEST = 4 << 20
 
 
-def _check(ci, n, outs, nch, slot, ll_max):
+def _check(ci, n, outs, nch, slot, ll_max, direct_max):
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, nch, slot, ll_max)
+    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
 
@@ -92,32 +94,44 @@ def test_single_process_ranks(n, monkeypatch):
                 assert c.async_error() == 0, f"{name}: spin timeout (protocol hang)"
             outs = [(xb[r] if coll == "ar_inplace" else yb[r]).cpu().numpy().view(xs[0].dtype)
                     for r in range(n)]
-            _check(ci, n, outs, nch, slot, LL_DEFAULT)
+            _check(ci, n, outs, nch, slot, LL_DEFAULT, DIRECT_TEST)
     finally:
         for c in comms:
             c.destroy()
 
 
 @pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (8, "test"),
-                                    (8, "ring_only")])
+                                    (8, "ring_only"), (4, "direct_only"), (8, "default8")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
-    ll_max = LL_DEFAULT
-    if geom in ("test", "ring_only"):
+    ll_max, direct_max = LL_DEFAULT, DIRECT_TEST
+    if geom in ("test", "ring_only", "direct_only"):
         env.update(TEST_GEOM)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
         if geom == "ring_only":  # NCCL_ALGO forces the ring for every size
             env["NCCL_ALGO"] = "Ring"
+            ll_max = direct_max = 0
+        if geom == "direct_only":  # every all-reduce that fits takes the direct path
+            env["NCCL_ALGO"] = "Direct"
             ll_max = 0
+    elif geom == "default8":
+        # library defaults except the LL grid (8 ranks share the one GPU)
+        for k in TEST_GEOM:
+            env.pop(k, None)
+        env.update(VCCL_ALLOW_SHARED_DEVICE="1", VCCL_LL_MAX_BLOCKS="32",
+                   VCCL_DIRECT_MAX_BLOCKS="16", VCCL_NTHREADS="256", VCCL_CHANNELS_PER_RING="2")
+        nch, slot = _ring.n_channels(n, per_ring=2), 512 << 10
+        ll_max, direct_max = 1 << 20, 16 << 20
     else:  # library defaults (2 ranks x 32 channels x 1024 threads fit on one GPU)
         for k in TEST_GEOM:
             env.pop(k, None)
         env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         nch, slot = _ring.n_channels(n), 512 << 10
         ll_max = (256 << 10) if n <= 2 else (1 << 20)
+        direct_max = 16 << 20
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
                                    str(r), str(n), "0", hexid, d], env=env,
@@ -136,7 +150,7 @@ def test_multi_process_ranks(n, geom):
         assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
-            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max)
+            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max)
 
 
 def test_graph_capture_replay():

@@ -1,0 +1,287 @@
+// Two-shot direct all-reduce over the fully connected xGMI mesh, for
+// mid-size buckets (between the one-shot LL path and the SIMPLE ring).
+//
+// Reference role: the mid-range protocol slot of VCCL's tuner (LL128 ring,
+// prims_ll128.h:11-434, chosen by enqueue.cc:2032 for 64 KiB - 8 MiB).  NCCL
+// fills that slot with a cheaper-per-byte protocol on the SAME 2(n-1)-hop
+// ring; on MI355X every GPU pair has its own xGMI link, so the mid range is
+// served by a different dependency structure instead: two hops in total.
+//
+//   shard o = elements [o*shardElts, (o+1)*shardElts), owned by rank o;
+//   each shard is cut into nBlocks blocks, block b handled by workgroup b
+//   on every rank (so a workgroup only ever waits for its namesakes).
+//   phase 1 (scatter): rank r writes block b of every foreign shard p into
+//            p's inbox region (0, r), then raises flag (0, r, b) at p;
+//   phase 2 (reduce):  rank o waits for the n-1 flags (0, *, b), folds its
+//            block in the reference ring order on the identity ring —
+//            x_{o+1} (+) x_{o+2} (+) ... (+) x_o, preOp on every input,
+//            postOp once (all_reduce.h:42-64 with chunk o finishing at ring
+//            index o) — and writes the result to its own output and to every
+//            peer's inbox region (1, o), then raises flag (1, o, b) there;
+//   phase 3 (gather):  every rank waits for the n-1 flags (1, *, b) and copies
+//            the owners' blocks from its inbox into its output.
+// Payload moves with sc0 sc1 (write-through, L2-bypassing) 16-byte accesses,
+// each storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier
+// and the relaxed system-scope flag store: the same hand-off as the ring
+// slots (ring.hpp).  Flags carry the call epoch (device-resident, see
+// epoch_next), so no buffer is ever cleared and graph replays stay in step.
+//
+// Buffer reuse without double buffering: rank r can rewrite region (0, r),
+// block b at p only in its NEXT call, i.e. after its workgroup b finished
+// phase 3 of this call, which waited for p's flag (1, p, b), which p raised
+// only after reading every region (0, *) block b.  Region (1, o) is
+// rewritten by o only after o received phase-1 data of the next call from
+// the reader, which that reader sends only after its own kernel completed.
+#pragma once
+#include "ll.hpp"
+#include "reduce_copy.hpp"
+#include "ring_types.hpp"
+
+namespace vccl {
+
+constexpr int kDirectMaxRanks = 8;     // phase 2 folds all n inputs in registers
+constexpr int kDirectMaxBlocks = 128;
+constexpr int kDirectFlagStride = 64;  // bytes between flags
+constexpr int kDirectThreads = 512;
+constexpr int kDirectUnroll = 2;
+
+// Every rank's inbox and flag array, mapped into this process (device memory,
+// so runtime peer indices never index a by-value kernel argument).
+struct DirectPeers {
+  char* buf[kDirectMaxRanks];
+  char* flags[kDirectMaxRanks];
+};
+
+struct DirectWork {
+  DevComm* comm;
+  const DirectPeers* peers;
+  const void* sendbuff;
+  void* recvbuff;
+  uint64_t count;        // elements
+  uint64_t redArg;
+  const void* redArgPtr;
+  int redArgBytes;
+  int preOp;
+  int nRanks, rank;
+  int nBlocks;
+  int pad0;
+  int64_t shardElts;     // elements per shard (16-byte multiple)
+  int64_t blkElts;       // elements per block (16-byte multiple)
+  int64_t regionBytes;   // bytes per (phase, rank) inbox region
+};
+
+__host__ __device__ __forceinline__ size_t direct_region_off(int phase, int src, int nRanks,
+                                                             int64_t regionBytes) {
+  return ((size_t)phase * nRanks + src) * (size_t)regionBytes;
+}
+__host__ __device__ __forceinline__ size_t direct_flag_off(int phase, int src, int b) {
+  return (((size_t)phase * kDirectMaxRanks + src) * kDirectMaxBlocks + b) * kDirectFlagStride;
+}
+constexpr size_t kDirectFlagBytes = (size_t)2 * kDirectMaxRanks * kDirectMaxBlocks * kDirectFlagStride;
+
+// Fold up to kDirectMaxRanks sources into up to kDirectMaxRanks destinations:
+// dst_d[i] = postOp(pre?(src_0[i]) (+) pre?(src_1[i]) (+) ...), preOp on
+// sources s < preN.  All sources' loads of a hunk are issued before the first
+// reduce (the inbox latency is paid once per hunk, not once per source).
+// DST_LAST: policy of the last destination (the own output); others kSys.
+template <class Fn, int U, int LDP, int STP, int STP_LAST>
+__device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)[kDirectMaxRanks],
+                                          int nS, int preN, bool post,
+                                          char* const (&dst)[kDirectMaxRanks], int nD,
+                                          int64_t nElts, int tid, int nthreads) {
+  using T = typename Fn::EltType;
+  if (nElts <= 0) return;
+  uintptr_t bits = 0;
+#pragma unroll
+  for (int s = 0; s < kDirectMaxRanks; s++)
+    if (s < nS) bits |= (uintptr_t)src[s];
+#pragma unroll
+  for (int d = 0; d < kDirectMaxRanks; d++)
+    if (d < nD) bits |= (uintptr_t)dst[d];
+  const int64_t nPacks = (bits & 15) == 0 ? nElts * (int64_t)sizeof(T) / 16 : 0;
+  const int64_t hunk = (int64_t)nthreads * U;
+  for (int64_t base = 0; base < nPacks; base += hunk) {
+    u32x4 v[kDirectMaxRanks][U];
+#pragma unroll
+    for (int s = 0; s < kDirectMaxRanks; s++) {
+      if (s < nS) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int64_t p = base + u * nthreads + tid;
+          if (p < nPacks) v[s][u] = ld16<LDP>(src[s], p * 16);
+        }
+      }
+    }
+    u32x4 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      acc[u] = v[0][u];
+      if (Fn::kPreOp && preN > 0) acc[u] = pack_preop(fn, acc[u]);
+#pragma unroll
+      for (int s = 1; s < kDirectMaxRanks; s++) {
+        if (s < nS) {
+          u32x4 t = v[s][u];
+          if (Fn::kPreOp && s < preN) t = pack_preop(fn, t);
+          acc[u] = pack_reduce(fn, acc[u], t);
+        }
+      }
+      if (Fn::kPostOp && post) acc[u] = pack_postop(fn, acc[u]);
+    }
+#pragma unroll
+    for (int d = 0; d < kDirectMaxRanks; d++) {
+      if (d < nD) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int64_t p = base + u * nthreads + tid;
+          if (p < nPacks) {
+            if (d == nD - 1) st16<STP_LAST>(dst[d], p * 16, acc[u]);
+            else st16<STP>(dst[d], p * 16, acc[u]);
+          }
+        }
+      }
+    }
+  }
+  // Element path: misaligned operands or the < 16-byte tail.
+  for (int64_t i = nPacks * 16 / (int64_t)sizeof(T) + tid; i < nElts; i += nthreads) {
+    T acc = ldT<LDP, T>(src[0], i);
+    if (Fn::kPreOp && preN > 0) acc = fn.preOp(acc);
+#pragma unroll
+    for (int s = 1; s < kDirectMaxRanks; s++) {
+      if (s < nS) {
+        T x = ldT<LDP, T>(src[s], i);
+        if (Fn::kPreOp && s < preN) x = fn.preOp(x);
+        acc = fn.reduce(acc, x);
+      }
+    }
+    if (Fn::kPostOp && post) acc = fn.postOp(acc);
+#pragma unroll
+    for (int d = 0; d < kDirectMaxRanks; d++) {
+      if (d < nD) {
+        if (d == nD - 1) stT<STP_LAST, T>(dst[d], i, acc);
+        else stT<STP, T>(dst[d], i, acc);
+      }
+    }
+  }
+}
+
+// Wait until every peer's flag (phase, peer, b) in MY flag array equals e.
+// Lane p of wave 0 polls peer p; bounded like RingCtx::spin_ge.
+__device__ __forceinline__ bool direct_wait(const DirectWork& w, const char* myFlags, int phase,
+                                            int b, uint32_t e, int* shFail) {
+  const int t = threadIdx.x;
+  if (t < w.nRanks && t != w.rank) {
+    const uint32_t* f = (const uint32_t*)(myFlags + direct_flag_off(phase, t, b));
+    const DevComm* comm = w.comm;
+    uint64_t spins = 0, start = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (start == 0) start = now;
+        if (*comm->abortFlag ||
+            __hip_atomic_load(comm->errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          *shFail = 1;
+          break;
+        }
+        if (now - start > comm->spinTimeoutTicks) {
+          __hip_atomic_store(comm->errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          *shFail = 1;
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  return *shFail == 0;
+}
+
+// Every storing wave drains, then lane k of wave 0 raises flag (phase, me, b)
+// at peer (me + k) mod n.
+__device__ __forceinline__ void direct_post(const DirectWork& w, const DirectPeers& P, int phase,
+                                            int b, uint32_t e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int k = threadIdx.x;
+  if (k >= 1 && k < w.nRanks) {
+    const int p = w.rank + k < w.nRanks ? w.rank + k : w.rank + k - w.nRanks;
+    __hip_atomic_store((uint32_t*)(P.flags[p] + direct_flag_off(phase, w.rank, b)), e,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <class Fn>
+__device__ void direct_allreduce(const DirectWork& w) {
+  using T = typename Fn::EltType;
+  __shared__ int shFail;
+  const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
+  const uint32_t e = epoch_next(&w.comm->dEpoch);
+  const DirectPeers& P = *w.peers;
+  const int n = w.nRanks, me = w.rank, b = blockIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int64_t count = (int64_t)w.count;
+  const char* in = (const char*)w.sendbuff;
+  char* out = (char*)w.recvbuff;
+  const int64_t inOff = (int64_t)b * w.blkElts * (int64_t)sizeof(T);  // block offset inside a region
+  char* myBuf = P.buf[me];
+  const char* myFlags = P.flags[me];
+  auto block_of = [&](int o, int64_t* off, int64_t* len) {
+    int64_t shardEnd = (int64_t)(o + 1) * w.shardElts;
+    shardEnd = shardEnd < count ? shardEnd : count;
+    int64_t lo = (int64_t)o * w.shardElts + (int64_t)b * w.blkElts;
+    int64_t hi = lo + w.blkElts < shardEnd ? lo + w.blkElts : shardEnd;
+    *off = lo;
+    *len = hi > lo ? hi - lo : 0;
+  };
+  if (tid == 0) shFail = 0;
+  __syncthreads();
+
+  // Phase 1: scatter my blocks of the foreign shards into their owners' inboxes.
+  for (int k = 1; k < n; k++) {
+    const int p = me + k < n ? me + k : me + k - n;
+    int64_t off, len;
+    block_of(p, &off, &len);
+    const char* s[kDirectMaxRanks] = {in + off * (int64_t)sizeof(T)};
+    char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + inOff};
+    direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+  }
+  direct_post(w, P, 0, b, e);
+
+  // Phase 2: fold my shard's block b, x_{me+1} (+) ... (+) x_{me}; send it out.
+  if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
+    int64_t off, len;
+    block_of(me, &off, &len);
+    // Operand j < n-1: peer (me + j + 1) mod n; operand n-1: my own input /
+    // output.  Filled with compile-time indices only (no scratch array).
+    const char* s[kDirectMaxRanks];
+    char* d[kDirectMaxRanks];
+#pragma unroll
+    for (int j = 0; j < kDirectMaxRanks; j++) {
+      const int src = me + j + 1 < n ? me + j + 1 : me + j + 1 - n;
+      if (j < n - 1) {
+        s[j] = myBuf + direct_region_off(0, src, n, w.regionBytes) + inOff;
+        d[j] = P.buf[src] + direct_region_off(1, me, n, w.regionBytes) + inOff;
+      } else {
+        s[j] = in + off * (int64_t)sizeof(T);
+        d[j] = out + off * (int64_t)sizeof(T);
+      }
+    }
+    direct_rc<Fn, kDirectUnroll, kSys, kSys, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, n, len,
+                                                     tid, nt);
+  }
+  direct_post(w, P, 1, b, e);
+
+  // Phase 3: gather the other owners' reduced blocks.
+  if (direct_wait(w, myFlags, 1, b, e, &shFail)) {
+    for (int k = 1; k < n; k++) {
+      const int o = me + k < n ? me + k : me + k - n;
+      int64_t off, len;
+      block_of(o, &off, &len);
+      const char* s[kDirectMaxRanks] = {myBuf + direct_region_off(1, o, n, w.regionBytes) + inOff};
+      char* d[kDirectMaxRanks] = {out + off * (int64_t)sizeof(T)};
+      direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+    }
+  }
+  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
+}
+
+}  // namespace vccl

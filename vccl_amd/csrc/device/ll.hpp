@@ -102,22 +102,27 @@ __device__ __forceinline__ bool ll_read_line(const char* line, uint32_t epoch, c
   }
 }
 
-// Epoch of this call: DevComm::llEpoch + 1 (wrapping past 0, the cleared
-// state).  The last workgroup to finish stores it back for the next call.
-__device__ __forceinline__ uint32_t ll_epoch_of(const DevComm* comm) {
-  uint32_t e = __hip_atomic_load(&comm->llEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+// Epoch of this call: *epochWord + 1 (wrapping past 0, the cleared state).
+// The last workgroup to finish (ticket in *doneWord) stores it back for the
+// next call, so the counter is device-resident and graph replays stay in step.
+__device__ __forceinline__ uint32_t epoch_next(const uint32_t* epochWord) {
+  uint32_t e = __hip_atomic_load(epochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   return e == 0 ? 1 : e;
 }
-__device__ __forceinline__ void ll_epoch_retire(DevComm* comm, uint32_t e) {
+__device__ __forceinline__ void epoch_retire(uint32_t* epochWord, uint32_t* doneWord, uint32_t e) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t done = __hip_atomic_fetch_add(&comm->llDone, 1u, __ATOMIC_ACQ_REL,
+    const uint32_t done = __hip_atomic_fetch_add(doneWord, 1u, __ATOMIC_ACQ_REL,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     if (done == gridDim.x - 1) {
-      __hip_atomic_store(&comm->llDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&comm->llEpoch, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(doneWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(epochWord, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+__device__ __forceinline__ uint32_t ll_epoch_of(const DevComm* comm) { return epoch_next(&comm->llEpoch); }
+__device__ __forceinline__ void ll_epoch_retire(DevComm* comm, uint32_t e) {
+  epoch_retire(&comm->llEpoch, &comm->llDone, e);
 }
 
 template <class Fn>

@@ -1,8 +1,9 @@
-// Ring collective kernels for ONE kernel element type (VCCL_KT): all-reduce
+// Collective kernels for ONE kernel element type (VCCL_KT): ring all-reduce
 // and reduce-scatter per reduction functor, plus (in the K_U8 unit) the
-// type-agnostic all-gather.  One workgroup per channel (enqueue.cc:1576-1666).
+// type-agnostic all-gather; the one-shot LL and two-shot direct all-reduce.  One workgroup per channel (enqueue.cc:1576-1666).
 #include <hip/hip_runtime.h>
 
+#include "direct.hpp"
 #include "dispatch.hpp"
 #include "ll.hpp"
 #include "ring.hpp"
@@ -52,6 +53,24 @@ hipError_t ll_launch<VCCL_KT>(int devOp, const LLWork& w, int grid, hipStream_t 
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
       hipLaunchKernelGGL((k_ll_allreduce<Fn>), dim3(grid), dim3(256), 0, stream, w);
+      err = hipGetLastError();
+    }
+  });
+  return err;
+}
+
+template <class Fn>
+__global__ __launch_bounds__(kDirectThreads) void k_direct_allreduce(DirectWork w) {
+  direct_allreduce<Fn>(w);
+}
+
+template <>
+hipError_t direct_launch<VCCL_KT>(int devOp, const DirectWork& w, hipStream_t stream) {
+  using T = typename KTypeOf<VCCL_KT>::T;
+  hipError_t err = hipErrorInvalidValue;
+  dispatch_op<T>(devOp, [&]<class Fn>() {
+    if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
+      hipLaunchKernelGGL((k_direct_allreduce<Fn>), dim3(w.nBlocks), dim3(kDirectThreads), 0, stream, w);
       err = hipGetLastError();
     }
   });

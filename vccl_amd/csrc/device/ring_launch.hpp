@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "direct.hpp"
 #include "ll.hpp"
 #include "ring_types.hpp"
 
@@ -17,5 +18,10 @@ hipError_t ring_launch(int coll, int devOp, const RingWork& w, int nthreads, hip
 // One-shot LL all-reduce (ll.hpp): 256-thread workgroups, `grid` of them.
 template <int K>
 hipError_t ll_launch(int devOp, const LLWork& w, int grid, hipStream_t stream);
+
+// Two-shot direct all-reduce (direct.hpp): w.nBlocks workgroups of
+// kDirectThreads threads.
+template <int K>
+hipError_t direct_launch(int devOp, const DirectWork& w, hipStream_t stream);
 
 }  // namespace vccl

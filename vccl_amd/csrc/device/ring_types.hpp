@@ -54,6 +54,9 @@ struct DevComm {
   // ticket) advances it for the next call.
   uint32_t llEpoch;
   uint32_t llDone;
+  // Same scheme for the two-shot direct all-reduce (direct.hpp).
+  uint32_t dEpoch;
+  uint32_t dDone;
 };
 
 // Per-launch work descriptor (kernel argument, by value).

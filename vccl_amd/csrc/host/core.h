@@ -16,6 +16,10 @@
 #include "../device/ring_types.hpp"
 
 namespace vccl {
+struct DirectPeers;  // direct.hpp
+}
+
+namespace vccl {
 
 // ----------------------------------------------------------------- logging
 // NCCL_DEBUG=WARN|INFO|TRACE (debug.h:22-34); VCCL_DEBUG is an alias.
@@ -72,9 +76,13 @@ struct PeerMap {               // what one rank published about itself
   hipIpcMemHandle_t fifoHandle;
   hipIpcMemHandle_t flagHandle;
   hipIpcMemHandle_t llHandle;
+  hipIpcMemHandle_t dBufHandle;
+  hipIpcMemHandle_t dFlagHandle;
   char* fifoPtr;               // raw pointers (valid only in the owner process)
   char* flagPtr;
   char* llPtr;
+  char* dBufPtr;
+  char* dFlagPtr;
 };
 
 struct UserRedOp {             // ncclRedOpCreatePreMulSum state (enqueue.cc:2528-2567)
@@ -100,7 +108,14 @@ struct ncclComm {
   int llLines = 0;             // lines per (parity, source) slot = llMaxBytes / 8
   size_t llMaxBytes = 0;       // largest all-reduce carried by LL
   std::vector<char*> llPeer;   // every rank's LL buffer mapped into this process
-  int algoForce = 0;           // NCCL_ALGO/NCCL_PROTO: 0 auto, 1 ring/SIMPLE, 2 tree/LL
+  // two-shot direct all-reduce (direct.hpp): inbox [2 phases][nRanks][dRegionBytes]
+  char* dBuf = nullptr;
+  char* dFlags = nullptr;      // kDirectFlagBytes of epoch flags
+  size_t directMaxBytes = 0;   // largest all-reduce carried by the direct path
+  int64_t dRegionBytes = 0;
+  int directMaxBlocks = 0;
+  vccl::DirectPeers* dPeers = nullptr;  // device-resident peer table
+  int algoForce = 0;           // NCCL_ALGO/NCCL_PROTO: 0 auto, 1 ring/SIMPLE, 2 tree/LL, 3 direct
   vccl::DevComm* devComm = nullptr;
   vccl::DevChannel* devChannels = nullptr;
   volatile int* abortFlag = nullptr;  // host pinned, mapped

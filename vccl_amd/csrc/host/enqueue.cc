@@ -272,14 +272,71 @@ static ncclResult_t launch_ll(const Task& t) {
   return ncclSuccess;
 }
 
+// Two-shot direct all-reduce for mid-size buckets (direct.hpp).
+static ncclResult_t launch_direct(const Task& t) {
+  ncclComm* comm = t.comm;
+  const int n = comm->nRanks;
+  const int64_t esz = type_size(t.datatype);
+  const int64_t eltAlign = std::max<int64_t>(1, 16 / esz);
+  auto align_up = [](int64_t x, int64_t a) { return (x + a - 1) / a * a; };
+  DirectWork w{};
+  w.comm = comm->devComm;
+  w.peers = comm->dPeers;
+  w.sendbuff = t.sendbuff;
+  w.recvbuff = t.recvbuff;
+  w.count = t.count;
+  w.redArg = t.arg;
+  w.redArgPtr = t.argPtr;
+  w.redArgBytes = (int)esz;
+  w.preOp = t.devOp == OP_PREMULSUM;
+  w.nRanks = n;
+  w.rank = comm->rank;
+  w.shardElts = align_up(((int64_t)t.count + n - 1) / n, eltAlign);
+  // Blocks of >= 16 KiB (one 512-thread x 2-pack hunk), at most the cap.
+  const int64_t minBlk = (16 << 10) / esz;
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((w.shardElts + minBlk - 1) / minBlk,
+                                                            comm->directMaxBlocks));
+  w.blkElts = align_up((w.shardElts + nb - 1) / nb, eltAlign);
+  w.nBlocks = (int)((w.shardElts + w.blkElts - 1) / w.blkElts);
+  w.regionBytes = comm->dRegionBytes;
+  if (w.shardElts * esz > w.regionBytes || w.nBlocks > kDirectMaxBlocks) return ncclInternalError;
+  const int kt = kernel_type_of(t.devOp, (int)t.datatype);
+  hipError_t e = hipErrorInvalidValue;
+  switch (kt) {
+    case K_U8: e = direct_launch<K_U8>(t.devOp, w, t.stream); break;
+    case K_U32: e = direct_launch<K_U32>(t.devOp, w, t.stream); break;
+    case K_U64: e = direct_launch<K_U64>(t.devOp, w, t.stream); break;
+    case K_F16: e = direct_launch<K_F16>(t.devOp, w, t.stream); break;
+    case K_F32: e = direct_launch<K_F32>(t.devOp, w, t.stream); break;
+    case K_F64: e = direct_launch<K_F64>(t.devOp, w, t.stream); break;
+    case K_BF16: e = direct_launch<K_BF16>(t.devOp, w, t.stream); break;
+    default: return ncclInvalidArgument;
+  }
+  if (e != hipSuccess) {
+    VWARN("direct kernel launch failed: %s", hipGetErrorString(e));
+    return ncclUnhandledCudaError;
+  }
+  return ncclSuccess;
+}
+
 // Algorithm choice (topoGetAlgoInfo, enqueue.cc:1805-1945, reduced to one
-// node): all-reduce buckets up to llMaxBytes take the one-shot LL path unless
-// NCCL_ALGO / NCCL_PROTO force the ring; everything else takes the ring.
-static bool use_ll(const Task& t) {
+// node over a full xGMI mesh): all-reduce buckets up to llMaxBytes take the
+// one-shot LL path, up to directMaxBytes the two-shot direct path (LL128's
+// mid-range slot), larger ones the SIMPLE ring.  NCCL_ALGO / NCCL_PROTO force
+// one: Ring/SIMPLE -> ring; Tree/LL -> LL where it fits; LL128/Direct ->
+// direct where it fits; anything that does not fit falls through to the ring.
+enum { kAlgoRing = 0, kAlgoLL = 1, kAlgoDirect = 2 };
+static int choose_algo(const Task& t) {
   const ncclComm* c = t.comm;
-  if (t.coll != kAllReduce || c->nRanks < 2 || !c->llBuf || c->algoForce == 1) return false;
+  if (t.coll != kAllReduce || c->nRanks < 2 || c->algoForce == 1) return kAlgoRing;
   const size_t bytes = t.count * (size_t)type_size(t.datatype);
-  return bytes <= c->llMaxBytes;
+  const bool llFits = c->llBuf && bytes <= c->llMaxBytes;
+  const bool directFits = c->dBuf && bytes <= c->directMaxBytes;
+  if (c->algoForce == 2) return llFits ? kAlgoLL : kAlgoRing;
+  if (c->algoForce == 3) return directFits ? kAlgoDirect : kAlgoRing;
+  if (llFits) return kAlgoLL;
+  if (directFits) return kAlgoDirect;
+  return kAlgoRing;
 }
 
 static ncclResult_t launch_task(const Task& t) {
@@ -297,10 +354,9 @@ static ncclResult_t launch_task(const Task& t) {
       }
     } else if (t.comm->nRanks == 1) {
       r = launch_one_rank(t);
-    } else if (use_ll(t)) {
-      r = launch_ll(t);
     } else {
-      r = launch_ring(t);
+      const int algo = choose_algo(t);
+      r = algo == kAlgoLL ? launch_ll(t) : algo == kAlgoDirect ? launch_direct(t) : launch_ring(t);
     }
   }
   if (r == ncclSuccess) r = stream_mark(t.comm, t.stream);

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <thread>
 
+#include "../device/direct.hpp"
 #include "core.h"
 
 namespace vccl {
@@ -73,6 +74,11 @@ static void free_resources(ncclComm* c) {
   if (c->flagBuf) (void)hipFree(c->flagBuf);
   if (c->llBuf) (void)hipFree(c->llBuf);
   c->llBuf = nullptr;
+  if (c->dBuf) (void)hipFree(c->dBuf);
+  if (c->dFlags) (void)hipFree(c->dFlags);
+  if (c->dPeers) (void)hipFree(c->dPeers);
+  c->dBuf = c->dFlags = nullptr;
+  c->dPeers = nullptr;
   if (c->devComm) (void)hipFree(c->devComm);
   if (c->devChannels) (void)hipFree(c->devChannels);
   if (c->abortFlag) (void)hipHostFree((void*)c->abortFlag);
@@ -87,12 +93,14 @@ static void free_resources(ncclComm* c) {
 }
 
 // Map a peer's buffer into this process/device.
-enum { kMapFifo = 0, kMapFlag = 1, kMapLL = 2 };
+enum { kMapFifo = 0, kMapFlag = 1, kMapLL = 2, kMapDirect = 3, kMapDirectFlag = 4 };
 static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, int which,
                              char** out) {
-  char* raw = which == kMapFifo ? p.fifoPtr : which == kMapFlag ? p.flagPtr : p.llPtr;
-  const hipIpcMemHandle_t& handle =
-      which == kMapFifo ? p.fifoHandle : which == kMapFlag ? p.flagHandle : p.llHandle;
+  char* const raws[] = {p.fifoPtr, p.flagPtr, p.llPtr, p.dBufPtr, p.dFlagPtr};
+  const hipIpcMemHandle_t* const handles[] = {&p.fifoHandle, &p.flagHandle, &p.llHandle,
+                                              &p.dBufHandle, &p.dFlagHandle};
+  char* raw = raws[which];
+  const hipIpcMemHandle_t& handle = *handles[which];
   if (p.pid == me.pid && p.hostHash == me.hostHash) {
     if (p.device != c->device) {
       hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
@@ -142,6 +150,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     const char* proto = getenv("NCCL_PROTO");
     auto has = [](const char* s, const char* w) { return s && strcasestr(s, w) != nullptr; };
     if (has(proto, "LL") || has(algo, "tree")) c->algoForce = 2;
+    // LL128's slot (the mid-range protocol) is the two-shot direct path here
+    if (has(proto, "LL128") || has(algo, "direct")) c->algoForce = 3;
     if (has(proto, "simple") || (has(algo, "ring") && !has(algo, "tree"))) c->algoForce = 1;
   }
   c->nThreads = (int)param_int("NTHREADS", 1024);
@@ -187,6 +197,25 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       HIPCHECK(hipMemset(c->llBuf, 0, llBytes));
       HIPCHECK(hipIpcGetMemHandle(&me.llHandle, c->llBuf));
       me.llPtr = c->llBuf;
+    }
+    // Inbox of the two-shot direct all-reduce (direct.hpp) for buckets in
+    // (LL threshold, VCCL_DIRECT_THRESHOLD]: 2 phases x n regions of one
+    // shard each (2 x the largest bucket), plus the epoch flags.
+    c->directMaxBytes = n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_THRESHOLD", 16 << 20) : 0;
+    c->directMaxBlocks = (int)std::max<int64_t>(
+        1, std::min<int64_t>(param_int("DIRECT_MAX_BLOCKS", 64), kDirectMaxBlocks));
+    if (c->directMaxBytes > c->llMaxBytes) {
+      c->dRegionBytes = (int64_t)((c->directMaxBytes + n - 1) / n + 16 + 255) / 256 * 256;
+      const size_t bytes = (size_t)2 * n * c->dRegionBytes;
+      NCCLCHECK(alloc_uncached((void**)&c->dBuf, bytes));
+      NCCLCHECK(alloc_uncached((void**)&c->dFlags, kDirectFlagBytes));
+      HIPCHECK(hipMemset(c->dFlags, 0, kDirectFlagBytes));
+      HIPCHECK(hipIpcGetMemHandle(&me.dBufHandle, c->dBuf));
+      HIPCHECK(hipIpcGetMemHandle(&me.dFlagHandle, c->dFlags));
+      me.dBufPtr = c->dBuf;
+      me.dFlagPtr = c->dFlags;
+    } else {
+      c->directMaxBytes = 0;
     }
   }
   VINFO("rank %d: exchange peer info", c->rank);
@@ -234,6 +263,20 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       }
       NCCLCHECK(map_peer(c, me, c->peers[r], kMapFifo, &fifoOf[r]));
       NCCLCHECK(map_peer(c, me, c->peers[r], kMapFlag, &flagOf[r]));
+    }
+    if (c->dBuf) {
+      DirectPeers dp{};
+      for (int r = 0; r < n; r++) {
+        if (r == c->rank) {
+          dp.buf[r] = c->dBuf;
+          dp.flags[r] = c->dFlags;
+          continue;
+        }
+        NCCLCHECK(map_peer(c, me, c->peers[r], kMapDirect, &dp.buf[r]));
+        NCCLCHECK(map_peer(c, me, c->peers[r], kMapDirectFlag, &dp.flags[r]));
+      }
+      HIPCHECK(hipMalloc((void**)&c->dPeers, sizeof(DirectPeers)));
+      HIPCHECK(hipMemcpy(c->dPeers, &dp, sizeof(dp), hipMemcpyHostToDevice));
     }
     c->llPeer.assign(n, nullptr);
     if (c->llBuf) {
