@@ -7,8 +7,9 @@ N = 1 (default): BASELINE config 2 — 2-input fp32 sum reduce-copy, 256 MiB
   / time.  Adds `roofline` (per-launch HIP-event duration vs 8 TB/s HBM3E) and
   `cpu_baseline` (the oracle's C restatement on the host cores, bounded sample).
 N > 1 (torch.distributed.run, one process per GPU): BASELINE config 3 at a
-  fixed bucket — ring all-reduce fp32 sum through ncclAllReduce (the repo's
-  own ring over xGMI peer memory; no RCCL).  value = aggregate bus bandwidth
+  fixed bucket — all-reduce fp32 sum through ncclAllReduce (the repo's own
+  transport over xGMI peer memory, no RCCL; the library's algorithm choice,
+  reported as config.algorithm).  value = aggregate bus bandwidth
   = sum over ranks of busbw, busbw = (S/t) * 2(n-1)/n (nccl-tests convention).
   torch.distributed (gloo, CPU tensors) only ships the unique id, barriers and
   the max-over-ranks time.  The same run adds `extras` (not `value`): config 3
@@ -289,10 +290,11 @@ def bench_allreduce(args):
         dt = _time_coll(dist, fn, steps, args.warmup)
         algbw = n * 4 * steps / dt / 1e9
         busbw = algbw * 2 * (world - 1) / world
-        rows.append({"bytes": n * 4, "us": dt / steps * 1e6, "algbw": algbw, "busbw": busbw})
+        rows.append({"bytes": n * 4, "us": dt / steps * 1e6, "algbw": algbw, "busbw": busbw,
+                     "algo": comm.coll_algo(0, n, nccl.ncclFloat32)})
         if rank == 0 and args.sweep:
             print(f"# allreduce {n*4:>12d} B  {dt/steps*1e6:10.1f} us  algbw {algbw:8.2f}  "
-                  f"busbw {busbw:8.2f} GB/s", file=sys.stderr, flush=True)
+                  f"busbw {busbw:8.2f} GB/s  {rows[-1]['algo']}", file=sys.stderr, flush=True)
     extras = None if args.sweep or args.no_extras else bench_extras(dist, comm, rank, world, args)
     err = comm.async_error()
     comm.destroy()
@@ -304,10 +306,11 @@ def bench_allreduce(args):
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(last["us"] / 1e3, 4),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "data": "synthetic uniform[-1,1) seed 1000+rank (device-resident)",
-           "config": {"workload": f"ring all-reduce fp32 sum, {last['bytes']} B per rank "
+           "config": {"workload": f"all-reduce fp32 sum, {last['bytes']} B per rank "
                                   "(BASELINE config 3), value = aggregate busbw over ranks",
+                      "algorithm": last["algo"],
                       "bytes_per_rank": last["bytes"], "busbw_per_rank": round(last["busbw"], 2),
-                      "algbw": round(last["algbw"], 2), "parallelism": f"ring x{world}",
+                      "algbw": round(last["algbw"], 2), "parallelism": f"{last['algo']} x{world}",
                       "async_error": err, "correct": correct},
            "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": peak,
                         "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
@@ -333,7 +336,7 @@ def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
                     steps, warmup)
     algbw = n * esz * steps / dt / 1e9
     return {"bytes": n * esz, "us": round(dt / steps * 1e6, 2),
-            "busbw": round(algbw * 2 * (world - 1) / world, 3)}
+            "busbw": round(algbw * 2 * (world - 1) / world, 3), "algo": comm.coll_algo(0, n, code)}
 
 
 def bench_extras(dist, comm, rank, world, args):

@@ -113,19 +113,34 @@ def expected_reducescatter(op, dtype, inputs, nch):
 
 
 def direct_shard_elts(count, n, elt_size):
-    """Shard length of the two-shot direct all-reduce (host/enqueue.cc
-    launch_direct): ceil(count / n) rounded up to 16 bytes."""
+    """Shard length of one chunk of the two-shot direct all-reduce
+    (direct.hpp direct_shard_elts): ceil(count / n) rounded up to 16 bytes."""
     return _align_up(_div_up(count, n), max(1, 16 // elt_size))
 
 
-def expected_direct(op, dtype, inputs):
-    """Direct all-reduce: shard o (owned by rank o) is folded in the ring order
-    of the identity ring, x_{o+1} (+) ... (+) x_o — the ring all-reduce fold
-    with chunk o finishing at ring index o (all_reduce.h:42-64)."""
+def direct_chunk_elts(count, n, elt_size, chunk_bytes=16 << 20):
+    """Elements per chunk (host/init.cc inbox region, host/enqueue.cc launch_direct)."""
+    region = (chunk_bytes + n - 1) // n // 256 * 256 + 256
+    unit = n * max(1, 16 // elt_size)
+    return min(count, (region - 16) // elt_size * n // unit * unit)
+
+
+def direct_owner(count, n, elt_size, chunk_bytes=16 << 20):
+    """Owner rank of every element: per chunk, shard o belongs to rank o."""
+    chunk = direct_chunk_elts(count, n, elt_size, chunk_bytes)
+    idx = np.arange(count)
+    c0 = idx // chunk * chunk
+    cc = np.minimum(chunk, count - c0)
+    shard = _align_up(_div_up(cc, n), max(1, 16 // elt_size))
+    return ((idx - c0) // shard).astype(np.int32)
+
+
+def expected_direct(op, dtype, inputs, chunk_bytes=16 << 20):
+    """Direct all-reduce: shard o of each chunk (owned by rank o) is folded in
+    the ring order of the identity ring, x_{o+1} (+) ... (+) x_o — the ring
+    all-reduce fold with chunk o finishing at ring index o (all_reduce.h:42-64)."""
     n = len(inputs)
     dev_op, arg = O.host_to_dev_redop(op, dtype, n)
     pre = dev_op == O.DEV_PREMULSUM
-    count = inputs[0].size
-    shard = direct_shard_elts(count, n, inputs[0].dtype.itemsize)
-    owner = (np.arange(count) // shard).astype(np.int32)
+    owner = direct_owner(inputs[0].size, n, inputs[0].dtype.itemsize, chunk_bytes)
     return O.ring_fold(dev_op, dtype, arg, pre, list(inputs), owner)

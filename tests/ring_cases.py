@@ -48,11 +48,12 @@ def gen_input(case_idx, rank, n_ranks):
     return rng.uniform(-1, 1, total).astype(O.NP_DTYPE[dt])
 
 
-def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0):
+def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20):
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
     (oracle ref_chain_fold); up to `direct_max` the two-shot direct path
-    (identity-ring fold per shard); larger ones the ring (owner-map ring fold)."""
+    (identity-ring fold per shard of each `direct_chunk`-byte chunk); larger
+    ones the ring (owner-map ring fold)."""
     name, coll, op, dt, count = CASES[case_idx]
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace"):
@@ -60,7 +61,7 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0):
             dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
             e = O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
         elif count * ins[0].dtype.itemsize <= direct_max:
-            e = _ring.expected_direct(op, dt, ins)
+            e = _ring.expected_direct(op, dt, ins, direct_chunk)
         else:
             e = _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
         return [e] * n_ranks

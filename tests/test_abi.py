@@ -13,7 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     names = set()
-    for h in ("nccl.h", "vccl_device.h", "vccl_bootstrap.h"):
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if not h.endswith(".h"):
+            continue
         text = open(os.path.join(ROOT, "include", h)).read()
         names |= set(re.findall(r"^\s*(?:ncclResult_t|const char\*|int)\s+(p?(?:nccl|vccl)[A-Z]\w*)\s*\(",
                                 text, flags=re.M))

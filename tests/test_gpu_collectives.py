@@ -38,14 +38,15 @@ os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
 TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10),
              "VCCL_ALLOW_SHARED_DEVICE": "1", "VCCL_LL_THRESHOLD": str(1 << 20),
              "VCCL_LL_MAX_BLOCKS": "32", "VCCL_DIRECT_THRESHOLD": str(4 << 20),
-             "VCCL_DIRECT_MAX_BLOCKS": "16"}
+             "VCCL_DIRECT_MAX_BLOCKS": "16", "VCCL_DIRECT_CHUNK_BYTES": str(1 << 20)}
 LL_DEFAULT = 1 << 20
 DIRECT_TEST = 4 << 20
+DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in chunks
 
 
-def _check(ci, n, outs, nch, slot, ll_max, direct_max):
+def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST):
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max)
+    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
 
@@ -55,6 +56,31 @@ def test_duplicate_device_rejected():
     with pytest.raises(nccl.VcclError) as e:
         nccl.Comm.init_all([0, 0])
     assert e.value.code == nccl.ncclInvalidUsage
+
+
+def test_algorithm_choice(monkeypatch):
+    """Library defaults: LL up to 64 KiB (2 ranks), direct above; RS / AG on
+    the ring; NCCL_ALGO / NCCL_PROTO force one (vcclCommCollAlgo)."""
+    monkeypatch.setenv("VCCL_ALLOW_SHARED_DEVICE", "1")
+    for k in ("NCCL_ALGO", "NCCL_PROTO", "VCCL_LL_THRESHOLD", "VCCL_DIRECT_THRESHOLD"):
+        monkeypatch.delenv(k, raising=False)
+    cases = {None: {(0, 16 << 10): "ll", (0, 17 << 10): "direct", (0, 1 << 28): "direct",
+                    (1, 1 << 10): "ring", (2, 1 << 10): "ring"},
+             "Ring": {(0, 1 << 10): "ring", (0, 1 << 20): "ring"},
+             "Tree": {(0, 1 << 10): "ll", (0, 1 << 20): "ring"},
+             "Direct": {(0, 1 << 10): "direct", (0, 1 << 28): "direct", (1, 1 << 10): "ring"}}
+    for algo, expect in cases.items():
+        if algo is None:
+            monkeypatch.delenv("NCCL_ALGO", raising=False)
+        else:
+            monkeypatch.setenv("NCCL_ALGO", algo)
+        comms = nccl.Comm.init_all([0, 0])
+        try:
+            for (coll, count), want in expect.items():
+                assert comms[0].coll_algo(coll, count, 7) == want, (algo, coll, count)
+        finally:
+            for c in comms:
+                c.destroy()
 
 
 # One process drives n ranks on the single GPU: the ranks' kernels are only
@@ -107,7 +133,7 @@ def test_multi_process_ranks(n, geom):
     hexid = nccl.unique_id_to_bytes(uid).hex()
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
-    ll_max, direct_max = LL_DEFAULT, DIRECT_TEST
+    ll_max, direct_max, chunk = LL_DEFAULT, DIRECT_TEST, DIRECT_CHUNK_TEST
     if geom in ("test", "ring_only", "direct_only"):
         env.update(TEST_GEOM)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
@@ -124,14 +150,14 @@ def test_multi_process_ranks(n, geom):
         env.update(VCCL_ALLOW_SHARED_DEVICE="1", VCCL_LL_MAX_BLOCKS="32",
                    VCCL_DIRECT_MAX_BLOCKS="16", VCCL_NTHREADS="256", VCCL_CHANNELS_PER_RING="2")
         nch, slot = _ring.n_channels(n, per_ring=2), 512 << 10
-        ll_max, direct_max = 1 << 20, 16 << 20
+        ll_max, direct_max, chunk = 128 << 10, 1 << 62, 16 << 20
     else:  # library defaults (2 ranks x 32 channels x 1024 threads fit on one GPU)
         for k in TEST_GEOM:
             env.pop(k, None)
         env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         nch, slot = _ring.n_channels(n), 512 << 10
-        ll_max = (256 << 10) if n <= 2 else (1 << 20)
-        direct_max = 16 << 20
+        ll_max = (64 << 10) if n <= 2 else (128 << 10)
+        direct_max, chunk = 1 << 62, 16 << 20
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
                                    str(r), str(n), "0", hexid, d], env=env,
@@ -150,7 +176,7 @@ def test_multi_process_ranks(n, geom):
         assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
-            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max)
+            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk)
 
 
 def test_graph_capture_replay():

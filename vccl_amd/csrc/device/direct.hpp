@@ -20,6 +20,8 @@
 //            peer's inbox region (1, o), then raises flag (1, o, b) there;
 //   phase 3 (gather):  every rank waits for the n-1 flags (1, *, b) and copies
 //            the owners' blocks from its inbox into its output.
+// Buckets larger than the inbox move through it in chunks (the three phases
+// per chunk, one launch); shards and blocks are laid out per chunk.
 // Payload moves with sc0 sc1 (write-through, L2-bypassing) 16-byte accesses,
 // each storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier
 // and the relaxed system-scope flag store: the same hand-off as the ring
@@ -27,11 +29,11 @@
 // epoch_next), so no buffer is ever cleared and graph replays stay in step.
 //
 // Buffer reuse without double buffering: rank r can rewrite region (0, r),
-// block b at p only in its NEXT call, i.e. after its workgroup b finished
-// phase 3 of this call, which waited for p's flag (1, p, b), which p raised
-// only after reading every region (0, *) block b.  Region (1, o) is
-// rewritten by o only after o received phase-1 data of the next call from
-// the reader, which that reader sends only after its own kernel completed.
+// block b at p only in its NEXT chunk (or call), i.e. after its workgroup b
+// finished phase 3 of this one, which waited for p's flag (1, p, b), which p
+// raised only after reading every region (0, *) block b.  Region (1, o) is
+// rewritten by o only after o received the reader's phase-1 data of the next
+// chunk, which workgroup b of the reader sends only after its own phase 3.
 #pragma once
 #include "ll.hpp"
 #include "reduce_copy.hpp"
@@ -63,12 +65,20 @@ struct DirectWork {
   int redArgBytes;
   int preOp;
   int nRanks, rank;
-  int nBlocks;
-  int pad0;
-  int64_t shardElts;     // elements per shard (16-byte multiple)
-  int64_t blkElts;       // elements per block (16-byte multiple)
+  int nBlocks;           // workgroups (block b of every shard -> workgroup b)
+  int nChunks;           // the bucket moves through the inbox in chunks
+  int64_t chunkElts;     // elements per chunk (last one shorter)
+  int64_t blkElts;       // elements per block, the same for every chunk
   int64_t regionBytes;   // bytes per (phase, rank) inbox region
 };
+
+// Shard length of a chunk of `cc` elements: ceil(cc / n) in 16-byte units.
+// The block length stays that of the first (largest) chunk, so block b sits
+// at the same inbox offset in every chunk (a shorter last chunk only leaves
+// high blocks empty) — the reuse argument above needs fixed offsets.
+__host__ __device__ __forceinline__ int64_t direct_shard_elts(int64_t cc, int n, int64_t eltAlign) {
+  return ((cc + n - 1) / n + eltAlign - 1) / eltAlign * eltAlign;
+}
 
 __host__ __device__ __forceinline__ size_t direct_region_off(int phase, int src, int nRanks,
                                                              int64_t regionBytes) {
@@ -214,74 +224,89 @@ __device__ void direct_allreduce(const DirectWork& w) {
   using T = typename Fn::EltType;
   __shared__ int shFail;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
-  const uint32_t e = epoch_next(&w.comm->dEpoch);
+  // Flag values: chunk c of this call raises base + c + 1; the last
+  // workgroup stores base + nChunks back (graph-replay safe, see epoch_next).
+  const uint32_t base = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const DirectPeers& P = *w.peers;
   const int n = w.nRanks, me = w.rank, b = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
-  const int64_t count = (int64_t)w.count;
-  const char* in = (const char*)w.sendbuff;
-  char* out = (char*)w.recvbuff;
-  const int64_t inOff = (int64_t)b * w.blkElts * (int64_t)sizeof(T);  // block offset inside a region
+  const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
+  (void)eltAlign;
   char* myBuf = P.buf[me];
   const char* myFlags = P.flags[me];
-  auto block_of = [&](int o, int64_t* off, int64_t* len) {
-    int64_t shardEnd = (int64_t)(o + 1) * w.shardElts;
-    shardEnd = shardEnd < count ? shardEnd : count;
-    int64_t lo = (int64_t)o * w.shardElts + (int64_t)b * w.blkElts;
-    int64_t hi = lo + w.blkElts < shardEnd ? lo + w.blkElts : shardEnd;
-    *off = lo;
-    *len = hi > lo ? hi - lo : 0;
-  };
   if (tid == 0) shFail = 0;
   __syncthreads();
 
-  // Phase 1: scatter my blocks of the foreign shards into their owners' inboxes.
-  for (int k = 1; k < n; k++) {
-    const int p = me + k < n ? me + k : me + k - n;
-    int64_t off, len;
-    block_of(p, &off, &len);
-    const char* s[kDirectMaxRanks] = {in + off * (int64_t)sizeof(T)};
-    char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + inOff};
-    direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
-  }
-  direct_post(w, P, 0, b, e);
+  for (int c = 0; c < w.nChunks && shFail == 0; c++) {
+    const uint32_t e = base + (uint32_t)c + 1;
+    const int64_t c0 = (int64_t)c * w.chunkElts;
+    const int64_t rest = (int64_t)w.count - c0;
+    const int64_t cc = rest < w.chunkElts ? rest : w.chunkElts;
+    const int64_t shardElts = direct_shard_elts(cc, n, eltAlign);
+    const char* in = (const char*)w.sendbuff + c0 * (int64_t)sizeof(T);
+    char* out = (char*)w.recvbuff + c0 * (int64_t)sizeof(T);
+    const int64_t inOff = (int64_t)b * w.blkElts * (int64_t)sizeof(T);  // block offset in a region
+    auto block_of = [&](int o, int64_t* off, int64_t* len) {
+      int64_t shardEnd = (int64_t)(o + 1) * shardElts;
+      shardEnd = shardEnd < cc ? shardEnd : cc;
+      int64_t lo = (int64_t)o * shardElts + (int64_t)b * w.blkElts;
+      int64_t hi = lo + w.blkElts < shardEnd ? lo + w.blkElts : shardEnd;
+      *off = lo;
+      *len = hi > lo ? hi - lo : 0;
+    };
 
-  // Phase 2: fold my shard's block b, x_{me+1} (+) ... (+) x_{me}; send it out.
-  if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
-    int64_t off, len;
-    block_of(me, &off, &len);
-    // Operand j < n-1: peer (me + j + 1) mod n; operand n-1: my own input /
-    // output.  Filled with compile-time indices only (no scratch array).
-    const char* s[kDirectMaxRanks];
-    char* d[kDirectMaxRanks];
+    // Phase 1: scatter my blocks of the foreign shards into their owners'
+    // inboxes.  Workgroup b starts at peer offset 1 + b mod (n-1), so at any
+    // moment the workgroups of a rank feed all n-1 outgoing links, not one.
+    for (int i = 0; i < n - 1; i++) {
+      int k = 1 + (b + i) % (n - 1);
+      const int p = me + k < n ? me + k : me + k - n;
+      int64_t off, len;
+      block_of(p, &off, &len);
+      const char* s[kDirectMaxRanks] = {in + off * (int64_t)sizeof(T)};
+      char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + inOff};
+      direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+    }
+    direct_post(w, P, 0, b, e);
+
+    // Phase 2: fold my shard's block b, x_{me+1} (+) ... (+) x_{me}; send it out.
+    if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
+      int64_t off, len;
+      block_of(me, &off, &len);
+      // Operand j < n-1: peer (me + j + 1) mod n; operand n-1: my own input /
+      // output.  Filled with compile-time indices only (no scratch array).
+      const char* s[kDirectMaxRanks];
+      char* d[kDirectMaxRanks];
 #pragma unroll
-    for (int j = 0; j < kDirectMaxRanks; j++) {
-      const int src = me + j + 1 < n ? me + j + 1 : me + j + 1 - n;
-      if (j < n - 1) {
-        s[j] = myBuf + direct_region_off(0, src, n, w.regionBytes) + inOff;
-        d[j] = P.buf[src] + direct_region_off(1, me, n, w.regionBytes) + inOff;
-      } else {
-        s[j] = in + off * (int64_t)sizeof(T);
-        d[j] = out + off * (int64_t)sizeof(T);
+      for (int j = 0; j < kDirectMaxRanks; j++) {
+        const int src = me + j + 1 < n ? me + j + 1 : me + j + 1 - n;
+        if (j < n - 1) {
+          s[j] = myBuf + direct_region_off(0, src, n, w.regionBytes) + inOff;
+          d[j] = P.buf[src] + direct_region_off(1, me, n, w.regionBytes) + inOff;
+        } else {
+          s[j] = in + off * (int64_t)sizeof(T);
+          d[j] = out + off * (int64_t)sizeof(T);
+        }
+      }
+      direct_rc<Fn, kDirectUnroll, kSys, kSys, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, n, len,
+                                                       tid, nt);
+    }
+    direct_post(w, P, 1, b, e);
+
+    // Phase 3: gather the other owners' reduced blocks.
+    if (direct_wait(w, myFlags, 1, b, e, &shFail)) {
+      for (int k = 1; k < n; k++) {
+        const int o = me + k < n ? me + k : me + k - n;
+        int64_t off, len;
+        block_of(o, &off, &len);
+        const char* s[kDirectMaxRanks] = {myBuf + direct_region_off(1, o, n, w.regionBytes) + inOff};
+        char* d[kDirectMaxRanks] = {out + off * (int64_t)sizeof(T)};
+        direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
       }
     }
-    direct_rc<Fn, kDirectUnroll, kSys, kSys, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, n, len,
-                                                     tid, nt);
+    __syncthreads();  // the region reads of this chunk precede the next chunk's posts
   }
-  direct_post(w, P, 1, b, e);
-
-  // Phase 3: gather the other owners' reduced blocks.
-  if (direct_wait(w, myFlags, 1, b, e, &shFail)) {
-    for (int k = 1; k < n; k++) {
-      const int o = me + k < n ? me + k : me + k - n;
-      int64_t off, len;
-      block_of(o, &off, &len);
-      const char* s[kDirectMaxRanks] = {myBuf + direct_region_off(1, o, n, w.regionBytes) + inOff};
-      char* d[kDirectMaxRanks] = {out + off * (int64_t)sizeof(T)};
-      direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
-    }
-  }
-  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
+  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, base + (uint32_t)w.nChunks);
 }
 
 }  // namespace vccl

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../../include/vccl_device.h"
+#include "../../../include/vccl_ext.h"
 #include "../device/dispatch.hpp"
 #include "../device/launch.hpp"
 #include "../device/ring_launch.hpp"
@@ -291,15 +292,21 @@ static ncclResult_t launch_direct(const Task& t) {
   w.preOp = t.devOp == OP_PREMULSUM;
   w.nRanks = n;
   w.rank = comm->rank;
-  w.shardElts = align_up(((int64_t)t.count + n - 1) / n, eltAlign);
-  // Blocks of >= 16 KiB (one 512-thread x 2-pack hunk), at most the cap.
+  // Chunk: as many elements as fit one shard per inbox region, a multiple
+  // of n x 16 bytes; blocks of >= 16 KiB (one 512-thread x 2-pack hunk) per
+  // shard of the largest chunk, at most the cap.
+  const int64_t regionElts = (comm->dRegionBytes - 16) / esz;
+  const int64_t chunkMax = regionElts * n / (n * eltAlign) * (n * eltAlign);
+  w.chunkElts = std::min<int64_t>((int64_t)t.count, chunkMax);
+  w.nChunks = (int)(((int64_t)t.count + w.chunkElts - 1) / w.chunkElts);
+  const int64_t shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
   const int64_t minBlk = (16 << 10) / esz;
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((w.shardElts + minBlk - 1) / minBlk,
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((shard0 + minBlk - 1) / minBlk,
                                                             comm->directMaxBlocks));
-  w.blkElts = align_up((w.shardElts + nb - 1) / nb, eltAlign);
-  w.nBlocks = (int)((w.shardElts + w.blkElts - 1) / w.blkElts);
+  w.blkElts = align_up((shard0 + nb - 1) / nb, eltAlign);
+  w.nBlocks = (int)((shard0 + w.blkElts - 1) / w.blkElts);
   w.regionBytes = comm->dRegionBytes;
-  if (w.shardElts * esz > w.regionBytes || w.nBlocks > kDirectMaxBlocks) return ncclInternalError;
+  if (shard0 * esz > w.regionBytes || w.nBlocks > kDirectMaxBlocks) return ncclInternalError;
   const int kt = kernel_type_of(t.devOp, (int)t.datatype);
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
@@ -527,4 +534,23 @@ ncclResult_t pncclGroupEnd(void) VCCL_ALIAS(ncclGroupEnd);
 ncclResult_t pncclRedOpCreatePreMulSum(ncclRedOp_t*, void*, ncclDataType_t, ncclScalarResidence_t,
                                        ncclComm_t) VCCL_ALIAS(ncclRedOpCreatePreMulSum);
 ncclResult_t pncclRedOpDestroy(ncclRedOp_t, ncclComm_t) VCCL_ALIAS(ncclRedOpDestroy);
+}
+
+extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count,
+                                         ncclDataType_t datatype, int* algo) {
+  NCCLCHECK(comm_check(comm, "vcclCommCollAlgo"));
+  if (!algo || coll < 0 || coll > 2 || (int)datatype < 0 || (int)datatype > 9)
+    return ncclInvalidArgument;
+  if (comm->nRanks == 1) {
+    *algo = vcclAlgoOneRank;
+    return ncclSuccess;
+  }
+  Task t{};
+  t.comm = comm;
+  t.coll = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : kAllGather;
+  t.count = count;
+  t.datatype = datatype;
+  const int a = choose_algo(t);
+  *algo = a == kAlgoLL ? vcclAlgoLL : a == kAlgoDirect ? vcclAlgoDirect : vcclAlgoRing;
+  return ncclSuccess;
 }

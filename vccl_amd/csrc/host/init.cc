@@ -186,9 +186,10 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     me.fifoPtr = c->fifoBuf;
     me.flagPtr = c->flagBuf;
     // LL buffers for the one-shot small-bucket all-reduce.
-    // LL vs ring crossover (profiles/r01_sweep_ar_2rank_*.log): the ring pays
-    // 2(n-1) dependent hops, LL one hop but (n-1)x the bytes per rank.
-    c->llMaxBytes = (size_t)param_int("LL_THRESHOLD", n <= 2 ? (256 << 10) : (1 << 20));
+    // LL vs direct crossover (profiles/r01_sweep_algos_*.log): LL pays one
+    // hop but moves 2(n-1)x the bucket per rank, the direct path two hops
+    // and 2(n-1)/n x; LL wins up to ~64 KiB (2 ranks) / ~128 KiB (more).
+    c->llMaxBytes = (size_t)param_int("LL_THRESHOLD", n <= 2 ? (64 << 10) : (128 << 10));
     c->llMaxBytes = (c->llMaxBytes + 7) / 8 * 8;
     if (c->llMaxBytes > 0) {
       c->llLines = (int)(c->llMaxBytes / 8);
@@ -200,12 +201,19 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     }
     // Inbox of the two-shot direct all-reduce (direct.hpp) for buckets in
     // (LL threshold, VCCL_DIRECT_THRESHOLD]: 2 phases x n regions of one
-    // shard each (2 x the largest bucket), plus the epoch flags.
-    c->directMaxBytes = n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_THRESHOLD", 16 << 20) : 0;
+    // shard of a VCCL_DIRECT_CHUNK_BYTES chunk each, plus the epoch flags.
+    // Larger buckets stream through the inbox chunk by chunk.  Default: every
+    // all-reduce above the LL threshold (n <= 8) — it beat the SIMPLE ring at
+    // every size in the rehearsals (same wire bytes, 2 hops instead of
+    // 2(n-1)); the ring stays for reduce-scatter / all-gather, n > 8 and
+    // NCCL_ALGO=Ring.
+    c->directMaxBytes =
+        n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_THRESHOLD", (int64_t)1 << 62) : 0;
     c->directMaxBlocks = (int)std::max<int64_t>(
         1, std::min<int64_t>(param_int("DIRECT_MAX_BLOCKS", 64), kDirectMaxBlocks));
     if (c->directMaxBytes > c->llMaxBytes) {
-      c->dRegionBytes = (int64_t)((c->directMaxBytes + n - 1) / n + 16 + 255) / 256 * 256;
+      const int64_t chunk = std::max<int64_t>(param_int("DIRECT_CHUNK_BYTES", 16 << 20), 64 << 10);
+      c->dRegionBytes = (chunk + n - 1) / n / 256 * 256 + 256;
       const size_t bytes = (size_t)2 * n * c->dRegionBytes;
       NCCLCHECK(alloc_uncached((void**)&c->dBuf, bytes));
       NCCLCHECK(alloc_uncached((void**)&c->dFlags, kDirectFlagBytes));

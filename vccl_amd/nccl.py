@@ -38,8 +38,9 @@ EXPORTED = [
     "ncclCommCuDevice", "ncclCommUserRank", "ncclRedOpCreatePreMulSum", "ncclRedOpDestroy",
     "ncclAllReduce", "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
-    "vcclBuildInfo", "vcclBootstrapAllGather",
+    "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo",
 ]
+ALGO_NAMES = {0: "ring", 1: "ll", 2: "direct", 3: "one_rank"}
 
 
 class VcclError(RuntimeError):
@@ -225,6 +226,13 @@ class Comm:
 
     def all_gather(self, send: int, recv: int, sendcount: int, dtype: int, stream: int = 0):
         check(lib().ncclAllGather(send, recv, sendcount, dtype, self.handle, stream), "ncclAllGather")
+
+    def coll_algo(self, coll: int, count: int, dtype: int) -> str:
+        """vcclCommCollAlgo: "ring" | "ll" | "direct" | "one_rank" (coll 0 AR, 1 RS, 2 AG)."""
+        a = ctypes.c_int()
+        check(lib().vcclCommCollAlgo(self.handle, coll, ctypes.c_size_t(count), dtype,
+                                     ctypes.byref(a)), "vcclCommCollAlgo")
+        return ALGO_NAMES[a.value]
 
     def create_premulsum(self, scalar_ptr: int, dtype: int, residence: int) -> int:
         op = ctypes.c_int()
