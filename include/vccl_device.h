@@ -50,8 +50,8 @@ ncclResult_t vcclReduceCopy(vcclDevRedOp_t devOp, ncclDataType_t datatype, uint6
 
 /* Launch-geometry override for measurement sweeps (0 = library default). */
 typedef struct {
-  int blockSize;    /* threads per workgroup: 256, 512 or 1024 */
-  int unroll;       /* 16-byte packs in flight per thread per source: 2, 4 or 8 */
+  int blockSize;    /* threads per workgroup: 64, 128, 256, 512 or 1024 */
+  int unroll;       /* 16-byte packs in flight per thread per source: 1, 2, 4 or 8 */
   int gridBlocks;   /* workgroups in the grid */
   int ntLoads;      /* load policy: 0 plain, 1 nontemporal, 2 sc0 sc1, 3 sc1 nt */
   int ntStores;     /* store policy: same encoding */

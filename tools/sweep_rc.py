@@ -37,6 +37,12 @@ def main():
             grid = (n * 4 + hunk - 1) // hunk
             variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
                              "ntLoads": ld, "ntStores": st, "order": order})
+    elif mode == "fine":  # small hunks, one per workgroup (nt loads, sc0 sc1 stores)
+        for block, unroll in itertools.product((64, 128, 256, 512), (1, 2, 4)):
+            hunk = block * unroll * 16
+            grid = (n * 4 + hunk - 1) // hunk
+            variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
+                             "ntLoads": 1, "ntStores": 2, "order": 0})
     else:  # geometry around the tuned policies (nt loads, sc0 sc1 stores)
         for block, unroll, per in itertools.product((256, 512, 1024), (2, 4, 8), (1, 2, 4)):
             hunk = block * unroll * 16

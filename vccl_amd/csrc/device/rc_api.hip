@@ -26,8 +26,9 @@ hipError_t reduce_copy_launch(int devOp, int datatype, uint64_t redArg, RCArgs a
   LaunchGeom lg;
   lg.block = (cfg && cfg->blockSize) ? cfg->blockSize : kRcDefBlock;
   lg.unroll = (cfg && cfg->unroll) ? cfg->unroll : kRcDefUnroll;
-  if (lg.block != 256 && lg.block != 512 && lg.block != 1024) return hipErrorInvalidValue;
-  if (lg.unroll != 2 && lg.unroll != 4 && lg.unroll != 8) return hipErrorInvalidValue;
+  if (lg.block != 64 && lg.block != 128 && lg.block != 256 && lg.block != 512 && lg.block != 1024)
+    return hipErrorInvalidValue;
+  if (lg.unroll != 1 && lg.unroll != 2 && lg.unroll != 4 && lg.unroll != 8) return hipErrorInvalidValue;
   lg.ntLoads = cfg ? cfg->ntLoads : kRcDefLd;
   lg.ntStores = cfg ? cfg->ntStores : kRcDefSt;
   lg.order = cfg ? cfg->order : kRcDefOrder;

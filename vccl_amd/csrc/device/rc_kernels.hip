@@ -29,7 +29,7 @@ static hipError_t launch_one(const RCArgs& a, int64_t nElts, uint64_t redArg, co
   return hipGetLastError();
 }
 
-// Sweep dispatch (benchmark shape only): unroll {2,4,8} x load policy
+// Sweep dispatch (benchmark shape only): unroll {1,2,4,8} x load policy
 // {plain, nt, sys, sc1nt} x store policy {plain, nt, sys, sc1nt} x order {0,1}.
 template <class Fn, int NS, int ND, int U>
 static hipError_t sweep_ls(const RCArgs& a, int64_t n, uint64_t r, const LaunchGeom& lg,
@@ -66,6 +66,7 @@ static hipError_t launch_nsnd(const RCArgs& a, int64_t nElts, uint64_t redArg,
   } else {
     if (lg.unroll == 8) return sweep_ls<Fn, NS, ND, 8>(a, nElts, redArg, lg, s);
     if (lg.unroll == 2) return sweep_ls<Fn, NS, ND, 2>(a, nElts, redArg, lg, s);
+    if (lg.unroll == 1) return sweep_ls<Fn, NS, ND, 1>(a, nElts, redArg, lg, s);
     return sweep_ls<Fn, NS, ND, 4>(a, nElts, redArg, lg, s);
   }
 }
