@@ -4,8 +4,9 @@
 N = 1 (default): BASELINE config 2 — 2-input fp32 sum reduce-copy, 256 MiB
   device-resident buffers, through the C ABI (vcclReduceCopy).  One step = one
   launch over the whole bucket; value = algorithmic GB/s = 3 * 2^28 B per step
-  / time.  Adds `roofline` (per-launch HIP-event duration vs 8 TB/s HBM3E) and
-  `cpu_baseline` (the oracle's C restatement on the host cores, bounded sample).
+  / time.  Adds `roofline` (per-launch HIP-event duration vs 8 TB/s HBM3E),
+  `cpu_baseline` (the oracle's C restatement on the host cores, bounded sample)
+  and `extras` (config 1: 1 KiB fp32 ncclAllReduce at world size 1, us/call).
 N > 1 (torch.distributed.run, one process per GPU): BASELINE config 3 at a
   fixed bucket — all-reduce fp32 sum through ncclAllReduce (the repo's own
   transport over xGMI peer memory, no RCCL; the library's algorithm choice,
@@ -13,8 +14,10 @@ N > 1 (torch.distributed.run, one process per GPU): BASELINE config 3 at a
   = sum over ranks of busbw, busbw = (S/t) * 2(n-1)/n (nccl-tests convention).
   torch.distributed (gloo, CPU tensors) only ships the unique id, barriers and
   the max-over-ranks time.  The same run adds `extras` (not `value`): config 3
-  at a few sizes, config 5 (fp16 LL sizes) and config 4 (RS + AG bf16, 4 GiB
-  bucket) — skip with --no-extras.
+  at a few sizes, config 5 (fp16 LL sizes), config 4 (RS + AG bf16, 4 GiB
+  bucket), the ring and the direct algorithm each forced at 64 MiB and the
+  headline bucket, and group aggregation (16 small all-reduces issued one by
+  one vs in one group) — skip with --no-extras.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--bytes S]
        [--workload reduce_copy|allreduce|rs_ag] [--sweep] [--no-extras]
@@ -114,7 +117,38 @@ def bench_reduce_copy(args):
            "roofline": roof}
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(n)
+    if not args.no_extras:
+        out["extras"] = {"config1_allreduce_1KiB_world1": bench_one_rank_latency()}
     return out
+
+
+def bench_one_rank_latency(iters=1000):
+    """BASELINE config 1: ncclAllReduce fp32 sum, 1 KiB (256 elements), world
+    size 1 through the loopback bootstrap: init/enqueue plumbing only (a D2D
+    copy out of place, nothing in place).  us per call = HIP-event time of
+    `iters` back-to-back calls / iters; output checked bitwise = input."""
+    uid = nccl.get_unique_id()
+    comm = nccl.Comm.init_rank(1, uid, 0)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    x = torch.rand(256, device="cuda", generator=torch.Generator(device="cuda").manual_seed(0)) * 2 - 1
+    y = torch.empty_like(x)
+    res = {}
+    for name, dst in (("out_of_place", y), ("in_place", x)):
+        for _ in range(20):
+            comm.all_reduce(x.data_ptr(), dst.data_ptr(), 256, nccl.ncclFloat32, nccl.ncclSum, sp)
+        e0, e1 = _evt(), _evt()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(iters):
+            comm.all_reduce(x.data_ptr(), dst.data_ptr(), 256, nccl.ncclFloat32, nccl.ncclSum, sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        res[name + "_us_per_call"] = round(e0.elapsed_time(e1) * 1e3 / iters, 3)
+        res[name + "_host_us_per_call"] = round((time.perf_counter() - t0) * 1e6 / iters, 3)
+    res["bitwise_equal"] = bool(torch.equal(x.view(torch.int32), y.view(torch.int32)))
+    comm.destroy()
+    return res
 
 
 def _pmc_traffic(workload, algo_bytes):
@@ -164,7 +198,16 @@ def _dist_setup():
     torch.cuda.set_device(local % torch.cuda.device_count())
     if world > torch.cuda.device_count():  # rehearsal on a smaller box only
         os.environ["VCCL_ALLOW_SHARED_DEVICE"] = "1"
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # gloo prints its connection summary on fd 1; keep stdout for the one JSON line
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
     obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     comm = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank)
@@ -339,6 +382,31 @@ def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
             "busbw": round(algbw * 2 * (world - 1) / world, 3), "algo": comm.coll_algo(0, n, code)}
 
 
+def _group_row(dist, comm, rank, world, S, k, steps=20, warmup=3):
+    """k all-reduces of S bytes (fp32 sum): issued one by one vs inside one
+    ncclGroupStart/End, where runs of small buckets are fused into one launch."""
+    sp = torch.cuda.current_stream().cuda_stream
+    n = S // 4
+    xs = [torch.rand(n, device="cuda") for _ in range(k)]
+    ys = [torch.empty_like(x) for x in xs]
+
+    def calls():
+        for x, y in zip(xs, ys):
+            comm.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+
+    def grouped():
+        nccl.group_start()
+        calls()
+        nccl.group_end()
+    t_sep = _time_coll(dist, calls, steps, warmup)
+    f0 = comm.launch_stats()[1]
+    t_grp = _time_coll(dist, grouped, steps, warmup)
+    return {"bytes": S, "calls": k, "us_separate": round(t_sep / steps * 1e6, 2),
+            "us_grouped": round(t_grp / steps * 1e6, 2),
+            "fused_launches_per_group": (comm.launch_stats()[1] - f0) / (steps + warmup),
+            "algo": comm.coll_algo(0, n, nccl.ncclFloat32)}
+
+
 def bench_extras(dist, comm, rank, world, args):
     """Secondary BASELINE configs measured in the same multi-GPU run (reported
     beside the headline, never as ``value``): config 3 at a few sizes (fp32,
@@ -352,6 +420,22 @@ def bench_extras(dist, comm, rank, world, args):
                                   for S in (8, 1 << 10, 16 << 10, 128 << 10)]
     except Exception as e:  # noqa: BLE001 - reported, not fatal to the headline
         ex["allreduce_error"] = repr(e)
+    try:
+        ex["group_fusion_f32"] = [_group_row(dist, comm, rank, world, S, 16) for S in (4 << 10, 32 << 10)]
+    except Exception as e:  # noqa: BLE001
+        ex["group_error"] = repr(e)
+    try:  # each algorithm forced at two bucket sizes (vcclCommSetAlgo): the SIMPLE
+        # ring of the north-star target beside the automatic choice
+        ex["allreduce_f32_by_algo"] = {}
+        for algo in ("ring", "direct"):
+            comm.set_algo(algo)
+            ex["allreduce_f32_by_algo"][algo] = [
+                _ar_size_row(dist, comm, rank, world, S, "f32", st, 2)
+                for S, st in ((64 << 20, 10), (args.bytes or (1 << 30), 5))]
+    except Exception as e:  # noqa: BLE001
+        ex["by_algo_error"] = repr(e)
+    finally:
+        comm.set_algo(None)
     try:
         ex["rs_ag_bf16"] = _rs_ag(dist, comm, rank, world, args.rs_ag_bytes, min(args.steps, 10), 2)
     except Exception as e:  # noqa: BLE001

@@ -7,6 +7,15 @@
  *                     topoGetAlgoInfo (src/enqueue.cc:1805-1945) that VCCL
  *                     only reports through NCCL_DEBUG=INFO logs.  For
  *                     benchmarks and tests; enqueues nothing.
+ *   vcclCommSetAlgo   per-communicator override of that choice (the
+ *                     NCCL_ALGO / NCCL_PROTO environment, graph/tuning.cc:
+ *                     354-373, read once at init): -1 = automatic, otherwise
+ *                     a vcclAlgo_t; an algorithm that cannot carry a call
+ *                     (bucket above its buffer, not an all-reduce) falls
+ *                     through to the ring, as with the environment.
+ *   vcclCommLaunchStats  collectives enqueued on this communicator so far and
+ *                     how many launches carried more than one of them (group
+ *                     aggregation of small all-reduces into one LL launch).
  */
 #ifndef VCCL_EXT_H_
 #define VCCL_EXT_H_
@@ -28,6 +37,9 @@ typedef enum {
 
 ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count, ncclDataType_t datatype,
                               int* algo);
+ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo);
+ncclResult_t vcclCommLaunchStats(ncclComm_t comm, unsigned long long* collectives,
+                                 unsigned long long* fusedLaunches);
 
 #ifdef __cplusplus
 }

@@ -42,6 +42,14 @@ def main():
             comm.all_gather(xb.data_ptr(), yb.data_ptr(), count, dt, s)
         torch.cuda.synchronize()
         res[name] = yb.cpu().numpy().view(x.dtype)
+    # one group of GROUP_CASES on two streams (LL runs fused into one launch)
+    streams = [torch.cuda.current_stream()]
+    if int(os.environ.get("VCCL_TEST_GROUP_STREAMS", "2")) > 1:
+        streams.append(torch.cuda.Stream())
+    g = RC.run_group([(comm, streams)], [rank], nranks)[0]
+    res.update(g)
+    before = comm.launch_stats()
+    res["launch_stats"] = np.array(before, dtype=np.int64)
     err = comm.async_error()
     comm.destroy()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)

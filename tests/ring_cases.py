@@ -48,6 +48,49 @@ def gen_input(case_idx, rank, n_ranks):
     return rng.uniform(-1, 1, total).astype(O.NP_DTYPE[dt])
 
 
+# One ncclGroupStart/End of all-reduces (name, op, dtype, count): runs of
+# small ones with one type and op are fused into one LL launch (up to 16 per
+# launch); a different type, a bucket above the LL threshold or the 16-part
+# cap starts a new launch.  Inputs are seeded per (group index, rank).
+GROUP_CASES = (
+    [("g_f32_sum_a", 0, 7, 1000), ("g_f32_sum_tiny", 0, 7, 3), ("g_f32_sum_b", 0, 7, 20_001),
+     ("g_f16_sum_a", 0, 6, 777), ("g_f16_sum_b", 0, 6, 4096),
+     ("g_f32_sum_big", 0, 7, 300_001),
+     ("g_f32_sum_c", 0, 7, 513), ("g_bf16_avg_a", 4, 9, 1001), ("g_bf16_avg_b", 4, 9, 2003),
+     ("g_i32_max_a", 2, 2, 999), ("g_u8_prod_a", 1, 1, 4097)]
+    + [(f"g_f32_min_{i}", 3, 7, 64 + 37 * i) for i in range(20)])
+
+
+def gen_group_input(gi, rank):
+    name, op, dt, count = GROUP_CASES[gi]
+    rng = np.random.default_rng(777_000 + 100 * gi + rank)
+    if dt in (0, 1, 2, 3, 4, 5):
+        if op == 1:
+            return rng.integers(1, 4, count).astype(O.NP_DTYPE[dt])
+        return rng.integers(-1000, 1000, count).astype(O.NP_DTYPE[dt])
+    if dt == 9:
+        return O.f32_to_bf16_bits(rng.uniform(-1, 1, count).astype(np.float32))
+    return rng.uniform(-1, 1, count).astype(O.NP_DTYPE[dt])
+
+
+def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20):
+    name, op, dt, count = GROUP_CASES[gi]
+    ins = [gen_group_input(gi, r) for r in range(n_ranks)]
+    return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk)
+
+
+def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk):
+    """All-reduce result: LL chain fold up to ll_max bytes, the direct path's
+    fold up to direct_max, the ring's owner-map fold above."""
+    count = len(ins[0])
+    if count * ins[0].dtype.itemsize <= ll_max:
+        dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
+        return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
+    if count * ins[0].dtype.itemsize <= direct_max:
+        return _ring.expected_direct(op, dt, ins, direct_chunk)
+    return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
+
+
 def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20):
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
@@ -57,13 +100,7 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
     name, coll, op, dt, count = CASES[case_idx]
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace"):
-        if count * ins[0].dtype.itemsize <= ll_max:
-            dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
-            e = O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
-        elif count * ins[0].dtype.itemsize <= direct_max:
-            e = _ring.expected_direct(op, dt, ins, direct_chunk)
-        else:
-            e = _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
+        e = expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk)
         return [e] * n_ranks
     if coll == "rs":
         return _ring.expected_reducescatter(op, dt, ins, nch)
@@ -74,3 +111,31 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
 def out_count(case_idx, n_ranks):
     name, coll, op, dt, count = CASES[case_idx]
     return count * n_ranks if coll == "ag" else count
+
+
+def run_group(comm_streams, rank_of, n_ranks):
+    """Enqueue GROUP_CASES inside one ncclGroupStart/End for each (comm, streams)
+    pair (streams alternate per call, so the fused launch joins two streams).
+    Returns {comm index: {name: output tensor}} once the device is idle."""
+    import torch
+    from vccl_amd import nccl
+    bufs = []
+    for ci, (comm, streams) in enumerate(comm_streams):
+        per = {}
+        for gi, (name, op, dt, count) in enumerate(GROUP_CASES):
+            x = gen_group_input(gi, rank_of[ci])
+            xb = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+            yb = torch.empty_like(xb)
+            per[name] = (xb, yb, x.dtype)
+        bufs.append(per)
+    torch.cuda.synchronize()
+    nccl.group_start()
+    for ci, (comm, streams) in enumerate(comm_streams):
+        for gi, (name, op, dt, count) in enumerate(GROUP_CASES):
+            xb, yb, _ = bufs[ci][name]
+            comm.all_reduce(xb.data_ptr(), yb.data_ptr(), count, dt, op,
+                            streams[gi % len(streams)].cuda_stream)
+    nccl.group_end()
+    torch.cuda.synchronize()
+    return {ci: {name: yb.cpu().numpy().view(npdt) for name, (xb, yb, npdt) in bufs[ci].items()}
+            for ci in range(len(comm_streams))}

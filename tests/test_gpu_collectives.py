@@ -127,7 +127,8 @@ def test_single_process_ranks(n, monkeypatch):
 
 
 @pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (8, "test"),
-                                    (8, "ring_only"), (4, "direct_only"), (8, "default8")])
+                                    (2, "ring_only"), (4, "ring_only"), (8, "ring_only"),
+                                    (4, "direct_only"), (8, "default8")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
@@ -177,6 +178,41 @@ def test_multi_process_ranks(n, geom):
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
             _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk)
+        _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot, ll_max,
+                     direct_max, chunk)
+        fused = int(res[0]["launch_stats"][1])
+        assert (fused > 0) == (ll_max > 0), f"fused group launches: {fused} (LL max {ll_max})"
+
+
+def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk):
+    for gi, (name, op, dt, count) in enumerate(RC.GROUP_CASES):
+        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk)
+        for r in range(n):
+            assert_bitexact(dt, outs[r][name], exp, minmax=op in (2, 3),
+                            what=f"group {name} n={n} rank {r}")
+
+
+def test_group_fusion_single_process(monkeypatch):
+    """Two comms driven from one thread: both comms' GROUP_CASES in ONE group,
+    calls interleaved per comm, two streams per comm; runs of small all-reduces
+    of one comm are fused into single LL launches (vcclCommLaunchStats)."""
+    for k, v in TEST_GEOM.items():
+        monkeypatch.setenv(k, v)
+    nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+    comms = nccl.Comm.init_all([0, 0])
+    try:
+        streams = [[torch.cuda.Stream(), torch.cuda.Stream()] for _ in comms]
+        outs = RC.run_group(list(zip(comms, streams)), [0, 1], 2)
+        for c in comms:
+            assert c.async_error() == 0
+        _check_group(2, [outs[0], outs[1]], nch, slot, LL_DEFAULT, DIRECT_TEST, DIRECT_CHUNK_TEST)
+        n_coll, fused = comms[0].launch_stats()
+        # GROUP_CASES: [f32 x3] [f16 x2] big [f32] [bf16 x2] [i32] [u8] [f32 min x20 -> 16 + 4]
+        assert fused == 5, fused
+        assert n_coll == len(RC.GROUP_CASES)
+    finally:
+        for c in comms:
+            c.destroy()
 
 
 def test_graph_capture_replay():

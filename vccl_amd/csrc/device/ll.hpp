@@ -17,25 +17,40 @@
 // Buffers are double-buffered by epoch parity: a peer can only run one call
 // ahead of us (it needs our contribution to finish), so parity reuse is safe
 // and no buffer is ever cleared.
+//
+// Group aggregation (the reference's planner packing several collectives of
+// one ncclGroupStart/End into one kernel, enqueue.cc:352-508 / :518-769): one
+// launch carries up to kLLMaxParts all-reduces of the same type and op; part
+// i occupies lines [line0_i, line0_i + ceil(bytes_i / 8)) of the slot, so the
+// whole batch costs one hop and one epoch.
 #pragma once
 #include "reduce_copy.hpp"
 #include "ring_types.hpp"
 
 namespace vccl {
 
+constexpr int kLLMaxParts = 16;
+
+struct LLPart {
+  const char* send;
+  char* recv;
+  int64_t nbytes;          // count * sizeof(T)
+  int64_t line0;           // first line of this part in the slot
+};
+
 struct LLWork {
   DevComm* comm;
-  const void* sendbuff;
-  void* recvbuff;
-  uint64_t count;          // elements
   uint64_t redArg;
   const void* redArgPtr;
   int redArgBytes;
   int preOp;
   int nRanks, rank;
   int linesPerSlot;        // capacity of one (parity, source) slot
+  int nParts;              // 1 .. kLLMaxParts all-reduces in this launch
+  int64_t nLines;          // lines of all parts (<= linesPerSlot)
   char* localBuf;          // my LL buffer: [2 parities][nRanks sources][linesPerSlot] lines
   char* peerBuf[kMaxRanks];  // every rank's LL buffer mapped here (peerBuf[rank] = local)
+  LLPart parts[kLLMaxParts];
 };
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -125,21 +140,42 @@ __device__ __forceinline__ void ll_epoch_retire(DevComm* comm, uint32_t e) {
   epoch_retire(&comm->llEpoch, &comm->llDone, e);
 }
 
+// Part table in LDS (filled through constant indices: a runtime index into
+// the by-value kernel argument would copy it to scratch); `advance` moves a
+// thread's part cursor forward to the part holding line l (lines visited by a
+// thread only grow).
+struct LLParts {
+  LLPart p[kLLMaxParts];
+};
+__device__ __forceinline__ void ll_load_parts(const LLWork& w, LLParts* sh) {
+#pragma unroll
+  for (int i = 0; i < kLLMaxParts; i++)
+    if ((int)threadIdx.x == i && i < w.nParts) sh->p[i] = w.parts[i];
+  __syncthreads();
+}
+__device__ __forceinline__ int ll_advance(const LLParts& sh, int nParts, int cur, int64_t l) {
+  while (cur + 1 < nParts && l >= sh.p[cur + 1].line0) cur++;
+  return cur;
+}
+
 template <class Fn>
 __device__ void ll_allreduce(const LLWork& w) {
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
-  using T = typename Fn::EltType;
+  __shared__ LLParts sh;
+  ll_load_parts(w, &sh);
   const uint32_t epoch = ll_epoch_of(w.comm);
-  const int64_t nbytes = (int64_t)w.count * (int64_t)sizeof(T);
-  const int64_t nLines = (nbytes + 7) / 8;
+  const int64_t nLines = w.nLines;
+  const int nParts = w.nParts;
   const int parity = (int)(epoch & 1);
   const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t gthreads = (int64_t)gridDim.x * blockDim.x;
-  const char* in = (const char*)w.sendbuff;
   const uint32_t e = epoch;
   // Phase 1: publish my input to every peer (one hop over xGMI).
+  int pc = 0;
   for (int64_t l = gtid; l < nLines; l += gthreads) {
-    const uint64_t v = ll_load8(in, l, nbytes);
+    pc = ll_advance(sh, nParts, pc, l);
+    const LLPart& part = sh.p[pc];
+    const uint64_t v = ll_load8(part.send, l - part.line0, part.nbytes);
     u32x4 line;
     line.x = (uint32_t)v;
     line.y = e;
@@ -155,9 +191,12 @@ __device__ void ll_allreduce(const LLWork& w) {
   // Loads for up to kLLBatch sources of a line are issued together (their
   // latencies overlap); a source whose line has not arrived yet is re-polled.
   constexpr int kLLBatch = 8;
-  char* out = (char*)w.recvbuff;
   bool ok = true;
+  pc = 0;
   for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
+    pc = ll_advance(sh, nParts, pc, l);
+    const LLPart& part = sh.p[pc];
+    const int64_t pl = l - part.line0;
     uint64_t acc = 0;
     for (int hi = w.nRanks - 1; hi >= 0 && ok; hi -= kLLBatch) {
       const int lo = hi - kLLBatch + 1 > 0 ? hi - kLLBatch + 1 : 0;
@@ -176,7 +215,7 @@ __device__ void ll_allreduce(const LLWork& w) {
         if (p < lo) break;
         uint64_t x;
         if (p == w.rank) {
-          x = ll_load8(in, l, nbytes);
+          x = ll_load8(part.send, pl, part.nbytes);
         } else if (v[b].y == e && v[b].w == e) {
           x = (uint64_t)v[b].x | ((uint64_t)v[b].z << 32);
         } else {
@@ -190,7 +229,7 @@ __device__ void ll_allreduce(const LLWork& w) {
     }
     if (!ok) break;
     if (Fn::kPostOp) acc = ll_apply(fn, acc, 0, 2);
-    ll_store8(out, l, nbytes, acc);
+    ll_store8(part.recv, pl, part.nbytes, acc);
   }
   ll_epoch_retire(w.comm, e);
 }

@@ -124,7 +124,10 @@ struct ncclComm {
   std::vector<vccl::PeerMap> peers;
   // ordering of launches on this comm across user streams
   hipEvent_t lastLaunch = nullptr;
+  hipEvent_t joinEvent = nullptr;     // joins other streams into a fused group launch
   hipStream_t lastStream = nullptr;
+  bool hasLastLaunch = false;         // lastLaunch/lastStream are valid
+  uint64_t fusedLaunches = 0;         // group launches that carried > 1 collective
   // state
   std::atomic<int> asyncError{0};
   std::vector<vccl::UserRedOp> userOps;

@@ -4,11 +4,13 @@
 // (collectives.cc:77-158 -> ncclEnqueueCheck enqueue.cc:2448-2525 -> ArgsCheck
 // misc/argcheck.cc:45-86 -> taskAppend enqueue.cc:2315-2442 with
 // hostToDevRedOp :2217-2310 and the nRanks==1 shortcut ncclLaunchOneRank
-// onerank.cu:47-83), re-implemented for one node: the planner has a single
-// algorithm (ring / SIMPLE over xGMI), so "planning" is the channel partition
-// done on the device (ring.hpp channel_part).  Group semantics
-// (group.cc:92-110, :393-506): calls between ncclGroupStart/End are queued
-// per thread and launched, in call order, at the outermost ncclGroupEnd.
+// onerank.cu:47-83), re-implemented for one node: the planner picks one of
+// three algorithms per call (choose_algo: one-shot LL, two-shot direct, SIMPLE
+// ring over xGMI); the ring's channel partition is done on the device
+// (ring.hpp channel_part).  Group semantics (group.cc:92-110, :393-506): calls
+// between ncclGroupStart/End are queued per thread and launched at the
+// outermost ncclGroupEnd in call order, runs of small all-reduces fused into
+// one LL launch (launch_group).
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -156,14 +158,17 @@ static ncclResult_t args_check(ncclComm* comm, const char* name, ncclDataType_t 
 
 // Order launches of one comm across different user streams (the reference
 // serialises through its internal strong stream, enqueue.cc:1445-1548).
+// The null stream (0) is a valid user stream, so "no launch yet" is a flag of
+// its own, not a null lastStream.
 static ncclResult_t stream_order(ncclComm* comm, hipStream_t s) {
-  if (comm->lastStream != nullptr && comm->lastStream != s)
+  if (comm->hasLastLaunch && comm->lastStream != s)
     HIPCHECK(hipStreamWaitEvent(s, comm->lastLaunch, 0));
   return ncclSuccess;
 }
 static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s) {
   HIPCHECK(hipEventRecord(comm->lastLaunch, s));
   comm->lastStream = s;
+  comm->hasLastLaunch = true;
   return ncclSuccess;
 }
 
@@ -231,13 +236,17 @@ static ncclResult_t launch_ring(const Task& t) {
 }
 
 // One-shot LL all-reduce for small buckets (ll.hpp); the chain-tree fold.
-static ncclResult_t launch_ll(const Task& t) {
+// `ts` holds 1 .. kLLMaxParts all-reduces of one comm with the same type and
+// op (ll_fusable) whose lines fit one slot; they run as one launch on
+// ts[0].stream (the caller orders the other streams around it).
+static int64_t ll_lines_of(const Task& t) {
+  return ((int64_t)t.count * type_size(t.datatype) + 7) / 8;
+}
+static ncclResult_t launch_ll(const Task* ts, int nTasks) {
+  const Task& t = ts[0];
   ncclComm* comm = t.comm;
   LLWork w{};
   w.comm = comm->devComm;
-  w.sendbuff = t.sendbuff;
-  w.recvbuff = t.recvbuff;
-  w.count = t.count;
   w.redArg = t.arg;
   w.redArgPtr = t.argPtr;
   w.redArgBytes = type_size(t.datatype);
@@ -247,9 +256,20 @@ static ncclResult_t launch_ll(const Task& t) {
   w.linesPerSlot = comm->llLines;
   w.localBuf = comm->llBuf;
   for (int r = 0; r < comm->nRanks; r++) w.peerBuf[r] = comm->llPeer[r];
+  if (nTasks < 1 || nTasks > kLLMaxParts) return ncclInternalError;
+  int64_t lines = 0;
+  for (int i = 0; i < nTasks; i++) {
+    w.parts[i].send = (const char*)ts[i].sendbuff;
+    w.parts[i].recv = (char*)ts[i].recvbuff;
+    w.parts[i].nbytes = (int64_t)ts[i].count * type_size(ts[i].datatype);
+    w.parts[i].line0 = lines;
+    lines += ll_lines_of(ts[i]);
+  }
+  w.nParts = nTasks;
+  w.nLines = lines;
+  if (lines > comm->llLines) return ncclInternalError;
   const int kt = kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
-  const int64_t lines = ((int64_t)t.count * type_size(t.datatype) + 7) / 8;
   // A bounded grid (<= VCCL_LL_MAX_BLOCKS 256-thread workgroups, each thread
   // looping over lines): every rank's LL workgroups must be resident at once
   // for the peers' spins to complete; 256 x 4 waves is 1/8 of a GPU's
@@ -363,13 +383,83 @@ static ncclResult_t launch_task(const Task& t) {
       r = launch_one_rank(t);
     } else {
       const int algo = choose_algo(t);
-      r = algo == kAlgoLL ? launch_ll(t) : algo == kAlgoDirect ? launch_direct(t) : launch_ring(t);
+      r = algo == kAlgoLL ? launch_ll(&t, 1) : algo == kAlgoDirect ? launch_direct(t) : launch_ring(t);
     }
   }
   if (r == ncclSuccess) r = stream_mark(t.comm, t.stream);
   t.comm->opCount++;
   if (old != t.comm->device) (void)hipSetDevice(old);
   return r;
+}
+
+// Group aggregation (enqueue.cc:352-508 ncclPrepareTasks / :518-769
+// scheduleCollTasksToPlan pack a group's collectives into one kernel plan):
+// here a run of consecutive LL all-reduces of one comm with the same type and
+// op becomes one LL launch (up to kLLMaxParts, lines within one slot).  The
+// decision depends only on the call sequence, never on streams, so every rank
+// fuses identically.  The fused launch runs on the first task's stream; the
+// other tasks' streams are joined before it and wait for it after.
+static bool ll_eligible(const Task& t) {
+  return t.coll == kAllReduce && t.comm->nRanks > 1 && choose_algo(t) == kAlgoLL;
+}
+static bool ll_fusable(const Task& a, const Task& b) {
+  return a.comm == b.comm && a.datatype == b.datatype && a.devOp == b.devOp && a.arg == b.arg &&
+         a.argPtr == b.argPtr;
+}
+
+static ncclResult_t launch_ll_batch(const std::vector<Task>& ts) {
+  ncclComm* comm = ts[0].comm;
+  const hipStream_t s0 = ts[0].stream;
+  int old = -1;
+  HIPCHECK(hipGetDevice(&old));
+  if (old != comm->device) HIPCHECK(hipSetDevice(comm->device));
+  std::vector<hipStream_t> others;
+  for (const Task& t : ts)
+    if (t.stream != s0 && std::find(others.begin(), others.end(), t.stream) == others.end())
+      others.push_back(t.stream);
+  ncclResult_t r = stream_order(comm, s0);
+  for (hipStream_t s : others) {
+    if (r != ncclSuccess) break;
+    if (hipEventRecord(comm->joinEvent, s) != hipSuccess ||
+        hipStreamWaitEvent(s0, comm->joinEvent, 0) != hipSuccess)
+      r = ncclUnhandledCudaError;
+  }
+  if (r == ncclSuccess) r = launch_ll(ts.data(), (int)ts.size());
+  if (r == ncclSuccess) r = stream_mark(comm, s0);
+  for (hipStream_t s : others)
+    if (r == ncclSuccess && hipStreamWaitEvent(s, comm->lastLaunch, 0) != hipSuccess)
+      r = ncclUnhandledCudaError;
+  comm->opCount += ts.size();
+  comm->fusedLaunches++;
+  if (old != comm->device) (void)hipSetDevice(old);
+  return r;
+}
+
+static ncclResult_t launch_group(std::vector<Task>& tasks) {
+  ncclResult_t ret = ncclSuccess;
+  std::vector<char> done(tasks.size(), 0);
+  const bool fuse = param_int("GROUP_FUSE", 1) != 0;
+  for (size_t i = 0; i < tasks.size(); i++) {
+    if (done[i]) continue;
+    ncclResult_t r;
+    if (fuse && ll_eligible(tasks[i])) {
+      std::vector<Task> batch{tasks[i]};
+      int64_t lines = ll_lines_of(tasks[i]);
+      for (size_t j = i + 1; j < tasks.size() && batch.size() < (size_t)kLLMaxParts; j++) {
+        if (done[j] || tasks[j].comm != tasks[i].comm) continue;
+        if (!ll_eligible(tasks[j]) || !ll_fusable(tasks[i], tasks[j])) break;
+        if (lines + ll_lines_of(tasks[j]) > tasks[i].comm->llLines) break;
+        lines += ll_lines_of(tasks[j]);
+        batch.push_back(tasks[j]);
+        done[j] = 1;
+      }
+      r = batch.size() == 1 ? launch_task(tasks[i]) : launch_ll_batch(batch);
+    } else {
+      r = launch_task(tasks[i]);
+    }
+    if (ret == ncclSuccess) ret = r;
+  }
+  return ret;
 }
 
 static ncclResult_t enqueue_check(int coll, const char* name, const void* sendbuff, void* recvbuff,
@@ -448,10 +538,8 @@ VCCL_EXPORT ncclResult_t ncclGroupEnd(void) {
   ncclResult_t ret = tl_groupError;
   std::vector<Task> tasks;
   tasks.swap(tl_tasks);
-  for (const Task& t : tasks) {
-    ncclResult_t r = launch_task(t);
-    if (ret == ncclSuccess) ret = r;
-  }
+  ncclResult_t r = launch_group(tasks);
+  if (ret == ncclSuccess) ret = r;
   tl_groupError = ncclSuccess;
   return ret;
 }
@@ -518,8 +606,8 @@ VCCL_EXPORT ncclResult_t vcclHostToDevRedOp(ncclRedOp_t op, ncclDataType_t datat
 }
 
 VCCL_EXPORT const char* vcclBuildInfo(void) {
-  return "vccl-mi355x " __DATE__ " gfx950; ring SIMPLE over xGMI (uncached receiver FIFOs); "
-         "reduce-copy 16B packs";
+  return "vccl-mi355x " __DATE__ " gfx950; one-shot LL / two-shot direct / SIMPLE ring over "
+         "xGMI (uncached receiver buffers); reduce-copy 16B packs; group-fused LL";
 }
 
 extern "C" {
@@ -552,5 +640,24 @@ extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count
   t.datatype = datatype;
   const int a = choose_algo(t);
   *algo = a == kAlgoLL ? vcclAlgoLL : a == kAlgoDirect ? vcclAlgoDirect : vcclAlgoRing;
+  return ncclSuccess;
+}
+
+extern "C" ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo) {
+  NCCLCHECK(comm_check(comm, "vcclCommSetAlgo"));
+  switch (algo) {
+    case -1: comm->algoForce = 0; return ncclSuccess;
+    case vcclAlgoRing: comm->algoForce = 1; return ncclSuccess;
+    case vcclAlgoLL: comm->algoForce = 2; return ncclSuccess;
+    case vcclAlgoDirect: comm->algoForce = 3; return ncclSuccess;
+  }
+  return ncclInvalidArgument;
+}
+
+extern "C" ncclResult_t vcclCommLaunchStats(ncclComm_t comm, unsigned long long* collectives,
+                                            unsigned long long* fusedLaunches) {
+  NCCLCHECK(comm_check(comm, "vcclCommLaunchStats"));
+  if (collectives) *collectives = comm->opCount;
+  if (fusedLaunches) *fusedLaunches = comm->fusedLaunches;
   return ncclSuccess;
 }

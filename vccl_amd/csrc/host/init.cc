@@ -84,6 +84,8 @@ static void free_resources(ncclComm* c) {
   if (c->abortFlag) (void)hipHostFree((void*)c->abortFlag);
   if (c->errorFlag) (void)hipHostFree(c->errorFlag);
   if (c->lastLaunch) (void)hipEventDestroy(c->lastLaunch);
+  if (c->joinEvent) (void)hipEventDestroy(c->joinEvent);
+  c->joinEvent = nullptr;
   c->fifoBuf = c->flagBuf = nullptr;
   c->devComm = nullptr;
   c->devChannels = nullptr;
@@ -162,6 +164,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   *c->abortFlag = 0;
   *c->errorFlag = 0;
   HIPCHECK(hipEventCreateWithFlags(&c->lastLaunch, hipEventDisableTiming));
+  HIPCHECK(hipEventCreateWithFlags(&c->joinEvent, hipEventDisableTiming));
 
   PeerMap me{};
   me.pid = (int)getpid();
@@ -192,7 +195,12 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     c->llMaxBytes = (size_t)param_int("LL_THRESHOLD", n <= 2 ? (64 << 10) : (128 << 10));
     c->llMaxBytes = (c->llMaxBytes + 7) / 8 * 8;
     if (c->llMaxBytes > 0) {
-      c->llLines = (int)(c->llMaxBytes / 8);
+      // Slot capacity: the single-call threshold, or more for group
+      // aggregation (VCCL_LL_GROUP_BYTES): a group's run of small all-reduces
+      // fills one slot even when their sum is above the single-call
+      // threshold — one LL launch still beats one launch per bucket there.
+      const int64_t groupBytes = std::max<int64_t>(param_int("LL_GROUP_BYTES", 1 << 20), 0);
+      c->llLines = (int)((std::max<int64_t>((int64_t)c->llMaxBytes, groupBytes) + 7) / 8);
       const size_t llBytes = (size_t)2 * n * c->llLines * 16;
       NCCLCHECK(alloc_uncached((void**)&c->llBuf, llBytes));
       HIPCHECK(hipMemset(c->llBuf, 0, llBytes));

@@ -38,7 +38,8 @@ EXPORTED = [
     "ncclCommCuDevice", "ncclCommUserRank", "ncclRedOpCreatePreMulSum", "ncclRedOpDestroy",
     "ncclAllReduce", "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
-    "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo",
+    "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
+    "vcclCommLaunchStats",
 ]
 ALGO_NAMES = {0: "ring", 1: "ll", 2: "direct", 3: "one_rank"}
 
@@ -233,6 +234,18 @@ class Comm:
         check(lib().vcclCommCollAlgo(self.handle, coll, ctypes.c_size_t(count), dtype,
                                      ctypes.byref(a)), "vcclCommCollAlgo")
         return ALGO_NAMES[a.value]
+
+    def set_algo(self, algo: str | None):
+        """vcclCommSetAlgo: force "ring" | "ll" | "direct" for later calls; None = automatic."""
+        code = -1 if algo is None else {v: k for k, v in ALGO_NAMES.items()}[algo]
+        check(lib().vcclCommSetAlgo(self.handle, code), "vcclCommSetAlgo")
+
+    def launch_stats(self) -> tuple[int, int]:
+        """vcclCommLaunchStats: (collectives enqueued, fused group launches)."""
+        a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        check(lib().vcclCommLaunchStats(self.handle, ctypes.byref(a), ctypes.byref(b)),
+              "vcclCommLaunchStats")
+        return a.value, b.value
 
     def create_premulsum(self, scalar_ptr: int, dtype: int, residence: int) -> int:
         op = ctypes.c_int()
