@@ -29,6 +29,10 @@ CASES = [
     ("rs_f32_sum", "rs", 0, 7, 65_537),
     ("rs_bf16_avg", "rs", 4, 9, 20_000),
     ("rs_u32_min", "rs", 3, 3, 9_999),
+    # per-rank blocks off 16-byte alignment: slot offsets + shifted sources
+    ("rs_bf16_sum_odd", "rs", 0, 9, 20_001),
+    ("rs_i8_max_odd", "rs", 2, 0, 1_003),
+    ("ag_f16_odd", "ag", 0, 6, 3_001),
     ("ag_f32", "ag", 0, 7, 4_099),
     ("ag_u8_odd", "ag", 0, 1, 1_001),
 ]

@@ -96,6 +96,42 @@ def test_misaligned_and_multi_dst(t):
             assert_bitexact(t, o, exp, what=f"t{t} offs{offs}")
 
 
+# Sources misaligned relative to destinations that share one misalignment:
+# the body moves in 16-byte packs realigned by wavefront shuffle + funnel
+# shift (reduce_copy_misaligned).  Sizes hit head-only, tail-only, one
+# partial wave, whole hunks; bytes around every destination stay untouched.
+SHIFT_OFFSETS = {1: ([1, 7, 15], [3, 3]), 2: ([2, 6, 14], [10, 10]),
+                 4: ([0, 4, 12], [8, 8]), 8: ([8, 0, 8], [8, 8])}
+
+
+@pytest.mark.parametrize("t", [0, 1, 2, 4, 6, 7, 8, 9])
+@pytest.mark.parametrize("op", [0, 1, 2, 4])
+def test_shifted_sources(t, op):
+    rng = np.random.default_rng(900 + 10 * t + op)
+    sz = np.dtype(O.NP_DTYPE[t]).itemsize
+    soffs, doffs = SHIFT_OFFSETS[sz]
+    for n in (1, 3, 17, 63, 1000, 4096 + 5, 100_003, (1 << 20) + 7):
+        nsrc = 3 if n % 2 else 2
+        srcs = [_rand(rng, t, n) for _ in range(nsrc)]
+        dev_op, arg, pre, post = _dev_args(op, t, nsrc)
+        exp = O.reduce_copy(dev_op, t, arg, srcs, pre_op_args=[arg] * pre, post_op=post)[0]
+        offs = soffs[:nsrc] + doffs
+        keep, sp = [], []
+        for i, x in enumerate(srcs):
+            tt, ptr = to_dev(x, offset=offs[i])
+            keep.append(tt)
+            sp.append(ptr)
+        outs = [empty_dev(n * sz, offset=o) for o in doffs]
+        nccl.reduce_copy(dev_op, t, arg, sp, [ptr for _, ptr in outs], n, stream_ptr(),
+                         pre_op_srcs=pre, post_op=post)
+        torch.cuda.synchronize()
+        for (tt, _), o in zip(outs, doffs):
+            got = from_dev(tt, O.NP_DTYPE[t], n, o)
+            assert_bitexact(t, got, exp, minmax=op == 2, what=f"t{t} op{op} n{n} offs{offs}")
+            raw = tt.cpu().numpy()
+            assert (raw[:o] == 0xA5).all() and (raw[o + n * sz:] == 0xA5).all(), "guard bytes written"
+
+
 def test_eight_sources_and_geometry_sweep():
     rng = np.random.default_rng(11)
     n = (1 << 22) + 5

@@ -29,6 +29,8 @@ def main():
     sp = s.cuda_stream
     variants = []
     mode = os.environ.get("SWEEP_MODE", "policies")
+    if mode == "misaligned":
+        return misaligned(n, rounds, reps)
     if mode == "policies":
         # load/store policy: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1 nt; order 1 = XCD-contiguous hunks
         for block, unroll, ld, st, order in itertools.product(
@@ -80,6 +82,40 @@ def main():
     rows.sort(key=lambda x: -x["median_gbs"])
     for row in rows:
         print(json.dumps(row))
+
+
+def misaligned(n, rounds, reps):
+    """2-src f32 sum at the config-2 size with byte offsets (src0, src1, dst):
+    aligned; a shifted source (wavefront-shuffle realignment); a common
+    misalignment (head/tail elements + aligned body); destinations that
+    differ from the sources AND each other are not in this set (element path,
+    measured as 'elements' by misaligning dst against a 2-dst pair)."""
+    base = [torch.empty(n * 4 + 64, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    for b in base[:2]:
+        b.view(torch.float32)[:n] = torch.rand(n, device="cuda")
+    s = torch.cuda.current_stream()
+    variants = {"aligned": ((0, 0), (0,)), "shifted_src1_+4": ((0, 4), (0,)),
+                "shifted_both_+4_+8": ((4, 8), (0,)), "common_+4": ((4, 4), (4,)),
+                "elements_dsts_0_4": ((0, 0), (0, 4))}
+    times = {k: [] for k in variants}
+    for r in range(rounds):
+        for name, (so, do) in variants.items():
+            srcs = [base[i].data_ptr() + o for i, o in enumerate(so)]
+            dsts = [base[2 + i].data_ptr() + o for i, o in enumerate(do)]
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(reps)]
+            for e0, e1 in ev:
+                e0.record(s)
+                nccl.reduce_copy(0, 7, 0, srcs, dsts, n - 4, s.cuda_stream)
+                e1.record(s)
+            torch.cuda.synchronize()
+            times[name] += [e0.elapsed_time(e1) for e0, e1 in ev]
+    for name, (so, do) in variants.items():
+        t = np.array(times[name][reps:])
+        nbytes = (2 + len(do)) * (n - 4) * 4
+        print(json.dumps({"cfg": name, "offsets": [so, do],
+                          "median_gbs": round(float(np.median(nbytes / (t / 1e3) / 1e9)), 1),
+                          "median_us": round(float(np.median(t)) * 1e3, 2)}))
 
 
 if __name__ == "__main__":

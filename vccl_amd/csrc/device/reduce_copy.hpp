@@ -315,6 +315,104 @@ __device__ __forceinline__ void rc_elems(const Fn& fn, const RCArgs& a, int64_t 
   }
 }
 
+// ------------------------------------------------------------ misaligned
+// Operands that are not 16-byte aligned (common_kernel.h:237-241 drops to
+// element packs for ANY misalignment).  Here the body still moves in 16-byte
+// packs when every destination shares one misalignment m (mod 16):
+//   head  — the first (16 - m) / sizeof(T) elements, element path;
+//   body  — packs aligned on the destinations; a source whose misalignment
+//           differs by k is read as ALIGNED 16-byte packs and realigned in
+//           registers: lane l funnel-shifts its pack with lane l+1's (a
+//           wavefront shuffle, ds_bpermute), lane 63 loads its successor
+//           pack itself, v_alignbyte_b32 extracts bytes [k, k+16);
+//   tail  — the last < 16 bytes, element path.
+// Aligned loads never cross a 16-byte boundary, so reading the bytes of the
+// first / last pack that lie outside an operand cannot fault.  Destinations
+// with different misalignments fall back to the element path.
+
+// Bytes [k, k + 16) of the 32-byte concatenation lo:hi (k wave-uniform).
+__device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, int k) {
+  const uint32_t r = (uint32_t)(k & 3);
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  u32x4 o;
+  switch (k >> 2) {
+#define VCCL_FUNNEL_CASE(Q)                                               \
+  case Q:                                                                 \
+    o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q + 0], r);              \
+    o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], r);              \
+    o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], r);              \
+    o.w = __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], r);              \
+    break;
+    VCCL_FUNNEL_CASE(0)
+    VCCL_FUNNEL_CASE(1)
+    VCCL_FUNNEL_CASE(2)
+    default:
+    VCCL_FUNNEL_CASE(3)
+#undef VCCL_FUNNEL_CASE
+  }
+  return o;
+}
+
+// The 16 bytes at alignedBase + off + k (k != 0, alignedBase + off 16-byte
+// aligned): this lane's aligned pack funnel-shifted with the next one, which
+// the next lane of the wave loaded (lane 63 loads it at offNext itself).
+template <int P>
+__device__ __forceinline__ u32x4 ld16_shifted(const char* alignedBase, int64_t off, int64_t offNext,
+                                              int k) {
+  const u32x4 cur = ld16<P>(alignedBase, off);
+  u32x4 nxt;
+  nxt.x = __shfl_down(cur.x, 1);
+  nxt.y = __shfl_down(cur.y, 1);
+  nxt.z = __shfl_down(cur.z, 1);
+  nxt.w = __shfl_down(cur.w, 1);
+  if (__lane_id() == 63) nxt = ld16<P>(alignedBase, offNext);
+  return funnel16(cur, nxt, k);
+}
+
+template <int POLS>
+__device__ __forceinline__ u32x4 ld16_src_shifted(const RCArgs& a, int s, int64_t off, int64_t offNext) {
+  const char* p = src_ptr(a, s);
+  const int k = (int)((uintptr_t)p & 15);
+  if (k == 0) return ld16_src<POLS>(a, s, off);
+  switch (s) {
+    case 0: return ld16_shifted<src_pol(POLS, 0)>(p - k, off, offNext, k);
+    case 1: return ld16_shifted<src_pol(POLS, 1)>(p - k, off, offNext, k);
+    case 2: return ld16_shifted<src_pol(POLS, 2)>(p - k, off, offNext, k);
+    default: return ld16_shifted<src_pol(POLS, 3)>(p - k, off, offNext, k);
+  }
+}
+
+// Body packs [0, nPacks) when every destination is 16-byte aligned and source
+// s starts k_s bytes past a 16-byte boundary.  Whole waves run (the shuffle
+// needs every lane): a lane past the end loads aligned pack nPacks (the one
+// holding the body's last bytes, so it cannot fault) and stores nothing.
+template <class Fn, int UNROLL, int POLS>
+__device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, int64_t nPacks,
+                                                 int64_t worker, int64_t nWorkers, int tid,
+                                                 int nthreads) {
+  const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
+  const int64_t nHunks = (nPacks + hunkPacks - 1) / hunkPacks;
+  for (int64_t h = worker; h < nHunks; h += nWorkers) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const int64_t p = h * hunkPacks + (int64_t)u * nthreads + tid;
+      if (p - __lane_id() >= nPacks) continue;  // the whole wave is past the end
+      const int64_t off = (p < nPacks ? p : nPacks) * 16;
+      const int64_t offNext = (p + 1 < nPacks ? p + 1 : nPacks) * 16;
+      u32x4 acc = ld16_src_shifted<POLS>(a, 0, off, offNext);
+      if (Fn::kPreOp && a.preOpSrcs > 0) acc = pack_preop(fn, acc);
+      for (int s = 1; s < a.nSrcs; s++) {
+        u32x4 v = ld16_src_shifted<POLS>(a, s, off, offNext);
+        if (Fn::kPreOp && s < a.preOpSrcs) v = pack_preop(fn, v);
+        acc = pack_reduce(fn, acc, v);
+      }
+      if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
+      if (p < nPacks)
+        for (int d = 0; d < a.nDsts; d++) st16_dst<POLS>(a, d, off, acc);
+    }
+  }
+}
+
 __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
   uintptr_t bits = 0;
   for (int s = 0; s < a.nSrcs; s++) bits |= (uintptr_t)src_ptr(a, s);
@@ -325,6 +423,37 @@ __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
 // Full reduce-copy of nElts elements by `nWorkers` cooperating workgroups of
 // `nthreads` threads (this workgroup = `worker`).  Pointers in `a` are the
 // element-0 addresses.  Wave-uniform control flow throughout.
+template <class Fn, int POLS>
+__device__ __forceinline__ void reduce_copy_misaligned(const Fn& fn, const RCArgs& a, int64_t nElts,
+                                                    int64_t worker, int64_t nWorkers, int tid,
+                                                    int nthreads) {
+  using T = typename Fn::EltType;
+  const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
+  constexpr int esz = (int)sizeof(T);
+  const int m = (int)((uintptr_t)a.dsts[0] & 15);
+  bool ok = m % esz == 0;
+  for (int d = 1; d < a.nDsts; d++) ok = ok && (int)((uintptr_t)dst_ptr(a, d) & 15) == m;
+  for (int s = 0; s < a.nSrcs; s++) ok = ok && ((uintptr_t)src_ptr(a, s) & (esz - 1)) == 0;
+  if (!ok) {
+    rc_elems<Fn, POLS>(fn, a, 0, nElts, gtid, gthreads);
+    return;
+  }
+  int64_t he = ((16 - m) & 15) / esz;
+  if (he > nElts) he = nElts;
+  if (he > 0) rc_elems<Fn, POLS>(fn, a, 0, he, gtid, gthreads);
+  const int64_t nPacks = (nElts - he) * esz / 16;
+  if (nPacks > 0) {
+    RCArgs b = a;
+#pragma unroll
+    for (int s = 0; s < kMaxSrcs; s++) b.srcs[s] = a.srcs[s] + he * esz;
+#pragma unroll
+    for (int d = 0; d < kMaxDsts; d++) b.dsts[d] = a.dsts[d] + he * esz;
+    rc_hunks_shifted<Fn, 2, POLS>(fn, b, nPacks, worker, nWorkers, tid, nthreads);
+  }
+  const int64_t eDone = he + nPacks * 16 / esz;
+  if (eDone < nElts) rc_elems<Fn, POLS>(fn, a, eDone, nElts, gtid, gthreads);
+}
+
 template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false>
 __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
                                             int64_t worker, int64_t nWorkers, int tid,
@@ -333,7 +462,7 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
   const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
   if (nElts <= 0) return;
   if (!rc_all_aligned16(a)) {
-    rc_elems<Fn, POLS>(fn, a, 0, nElts, gtid, gthreads);
+    reduce_copy_misaligned<Fn, POLS>(fn, a, nElts, worker, nWorkers, tid, nthreads);
     return;
   }
   const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;

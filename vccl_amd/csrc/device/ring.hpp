@@ -72,8 +72,10 @@ struct RingCtx {
   // One primitive call: at most one slot of payload.
   //   srcs = [SRC ? own input] ++ [RECV ? recv slot]
   //   dsts = [SEND ? peer slot] ++ [DST ? own output]
+  //   recvOff / sendOff: byte offset of the chunk inside its slot (< 16)
   template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
-  __device__ void prim(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp) {
+  __device__ void prim(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
+                       int recvOff = 0, int sendOff = 0) {
     if (aborted()) return;
     if (tid == 0) {
       bool ok = true;
@@ -98,8 +100,8 @@ struct RingCtx {
       RCArgs a;
       int s = 0, d = 0;
       if (SRC) a.srcs[s++] = (const char*)src;
-      if (RECV) a.srcs[s++] = ch->recvFifo + (int64_t)(recvStep % kSteps) * slotBytes;
-      if (SEND) a.dsts[d++] = ch->sendFifo + (int64_t)(sendStep % kSteps) * slotBytes;
+      if (RECV) a.srcs[s++] = ch->recvFifo + (int64_t)(recvStep % kSteps) * slot_stride(slotBytes) + recvOff;
+      if (SEND) a.dsts[d++] = ch->sendFifo + (int64_t)(sendStep % kSteps) * slot_stride(slotBytes) + sendOff;
       if (DST) a.dsts[d++] = (char*)dst;
       a.nSrcs = NS;
       a.nDsts = ND;
@@ -192,18 +194,24 @@ __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, 
   T* out = (T*)w.recvbuff;
   const int* ringRanks = r.ch->ringRanks;
   const int64_t chunkCount = w.slotBytes / (int64_t)sizeof(T);
+  // A chunk for rank k sits in its slots at k's block misalignment (the same
+  // on every rank: dataOff is a 16-byte multiple), so the FIFO operand shares
+  // the input block's alignment (reduce_copy_misaligned).
+  auto mis = [&](int k) { return (int)(((int64_t)k * count * (int64_t)sizeof(T)) & 15); };
   for (int64_t eo = 0; eo < chCount; eo += chunkCount) {
     const int64_t nelem = chCount - eo < chunkCount ? chCount - eo : chunkCount;
     const int64_t dataOff = gridOff + eo;
     int rankDest = ringRanks[n - 1];
-    r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false);
+    r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false,
+                                                 0, mis(rankDest));
     for (int j = 2; j < n; ++j) {
       rankDest = ringRanks[n - j];
-      r.prim<Fn, true, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false);
+      r.prim<Fn, true, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false,
+                                                  mis(rankDest), mis(rankDest));
     }
     rankDest = ringRanks[0];
     r.prim<Fn, true, false, true, true, UNROLL>(fn, in + dataOff + rankDest * count, out + dataOff,
-                                                nelem, true);
+                                                nelem, true, mis(rankDest), 0);
   }
 }
 
@@ -221,23 +229,29 @@ __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
   uint8_t* out = (uint8_t*)w.recvbuff;
   const int* ringRanks = r.ch->ringRanks;
   const int64_t chunkCount = w.slotBytes;
+  // A block for rank k travels at k's output misalignment inside the slots
+  // (same on every rank), so the slot and the output block share alignment.
+  auto mis = [&](int k) { return (int)(((int64_t)k * count) & 15); };
   for (int64_t eo = 0; eo < partCount; eo += chunkCount) {
     const int64_t nelem = partCount - eo < chunkCount ? partCount - eo : chunkCount;
     const int64_t dataOff = partOff + eo;
     int rankDest = ringRanks[0];
     int64_t off = dataOff + rankDest * count;
     if (in + dataOff == out + off)
-      r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff, nullptr, nelem, false);
+      r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff, nullptr, nelem, false, 0,
+                                                   mis(rankDest));
     else
-      r.prim<Fn, false, true, true, true, UNROLL>(fn, in + dataOff, out + off, nelem, false);
+      r.prim<Fn, false, true, true, true, UNROLL>(fn, in + dataOff, out + off, nelem, false, 0,
+                                                  mis(rankDest));
     for (int j = 1; j < n - 1; ++j) {
       rankDest = ringRanks[n - j];
       off = dataOff + rankDest * count;
-      r.prim<Fn, true, true, false, true, UNROLL>(fn, nullptr, out + off, nelem, false);
+      r.prim<Fn, true, true, false, true, UNROLL>(fn, nullptr, out + off, nelem, false, mis(rankDest),
+                                                  mis(rankDest));
     }
     rankDest = ringRanks[1];
     off = dataOff + rankDest * count;
-    r.prim<Fn, true, false, false, true, UNROLL>(fn, nullptr, out + off, nelem, false);
+    r.prim<Fn, true, false, false, true, UNROLL>(fn, nullptr, out + off, nelem, false, mis(rankDest), 0);
   }
 }
 

@@ -20,6 +20,11 @@ constexpr int kSteps = 8;            // NCCL_STEPS (device.h:24)
 constexpr int kMaxRanks = 64;
 constexpr int kMaxChannels = 64;     // MAXCHANNELS (device.h:62)
 constexpr int kFlagStride = 128;     // bytes between flags (one line each)
+// Slot stride = slotBytes + kSlotPad: RS / AG place a chunk at byte offset
+// (logical offset mod 16) inside its slot, so the slot shares the user
+// block's misalignment and the copy stays on 16-byte packs (ring.hpp).
+constexpr int kSlotPad = 64;
+__host__ __device__ constexpr int64_t slot_stride(int slotBytes) { return (int64_t)slotBytes + kSlotPad; }
 
 struct DevChannel {
   // ring order: ringRanks[k] = rank at ring position (myPos + k) mod n

@@ -178,7 +178,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     me.busId = ((int64_t)dom << 16) | (bus << 8) | dev;
   }
   if (n > 1) {
-    const size_t fifoBytes = (size_t)c->nChannels * kSteps * c->slotBytes;
+    const size_t fifoBytes = (size_t)c->nChannels * kSteps * slot_stride(c->slotBytes);
     const size_t flagBytes = (size_t)c->nChannels * 2 * kFlagStride;
     VINFO("rank %d: alloc fifo %zu B", c->rank, fifoBytes);
     NCCLCHECK(alloc_uncached((void**)&c->fifoBuf, fifoBytes));
@@ -302,7 +302,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       }
     }
     std::vector<DevChannel> chans(c->nChannels);
-    const size_t fifoPerCh = (size_t)kSteps * c->slotBytes;
+    const size_t fifoPerCh = (size_t)kSteps * slot_stride(c->slotBytes);
     for (int ch = 0; ch < c->nChannels; ch++) {
       const auto& ring = rings[ch % nRings];
       int pos = (int)(std::find(ring.begin(), ring.end(), c->rank) - ring.begin());
