@@ -353,63 +353,131 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, int k) {
   return o;
 }
 
-// The 16 bytes at alignedBase + off + k (k != 0, alignedBase + off 16-byte
-// aligned): this lane's aligned pack funnel-shifted with the next one, which
-// the next lane of the wave loaded (lane 63 loads it at offNext itself).
+// Load of source s for the shifted body: an aligned source reads its own pack
+// (clamped to the last body pack, never past the body); a source k bytes past
+// a 16-byte boundary reads the aligned pack at or below (clamped to pack
+// nPacks, which still holds body bytes, so it cannot fault).
 template <int P>
-__device__ __forceinline__ u32x4 ld16_shifted(const char* alignedBase, int64_t off, int64_t offNext,
-                                              int k) {
-  const u32x4 cur = ld16<P>(alignedBase, off);
+__device__ __forceinline__ u32x4 ld16_body(const char* p, int k, int64_t pk, int64_t nPacks) {
+  if (k == 0) return ld16<P>(p, (pk < nPacks ? pk : nPacks - 1) * 16);
+  return ld16<P>(p - k, (pk < nPacks ? pk : nPacks) * 16);
+}
+template <int POLS>
+__device__ __forceinline__ u32x4 ld16_body_src(const RCArgs& a, int s, int k, int64_t pk,
+                                               int64_t nPacks) {
+  switch (s) {
+    case 0: return ld16_body<src_pol(POLS, 0)>(a.srcs[0], k, pk, nPacks);
+    case 1: return ld16_body<src_pol(POLS, 1)>(a.srcs[1], k, pk, nPacks);
+    case 2: return ld16_body<src_pol(POLS, 2)>(a.srcs[2], k, pk, nPacks);
+    default: return ld16_body<src_pol(POLS, 3)>(src_ptr(a, s), k, pk, nPacks);
+  }
+}
+// The aligned pack at byte offset `off` below source s's start (k bytes past
+// a boundary): lane 63's successor pack.
+template <int POLS>
+__device__ __forceinline__ u32x4 ld16_succ_src(const RCArgs& a, int s, int k, int64_t off) {
+  switch (s) {
+    case 0: return ld16<src_pol(POLS, 0)>(a.srcs[0] - k, off);
+    case 1: return ld16<src_pol(POLS, 1)>(a.srcs[1] - k, off);
+    case 2: return ld16<src_pol(POLS, 2)>(a.srcs[2] - k, off);
+    default: return ld16<src_pol(POLS, 3)>(src_ptr(a, s) - k, off);
+  }
+}
+// This lane's pack funnel-shifted with the next lane's (wavefront shuffle);
+// lane 63 supplies `ext`, its own load of the successor pack.
+__device__ __forceinline__ u32x4 realign(u32x4 cur, u32x4 ext, int k) {
   u32x4 nxt;
   nxt.x = __shfl_down(cur.x, 1);
   nxt.y = __shfl_down(cur.y, 1);
   nxt.z = __shfl_down(cur.z, 1);
   nxt.w = __shfl_down(cur.w, 1);
-  if (__lane_id() == 63) nxt = ld16<P>(alignedBase, offNext);
+  if (__lane_id() == 63) nxt = ext;
   return funnel16(cur, nxt, k);
 }
 
-template <int POLS>
-__device__ __forceinline__ u32x4 ld16_src_shifted(const RCArgs& a, int s, int64_t off, int64_t offNext) {
-  const char* p = src_ptr(a, s);
-  const int k = (int)((uintptr_t)p & 15);
-  if (k == 0) return ld16_src<POLS>(a, s, off);
-  switch (s) {
-    case 0: return ld16_shifted<src_pol(POLS, 0)>(p - k, off, offNext, k);
-    case 1: return ld16_shifted<src_pol(POLS, 1)>(p - k, off, offNext, k);
-    case 2: return ld16_shifted<src_pol(POLS, 2)>(p - k, off, offNext, k);
-    default: return ld16_shifted<src_pol(POLS, 3)>(p - k, off, offNext, k);
-  }
-}
-
 // Body packs [0, nPacks) when every destination is 16-byte aligned and source
-// s starts k_s bytes past a 16-byte boundary.  Whole waves run (the shuffle
-// needs every lane): a lane past the end loads aligned pack nPacks (the one
-// holding the body's last bytes, so it cannot fault) and stores nothing.
-template <class Fn, int UNROLL, int POLS>
+// s starts k_s bytes past a 16-byte boundary (some k_s != 0).  Whole waves
+// run (the shuffle needs every lane); a lane past the end loads clamped packs
+// and stores nothing.  NS / ND compile-time (NS > 0): every load of a hunk —
+// the aligned packs and lane 63's successor packs — is issued before the
+// first shuffle, so their latencies overlap.
+template <class Fn, int NS, int ND, int UNROLL, int POLS>
 __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, int64_t nPacks,
                                                  int64_t worker, int64_t nWorkers, int tid,
                                                  int nthreads) {
+  static_assert(NS >= 1 && NS <= kMaxSrcs, "compile-time source count");
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t nHunks = (nPacks + hunkPacks - 1) / hunkPacks;
+  const bool last = __lane_id() == 63;
+  int k[NS];
+#pragma unroll
+  for (int s = 0; s < NS; s++) k[s] = (int)((uintptr_t)src_ptr(a, s) & 15);
   for (int64_t h = worker; h < nHunks; h += nWorkers) {
+    const int64_t p0 = h * hunkPacks + tid;
+    if (p0 - __lane_id() >= nPacks) continue;  // the whole wave is past the end
+    u32x4 cur[NS][UNROLL], ext[NS][UNROLL];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++)
+        cur[s][u] = ld16_body_src<POLS>(a, s, k[s], p0 + (int64_t)u * nthreads, nPacks);
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++) {
+        ext[s][u] = cur[s][u];
+        const int64_t pn = p0 + (int64_t)u * nthreads + 1;
+        if (k[s] != 0 && last)
+          ext[s][u] = ld16_succ_src<POLS>(a, s, k[s], (pn < nPacks ? pn : nPacks) * 16);
+      }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
-      const int64_t p = h * hunkPacks + (int64_t)u * nthreads + tid;
-      if (p - __lane_id() >= nPacks) continue;  // the whole wave is past the end
-      const int64_t off = (p < nPacks ? p : nPacks) * 16;
-      const int64_t offNext = (p + 1 < nPacks ? p + 1 : nPacks) * 16;
-      u32x4 acc = ld16_src_shifted<POLS>(a, 0, off, offNext);
+      const int64_t p = p0 + (int64_t)u * nthreads;
+      u32x4 acc = k[0] ? realign(cur[0][u], ext[0][u], k[0]) : cur[0][u];
       if (Fn::kPreOp && a.preOpSrcs > 0) acc = pack_preop(fn, acc);
-      for (int s = 1; s < a.nSrcs; s++) {
-        u32x4 v = ld16_src_shifted<POLS>(a, s, off, offNext);
+#pragma unroll
+      for (int s = 1; s < NS; s++) {
+        u32x4 v = k[s] ? realign(cur[s][u], ext[s][u], k[s]) : cur[s][u];
         if (Fn::kPreOp && s < a.preOpSrcs) v = pack_preop(fn, v);
         acc = pack_reduce(fn, acc, v);
       }
       if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
-      if (p < nPacks)
-        for (int d = 0; d < a.nDsts; d++) st16_dst<POLS>(a, d, off, acc);
+      if (p < nPacks) {
+#pragma unroll
+        for (int d = 0; d < ND; d++) st16_dst<POLS>(a, d, p * 16, acc);
+      }
     }
+  }
+}
+
+// Runtime operand counts (any nSrcs / nDsts up to the maxima), one pack per
+// thread per step.
+template <class Fn, int POLS>
+__device__ __forceinline__ void rc_hunks_shifted_rt(const Fn& fn, const RCArgs& a, int64_t nPacks,
+                                                    int64_t worker, int64_t nWorkers, int tid,
+                                                    int nthreads) {
+  const int64_t nSteps = (nPacks + nthreads - 1) / nthreads;
+  for (int64_t h = worker; h < nSteps; h += nWorkers) {
+    const int64_t p = h * nthreads + tid;
+    if (p - __lane_id() >= nPacks) continue;
+    auto load = [&](int s) __attribute__((always_inline)) -> u32x4 {
+      const int k = (int)((uintptr_t)src_ptr(a, s) & 15);
+      const u32x4 cur = ld16_body_src<POLS>(a, s, k, p, nPacks);
+      if (k == 0) return cur;
+      u32x4 ext = cur;
+      if (__lane_id() == 63) ext = ld16_succ_src<POLS>(a, s, k, (p + 1 < nPacks ? p + 1 : nPacks) * 16);
+      return realign(cur, ext, k);
+    };
+    u32x4 acc = load(0);
+    if (Fn::kPreOp && a.preOpSrcs > 0) acc = pack_preop(fn, acc);
+    for (int s = 1; s < a.nSrcs; s++) {
+      u32x4 v = load(s);
+      if (Fn::kPreOp && s < a.preOpSrcs) v = pack_preop(fn, v);
+      acc = pack_reduce(fn, acc, v);
+    }
+    if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
+    if (p < nPacks)
+      for (int d = 0; d < a.nDsts; d++) st16_dst<POLS>(a, d, p * 16, acc);
   }
 }
 
@@ -420,51 +488,13 @@ __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
   return (bits & 15) == 0;
 }
 
-// Full reduce-copy of nElts elements by `nWorkers` cooperating workgroups of
-// `nthreads` threads (this workgroup = `worker`).  Pointers in `a` are the
-// element-0 addresses.  Wave-uniform control flow throughout.
-template <class Fn, int POLS>
-__device__ __forceinline__ void reduce_copy_misaligned(const Fn& fn, const RCArgs& a, int64_t nElts,
+// Aligned operands: full hunks, then < one hunk of packs, then < 16 bytes.
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER, bool PIPE>
+__device__ __forceinline__ void reduce_copy_aligned(const Fn& fn, const RCArgs& a, int64_t nElts,
                                                     int64_t worker, int64_t nWorkers, int tid,
                                                     int nthreads) {
   using T = typename Fn::EltType;
   const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
-  constexpr int esz = (int)sizeof(T);
-  const int m = (int)((uintptr_t)a.dsts[0] & 15);
-  bool ok = m % esz == 0;
-  for (int d = 1; d < a.nDsts; d++) ok = ok && (int)((uintptr_t)dst_ptr(a, d) & 15) == m;
-  for (int s = 0; s < a.nSrcs; s++) ok = ok && ((uintptr_t)src_ptr(a, s) & (esz - 1)) == 0;
-  if (!ok) {
-    rc_elems<Fn, POLS>(fn, a, 0, nElts, gtid, gthreads);
-    return;
-  }
-  int64_t he = ((16 - m) & 15) / esz;
-  if (he > nElts) he = nElts;
-  if (he > 0) rc_elems<Fn, POLS>(fn, a, 0, he, gtid, gthreads);
-  const int64_t nPacks = (nElts - he) * esz / 16;
-  if (nPacks > 0) {
-    RCArgs b = a;
-#pragma unroll
-    for (int s = 0; s < kMaxSrcs; s++) b.srcs[s] = a.srcs[s] + he * esz;
-#pragma unroll
-    for (int d = 0; d < kMaxDsts; d++) b.dsts[d] = a.dsts[d] + he * esz;
-    rc_hunks_shifted<Fn, 2, POLS>(fn, b, nPacks, worker, nWorkers, tid, nthreads);
-  }
-  const int64_t eDone = he + nPacks * 16 / esz;
-  if (eDone < nElts) rc_elems<Fn, POLS>(fn, a, eDone, nElts, gtid, gthreads);
-}
-
-template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false>
-__device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
-                                            int64_t worker, int64_t nWorkers, int tid,
-                                            int nthreads) {
-  using T = typename Fn::EltType;
-  const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
-  if (nElts <= 0) return;
-  if (!rc_all_aligned16(a)) {
-    reduce_copy_misaligned<Fn, POLS>(fn, a, nElts, worker, nWorkers, tid, nthreads);
-    return;
-  }
   const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t fullPacks = (nPacks / hunkPacks) * hunkPacks;
@@ -487,6 +517,60 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
   }
   // Element tail (< 16 bytes).
   const int64_t eDone = nPacks * 16 / (int64_t)sizeof(T);
+  if (eDone < nElts) rc_elems<Fn, POLS>(fn, a, eDone, nElts, gtid, gthreads);
+}
+
+// Full reduce-copy of nElts elements by `nWorkers` cooperating workgroups of
+// `nthreads` threads (this workgroup = `worker`).  Pointers in `a` are the
+// element-0 addresses.  Wave-uniform control flow throughout (every branch
+// below depends on pointers and counts only).
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false>
+__device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
+                                            int64_t worker, int64_t nWorkers, int tid,
+                                            int nthreads) {
+  using T = typename Fn::EltType;
+  constexpr int esz = (int)sizeof(T);
+  const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
+  if (nElts <= 0) return;
+  if (rc_all_aligned16(a)) {
+    reduce_copy_aligned<Fn, NS, ND, UNROLL, POLS, ORDER, PIPE>(fn, a, nElts, worker, nWorkers, tid,
+                                                               nthreads);
+    return;
+  }
+  // Misaligned (see above): destinations must share one misalignment m.
+  const int m = (int)((uintptr_t)a.dsts[0] & 15);
+  bool ok = m % esz == 0;
+  for (int d = 1; d < a.nDsts; d++) ok = ok && (int)((uintptr_t)dst_ptr(a, d) & 15) == m;
+  for (int s = 0; s < a.nSrcs; s++) ok = ok && ((uintptr_t)src_ptr(a, s) & (esz - 1)) == 0;
+  if (!ok) {
+    rc_elems<Fn, POLS>(fn, a, 0, nElts, gtid, gthreads);
+    return;
+  }
+  int64_t he = ((16 - m) & 15) / esz;
+  if (he > nElts) he = nElts;
+  if (he > 0) rc_elems<Fn, POLS>(fn, a, 0, he, gtid, gthreads);
+  if (he == nElts) return;
+  RCArgs b = a;
+#pragma unroll
+  for (int s = 0; s < kMaxSrcs; s++) b.srcs[s] = a.srcs[s] + he * esz;
+#pragma unroll
+  for (int d = 0; d < kMaxDsts; d++) b.dsts[d] = a.dsts[d] + he * esz;
+  if (rc_all_aligned16(b)) {  // one common misalignment: the aligned engine past the head
+    reduce_copy_aligned<Fn, NS, ND, UNROLL, POLS, ORDER, PIPE>(fn, b, nElts - he, worker, nWorkers,
+                                                               tid, nthreads);
+    return;
+  }
+  const int64_t nPacks = (nElts - he) * esz / 16;
+  if (nPacks > 0) {
+    // batched loads for the grid kernels; the in-ring copy (PIPE, a 1024-thread
+    // workgroup with a 128-VGPR budget) keeps the lean one-pack loop
+    if constexpr (NS >= 1 && ND >= 1 && !PIPE)
+      rc_hunks_shifted<Fn, NS, ND, (UNROLL < 2 ? UNROLL : 2), POLS>(fn, b, nPacks, worker, nWorkers,
+                                                                    tid, nthreads);
+    else
+      rc_hunks_shifted_rt<Fn, POLS>(fn, b, nPacks, worker, nWorkers, tid, nthreads);
+  }
+  const int64_t eDone = he + nPacks * 16 / esz;
   if (eDone < nElts) rc_elems<Fn, POLS>(fn, a, eDone, nElts, gtid, gthreads);
 }
 
