@@ -184,6 +184,37 @@ def test_multi_process_ranks(n, geom):
         assert (fused > 0) == (ll_max > 0), f"fused group launches: {fused} (LL max {ll_max})"
 
 
+def test_beyond_2gib_two_ranks():
+    """Per-rank buffers past 2 GiB (BASELINE config 4 is 4 GiB per rank): user
+    buffer and FIFO / inbox accesses must address bytes beyond a 32-bit
+    offset.  Two processes (one HIP queue set each, so the two ranks' kernels
+    are co-resident) run ring AR, direct AR, ring RS and ring AG
+    (tests/mp_big_worker.py checks each output with torch)."""
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.update(TEST_GEOM)
+    env.pop("VCCL_DIRECT_THRESHOLD")  # direct: no size cap, default 16 MiB inbox chunks
+    env.pop("VCCL_DIRECT_CHUNK_BYTES")
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    n = 2
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_big_worker.py"),
+                               str(r), str(n), "0", hexid], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(n)]
+    logs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(out.decode(errors="replace")[-2000:])
+    codes = [p.returncode for p in procs]
+    assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
+
+
 def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk):
     for gi, (name, op, dt, count) in enumerate(RC.GROUP_CASES):
         exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk)

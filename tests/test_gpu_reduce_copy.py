@@ -175,6 +175,30 @@ def test_full_size_config2_bitexact():
     assert torch.equal(d.view(torch.int32), ref.view(torch.int32))
 
 
+@pytest.mark.parametrize("offs", [(0, 0, 0), (0, 1, 0), (1, 1, 1), (0, 0, 1)],
+                         ids=["aligned", "shifted_src1", "common_misalign", "element_dst"])
+def test_beyond_2gib(offs):
+    """Buffers past 2 GiB: every access policy (nt, write-through sc0 sc1 buffer
+    stores, shifted-source realignment, element path) must address bytes beyond
+    a 32-bit signed offset.  offs = f32-element offsets of (src0, src1, dst)."""
+    n = (1 << 29) + 1037  # 2 GiB + 4148 B per buffer
+    g = torch.Generator(device="cuda").manual_seed(7)
+    bufs = []
+    for o in offs:
+        t = torch.empty(n + o, device="cuda")
+        bufs.append(t[o:])
+    a, b, d = bufs
+    a.uniform_(-1, 1, generator=g)
+    b.uniform_(-1, 1, generator=g)
+    d.fill_(float("nan"))
+    nccl.reduce_copy(0, 7, 0, [a.data_ptr(), b.data_ptr()], [d.data_ptr()], n, stream_ptr())
+    torch.cuda.synchronize()
+    ref = a + b
+    assert torch.equal(d.view(torch.int32), ref.view(torch.int32))
+    del a, b, d, ref, bufs
+    torch.cuda.empty_cache()
+
+
 def test_abi_errors():
     L = nccl.lib()
     import ctypes

@@ -96,10 +96,10 @@ __device__ __forceinline__ uint64_t ll_apply(const Fn& fn, uint64_t acc, uint64_
 // Poll one LL line until both halves carry `epoch`; returns the 8 data bytes.
 __device__ __forceinline__ bool ll_read_line(const char* line, uint32_t epoch, const DevComm* comm,
                                              uint64_t* out) {
-  const __amdgpu_buffer_rsrc_t r = sys_rsrc(line);
+  const SysAddr s = sys_addr(line);
   uint64_t spins = 0, start = 0;
   for (;;) {
-    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, kSysAux);
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(s.r, s.voff, 0, kSysAux);
     if (v.y == epoch && v.w == epoch) {
       *out = (uint64_t)v.x | ((uint64_t)v.z << 32);
       return true;
@@ -183,8 +183,8 @@ __device__ void ll_allreduce(const LLWork& w) {
     line.w = e;
     for (int k = 1; k < w.nRanks; k++) {
       const int peer = w.rank + k < w.nRanks ? w.rank + k : w.rank + k - w.nRanks;
-      char* dst = w.peerBuf[peer] + ll_slot_off(parity, w.rank, w.nRanks, w.linesPerSlot) + l * 16;
-      __builtin_amdgcn_raw_buffer_store_b128(line, sys_rsrc(dst), 0, 0, kSysAux);
+      const SysAddr d = sys_addr(w.peerBuf[peer] + ll_slot_off(parity, w.rank, w.nRanks, w.linesPerSlot) + l * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(line, d.r, d.voff, 0, kSysAux);
     }
   }
   // Phase 2: fold all inputs in chain order, x_0 (+) (x_1 (+) (... x_{n-1})).
@@ -204,10 +204,10 @@ __device__ void ll_allreduce(const LLWork& w) {
 #pragma unroll
       for (int b = 0; b < kLLBatch; b++) {
         const int p = hi - b;
-        if (p >= lo && p != w.rank)
-          v[b] = __builtin_amdgcn_raw_buffer_load_b128(
-              sys_rsrc(w.localBuf + ll_slot_off(parity, p, w.nRanks, w.linesPerSlot) + l * 16), 0, 0,
-              kSysAux);
+        if (p >= lo && p != w.rank) {
+          const SysAddr a = sys_addr(w.localBuf + ll_slot_off(parity, p, w.nRanks, w.linesPerSlot) + l * 16);
+          v[b] = __builtin_amdgcn_raw_buffer_load_b128(a.r, a.voff, 0, kSysAux);
+        }
       }
 #pragma unroll
       for (int b = 0; b < kLLBatch; b++) {

@@ -46,33 +46,51 @@ constexpr int dst_pol(int POLS, int d) { return (POLS >> (8 + 2 * (d < 3 ? d : 3
 constexpr int kSysAux = 1 | 16;  // cache-policy bits sc0 | sc1 (gfx940+ CPol)
 constexpr int kSc1NTAux = 2 | 16;  // nt | sc1: streamed, L1-bypassing
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const char* base) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+// Buffer descriptor + lane offset for a system-coherent access to `a`.  The
+// descriptor is built from the FIRST ACTIVE LANE's address (readfirstlane),
+// so hipcc can prove it wave-uniform and emits no waterfall loop around the
+// buffer op (cdna_hip_programming.md T20); every other lane's distance from
+// it is the 32-bit voffset.  Every caller's lane addresses grow with the lane
+// index and span < 2 GiB within a wave, so voffset >= 0 and buffers past
+// 2 GiB are addressed correctly (an offset folded into a 32-bit voffset from
+// a fixed base would not be).
+struct SysAddr {
+  __amdgpu_buffer_rsrc_t r;
+  int voff;
+};
+__device__ __forceinline__ SysAddr sys_addr(const char* a) {
+  const uint64_t x = (uint64_t)(uintptr_t)a;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  const uint64_t x0 = ((uint64_t)hi << 32) | lo;
+  return {__builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)x0, 0, 0x7fffffff, 0x00020000),
+          (int)(x - x0)};
 }
 
 template <int P>
 __device__ __forceinline__ u32x4 ld16(const char* base, int64_t off) {
   if constexpr (P == kNT) return __builtin_nontemporal_load((const u32x4*)(base + off));
-  else if constexpr (P == kSys)
-    return __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base), (int)off, 0, kSysAux);
-  else if constexpr (P == kSc1NT)
-    return __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base), (int)off, 0, kSc1NTAux);
-  else return *(const u32x4*)(base + off);
+  else if constexpr (P == kSys || P == kSc1NT) {
+    const SysAddr s = sys_addr(base + off);
+    return __builtin_amdgcn_raw_buffer_load_b128(s.r, s.voff, 0, P == kSys ? kSysAux : kSc1NTAux);
+  } else return *(const u32x4*)(base + off);
 }
 template <int P>
 __device__ __forceinline__ void st16(char* base, int64_t off, u32x4 v) {
   if constexpr (P == kNT) __builtin_nontemporal_store(v, (u32x4*)(base + off));
-  else if constexpr (P == kSys) __builtin_amdgcn_raw_buffer_store_b128(v, sys_rsrc(base), (int)off, 0, kSysAux);
-  else if constexpr (P == kSc1NT) __builtin_amdgcn_raw_buffer_store_b128(v, sys_rsrc(base), (int)off, 0, kSc1NTAux);
-  else *(u32x4*)(base + off) = v;
+  else if constexpr (P == kSys || P == kSc1NT) {
+    const SysAddr s = sys_addr(base + off);
+    __builtin_amdgcn_raw_buffer_store_b128(v, s.r, s.voff, 0, P == kSys ? kSysAux : kSc1NTAux);
+  } else *(u32x4*)(base + off) = v;
 }
 
 // Element-sized accesses (T = 1, 2, 4 or 8 bytes), same policies.
 template <int P, typename T>
 __device__ __forceinline__ T ldT(const char* base, int64_t i) {
   if constexpr (P == kSys) {
-    auto r = sys_rsrc(base);
-    const int off = (int)(i * (int64_t)sizeof(T));
+    const SysAddr s = sys_addr(base + i * (int64_t)sizeof(T));
+    const auto r = s.r;
+    const int off = s.voff;
     if constexpr (sizeof(T) == 1) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, kSysAux));
     else if constexpr (sizeof(T) == 2) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, kSysAux));
     else if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSysAux));
@@ -84,8 +102,9 @@ __device__ __forceinline__ T ldT(const char* base, int64_t i) {
 template <int P, typename T>
 __device__ __forceinline__ void stT(char* base, int64_t i, T v) {
   if constexpr (P == kSys) {
-    auto r = sys_rsrc(base);
-    const int off = (int)(i * (int64_t)sizeof(T));
+    const SysAddr s = sys_addr(base + i * (int64_t)sizeof(T));
+    const auto r = s.r;
+    const int off = s.voff;
     if constexpr (sizeof(T) == 1) __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, v), r, off, 0, kSysAux);
     else if constexpr (sizeof(T) == 2) __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, v), r, off, 0, kSysAux);
     else if constexpr (sizeof(T) == 4) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, kSysAux);
