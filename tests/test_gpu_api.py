@@ -72,6 +72,26 @@ def test_one_rank_all_ops(comm1, dt, tdt, op):
     assert torch.equal(x.view(torch.uint8), w.view(torch.uint8))
 
 
+@pytest.mark.parametrize("nbytes", [1, 1023, 1024, 4097, (1 << 20) - 3, (1 << 20) + 5, 3 << 20])
+@pytest.mark.parametrize("shift", [0, 3])
+def test_one_rank_copy_sizes(comm1, nbytes, shift):
+    """World-size-1 copies on both sides of the kernel-copy / hipMemcpy
+    threshold (1 MiB), misaligned by `shift` bytes: AR, RS and AG."""
+    src = torch.randint(0, 256, (nbytes + shift,), dtype=torch.uint8, device="cuda")[shift:]
+    for coll in ("ar", "rs", "ag"):
+        dst = torch.zeros(nbytes + 2 * shift + 1, dtype=torch.uint8, device="cuda")
+        d = dst[shift:shift + nbytes]
+        if coll == "ar":
+            comm1.all_reduce(src.data_ptr(), d.data_ptr(), nbytes, nccl.ncclUint8, 0, stream_ptr())
+        elif coll == "rs":
+            comm1.reduce_scatter(src.data_ptr(), d.data_ptr(), nbytes, nccl.ncclUint8, 2, stream_ptr())
+        else:
+            comm1.all_gather(src.data_ptr(), d.data_ptr(), nbytes, nccl.ncclUint8, stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(d, src), coll
+        assert int(dst[:shift].sum()) == 0 and int(dst[shift + nbytes:].sum()) == 0, coll
+
+
 def test_user_premulsum(comm1):
     n = 1000
     x = torch.randn(n, device="cuda")

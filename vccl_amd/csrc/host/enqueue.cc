@@ -175,9 +175,22 @@ static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s) {
 // ncclLaunchOneRank (onerank.cu:47-83): a copy, or the PreMulSum kernel.
 static ncclResult_t launch_one_rank(const Task& t) {
   const size_t bytes = t.count * (size_t)type_size(t.datatype);
-  if (t.devOp != OP_PREMULSUM) {
-    if (t.recvbuff != t.sendbuff)
-      HIPCHECK(hipMemcpyAsync(t.recvbuff, t.sendbuff, bytes, hipMemcpyDeviceToDevice, t.stream));
+  if (t.coll == kAllGather || t.devOp != OP_PREMULSUM) {  // AG: a plain copy
+    if (t.recvbuff == t.sendbuff) return ncclSuccess;
+    // Small buckets: the library's own byte-copy kernel (one launch) — a
+    // hipMemcpyAsync D2D costs more host time than the whole 1 KiB copy
+    // (BASELINE config 1).  Large ones: the runtime's copy engine path.
+    static const size_t kKernelCopyMax = (size_t)param_int("ONERANK_KERNEL_COPY_BYTES", 1 << 20);
+    if (bytes <= kKernelCopyMax) {
+      RCArgs a = {};
+      a.srcs[0] = (const char*)t.sendbuff;
+      a.dsts[0] = (char*)t.recvbuff;
+      a.nSrcs = a.nDsts = 1;
+      hipError_t e = reduce_copy_launch(OP_COPY, (int)ncclUint8, 0, a, (int64_t)bytes, nullptr,
+                                        t.stream);
+      return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+    }
+    HIPCHECK(hipMemcpyAsync(t.recvbuff, t.sendbuff, bytes, hipMemcpyDeviceToDevice, t.stream));
     return ncclSuccess;
   }
   RCArgs a = {};
@@ -370,16 +383,17 @@ static ncclResult_t launch_task(const Task& t) {
   int old = -1;
   HIPCHECK(hipGetDevice(&old));
   if (old != t.comm->device) HIPCHECK(hipSetDevice(t.comm->device));
+  // A one-rank in-place call without a preOp enqueues nothing (onerank.cu:
+  // 47-83): no stream bookkeeping either.
+  if (t.comm->nRanks == 1 && t.sendbuff == t.recvbuff &&
+      (t.coll == kAllGather || t.devOp != OP_PREMULSUM)) {
+    t.comm->opCount++;
+    if (old != t.comm->device) (void)hipSetDevice(old);
+    return ncclSuccess;
+  }
   ncclResult_t r = stream_order(t.comm, t.stream);
   if (r == ncclSuccess) {
-    if (t.comm->nRanks == 1 && t.coll == kAllGather) {
-      if (t.recvbuff != t.sendbuff) {
-        hipError_t e = hipMemcpyAsync(t.recvbuff, t.sendbuff,
-                                      t.count * (size_t)type_size(t.datatype),
-                                      hipMemcpyDeviceToDevice, t.stream);
-        r = e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
-      }
-    } else if (t.comm->nRanks == 1) {
+    if (t.comm->nRanks == 1) {
       r = launch_one_rank(t);
     } else {
       const int algo = choose_algo(t);
