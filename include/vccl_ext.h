@@ -16,10 +16,18 @@
  *   vcclCommLaunchStats  collectives enqueued on this communicator so far and
  *                     how many launches carried more than one of them (group
  *                     aggregation of small all-reduces into one LL launch).
+ *   vcclCommNetStats  payload bytes this rank's net proxy has sent / received
+ *                     and its connection count (0 when every peer is reached
+ *                     over xGMI).  The net transport carries ring connections
+ *                     to peers on other nodes (or every connection with
+ *                     VCCL_NET_FORCE=1) through host-pinned staging buffers
+ *                     and TCP, as the reference's proxy + net transport
+ *                     (src/proxy.cc:914-971, src/transport/net.cc:1293-1482).
  */
 #ifndef VCCL_EXT_H_
 #define VCCL_EXT_H_
 #include <stddef.h>
+#include <stdint.h>
 
 #include "nccl.h"
 
@@ -40,6 +48,8 @@ ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count, ncclDataT
 ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo);
 ncclResult_t vcclCommLaunchStats(ncclComm_t comm, unsigned long long* collectives,
                                  unsigned long long* fusedLaunches);
+ncclResult_t vcclCommNetStats(ncclComm_t comm, uint64_t* bytesSent, uint64_t* bytesReceived,
+                              int* connections);
 
 #ifdef __cplusplus
 }

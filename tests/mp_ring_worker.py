@@ -50,6 +50,7 @@ def main():
     res.update(g)
     before = comm.launch_stats()
     res["launch_stats"] = np.array(before, dtype=np.int64)
+    res["net_stats"] = np.array(comm.net_stats(), dtype=np.int64)
     err = comm.async_error()
     comm.destroy()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)

@@ -128,7 +128,7 @@ def test_single_process_ranks(n, monkeypatch):
 
 @pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (8, "test"),
                                     (2, "ring_only"), (4, "ring_only"), (8, "ring_only"),
-                                    (4, "direct_only"), (8, "default8")])
+                                    (4, "direct_only"), (8, "default8"), (2, "net"), (3, "net")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
@@ -144,6 +144,14 @@ def test_multi_process_ranks(n, geom):
         if geom == "direct_only":  # every all-reduce that fits takes the direct path
             env["NCCL_ALGO"] = "Direct"
             ll_max = 0
+    elif geom == "net":
+        # every ring connection through the net proxy (host-pinned staging +
+        # TCP, proxy.cc), as between nodes; LL / direct need the xGMI mesh,
+        # so every all-reduce takes the ring, on NET_NCHANNELS channels
+        env.update(TEST_GEOM)
+        env.update(VCCL_NET_FORCE="1", VCCL_NET_NCHANNELS="3", VCCL_SLOT_BYTES=str(64 << 10))
+        nch, slot = 3, 64 << 10
+        ll_max = direct_max = 0
     elif geom == "default8":
         # library defaults except the LL grid (8 ranks share the one GPU)
         for k in TEST_GEOM:
@@ -182,6 +190,12 @@ def test_multi_process_ranks(n, geom):
                      direct_max, chunk)
         fused = int(res[0]["launch_stats"][1])
         assert (fused > 0) == (ll_max > 0), f"fused group launches: {fused} (LL max {ll_max})"
+        for r in range(n):
+            sent, recvd, conns = (int(v) for v in res[r]["net_stats"])
+            if geom == "net":  # one send and one receive connection per channel
+                assert conns == 2 * nch and sent > 0 and recvd > 0, (r, sent, recvd, conns)
+            else:
+                assert conns == 0 and sent == 0, (r, sent, conns)
 
 
 def test_beyond_2gib_two_ranks():

@@ -116,6 +116,10 @@ struct RingCtx {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system-scope release (L2 writeback)
         drain_vmem();
       }
+      if (SEND && ch->sendSizes)
+        __hip_atomic_store(ch->sendSizes + sendStep % kSteps,
+                           (uint32_t)(nelem > 0 ? sendOff + nelem * (int64_t)sizeof(typename Fn::EltType) : 0),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (SEND) st_sys(ch->nextRecvTail, sendStep + 1);
       if (RECV) st_sys(ch->prevSendHead, recvStep + 1);
     }

@@ -40,6 +40,9 @@ struct DevChannel {
   char* sendFifo;                    // next's recvFifo (remote)
   uint64_t* nextRecvTail;            // next's recvTail (remote)
   uint64_t* sendHead;                // local flag, written by next
+  // Net connection only (null over xGMI): bytes of each posted slot, stored
+  // before the tail so the proxy sends only what the step filled.
+  uint32_t* sendSizes;
   // persistent step counters (kernel reads at start, writes at end)
   uint64_t recvStep;
   uint64_t sendStep;

@@ -225,6 +225,15 @@ ncclResult_t bootstrap_barrier(Bootstrap* b) {
   return bootstrap_allgather(b, tmp.data(), 1);
 }
 
+// IPv4 address (network order) of the interface this rank reaches the root
+// through: the address peers on other nodes can reach this rank at.
+uint32_t bootstrap_local_ip(Bootstrap* b) {
+  sockaddr_in a{};
+  socklen_t sl = sizeof(a);
+  if (!b || getsockname(b->fd, (sockaddr*)&a, &sl) != 0) return htonl(INADDR_LOOPBACK);
+  return a.sin_addr.s_addr;
+}
+
 void bootstrap_close(Bootstrap* b) {
   if (!b) return;
   if (b->fd >= 0) close(b->fd);

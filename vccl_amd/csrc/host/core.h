@@ -60,6 +60,12 @@ ncclResult_t bootstrap_init(const ncclUniqueId* id, int rank, int nranks, Bootst
 ncclResult_t bootstrap_allgather(Bootstrap* b, void* buf, size_t bytes);
 ncclResult_t bootstrap_barrier(Bootstrap* b);
 void bootstrap_close(Bootstrap* b);
+uint32_t bootstrap_local_ip(Bootstrap* b);
+
+// ----------------------------------------------------------------- net proxy
+// Inter-node ring connections through host-pinned staging buffers moved by a
+// proxy thread pair over TCP (proxy.cc).  Opaque here.
+struct NetProxy;
 
 // ----------------------------------------------------------------- rings
 // Ring orders for one node: for n in {2,4,8} the
@@ -73,6 +79,9 @@ struct PeerMap {               // what one rank published about itself
   int device;
   uint64_t hostHash;
   int64_t busId;               // PCI domain/bus/device: the GPU's identity across processes
+  uint32_t netIp;              // net proxy listener (network order), see proxy.cc
+  uint16_t netPort;
+  uint16_t pad0;
   hipIpcMemHandle_t fifoHandle;
   hipIpcMemHandle_t flagHandle;
   hipIpcMemHandle_t llHandle;
@@ -115,6 +124,8 @@ struct ncclComm {
   int64_t dRegionBytes = 0;
   int directMaxBlocks = 0;
   vccl::DirectPeers* dPeers = nullptr;  // device-resident peer table
+  vccl::NetProxy* net = nullptr;  // inter-node ring connections (proxy.cc)
+  int netListenFd = -1;        // proxy listener, open from init until connections are made
   int algoForce = 0;           // NCCL_ALGO/NCCL_PROTO: 0 auto, 1 ring/SIMPLE, 2 tree/LL, 3 direct
   vccl::DevComm* devComm = nullptr;
   vccl::DevChannel* devChannels = nullptr;
@@ -139,4 +150,14 @@ struct ncclComm {
 namespace vccl {
 constexpr uint64_t kCommMagic = 0x76636363'6c6d6933ull;  // "vccclmi3"
 ncclResult_t comm_check(const ncclComm* comm, const char* api);
+
+// Net proxy (proxy.cc).  net_listen opens this rank's listener before the
+// peer exchange (address published in `me`); net_connect builds the
+// connections of every channel whose prev / next is flagged in netPeer,
+// points those channel ends at host-pinned staging memory and starts the
+// proxy threads; net_stop joins them and frees everything (idempotent).
+ncclResult_t net_listen(ncclComm* c, PeerMap* me);
+ncclResult_t net_connect(ncclComm* c, const std::vector<std::vector<int>>& rings,
+                         std::vector<DevChannel>& chans, const std::vector<char>& netPeer);
+void net_stop(ncclComm* c);
 }  // namespace vccl

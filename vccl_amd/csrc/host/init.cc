@@ -68,6 +68,7 @@ static ncclResult_t alloc_uncached(void** p, size_t bytes) {
 }
 
 static void free_resources(ncclComm* c) {
+  net_stop(c);  // first: its threads read the host staging memory and flags
   for (void* p : c->ipcOpened) (void)hipIpcCloseMemHandle(p);
   c->ipcOpened.clear();
   if (c->fifoBuf) (void)hipFree(c->fifoBuf);
@@ -234,15 +235,34 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       c->directMaxBytes = 0;
     }
   }
+  if (n > 1) NCCLCHECK(net_listen(c, &me));
   VINFO("rank %d: exchange peer info", c->rank);
   c->peers.assign(n, PeerMap{});
   c->peers[c->rank] = me;
   NCCLCHECK(bootstrap_allgather(c->bootstrap, c->peers.data(), sizeof(PeerMap)));
+  // Transport per peer (the reference's selectTransport, transport.cc:
+  // 37-68, reduced to two): xGMI peer memory within the node, the net proxy
+  // (proxy.cc) to a peer on another node — or to every peer with
+  // VCCL_NET_FORCE=1, which runs the inter-node path on one node.
+  const bool netForce = param_int("NET_FORCE", 0) != 0;
+  std::vector<char> netPeer(n, 0);
+  bool anyNet = false;
   for (int r = 0; r < n; r++) {
-    if (c->peers[r].hostHash != me.hostHash) {
-      VWARN("rank %d is on another node: inter-node transport is out of scope", r);
-      return ncclInvalidUsage;
-    }
+    if (r == c->rank) continue;
+    netPeer[r] = netForce || c->peers[r].hostHash != me.hostHash;
+    anyNet |= netPeer[r] != 0;
+  }
+  if (anyNet) {
+    // LL and the two-shot direct path need every peer's memory mapped
+    // (full xGMI mesh): all-reduce takes the ring.  Net channels move
+    // through the proxy, a few are enough (NCCL's net defaults use 2-4).
+    c->llMaxBytes = 0;
+    c->directMaxBytes = 0;
+    c->nChannels = std::max(1, std::min(c->nChannels, (int)param_int("NET_NCHANNELS", 4)));
+    VINFO("rank %d: inter-node ring through the net proxy, %d channels", c->rank, c->nChannels);
+  }
+  for (int r = 0; r < n; r++) {
+    if (netPeer[r]) continue;
     // init.cc:732-735: two ranks on one GPU is invalid usage.  The escape
     // hatch exists for protocol tests on a 1-GPU machine only.
     if (r != c->rank && c->peers[r].busId == me.busId && !param_int("ALLOW_SHARED_DEVICE", 0)) {
@@ -264,6 +284,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   // writeback / invalidate is needed per slot; VCCL_FENCES=1 adds the
   // system-scope release/acquire fences back (A/B and safety valve).
   dc.useFences = (int)param_int("FENCES", 0);
+  if (anyNet) dc.useFences = 1;  // slots and flags in host memory: full system-scope fences
   dc.pollMode = (int)param_int("POLL_MODE", 0);
   HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));
@@ -277,10 +298,11 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
         flagOf[r] = c->flagBuf;
         continue;
       }
+      if (netPeer[r]) continue;  // reached through the net proxy
       NCCLCHECK(map_peer(c, me, c->peers[r], kMapFifo, &fifoOf[r]));
       NCCLCHECK(map_peer(c, me, c->peers[r], kMapFlag, &flagOf[r]));
     }
-    if (c->dBuf) {
+    if (c->dBuf && !anyNet) {
       DirectPeers dp{};
       for (int r = 0; r < n; r++) {
         if (r == c->rank) {
@@ -295,7 +317,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       HIPCHECK(hipMemcpy(c->dPeers, &dp, sizeof(dp), hipMemcpyHostToDevice));
     }
     c->llPeer.assign(n, nullptr);
-    if (c->llBuf) {
+    if (c->llBuf && !anyNet) {
       for (int r = 0; r < n; r++) {
         if (r == c->rank) c->llPeer[r] = c->llBuf;
         else NCCLCHECK(map_peer(c, me, c->peers[r], kMapLL, &c->llPeer[r]));
@@ -321,7 +343,19 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       d.nextRecvTail = flag(next, 0);
       d.sendHead = flag(c->rank, 1);
       d.recvStep = d.sendStep = 0;
+      d.sendSizes = nullptr;
+      // a net end's pointers are set by net_connect below
+      if (netPeer[prev]) {
+        d.recvFifo = nullptr;
+        d.recvTail = d.prevSendHead = nullptr;
+      }
+      if (netPeer[next]) {
+        d.sendFifo = nullptr;
+        d.nextRecvTail = d.sendHead = nullptr;
+      }
     }
+    if (anyNet) NCCLCHECK(net_connect(c, rings, chans, netPeer));
+    else net_stop(c);  // close the unused listener
     HIPCHECK(hipMalloc((void**)&c->devChannels, sizeof(DevChannel) * c->nChannels));
     HIPCHECK(hipMemcpy(c->devChannels, chans.data(), sizeof(DevChannel) * c->nChannels,
                        hipMemcpyHostToDevice));

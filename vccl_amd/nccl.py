@@ -39,7 +39,7 @@ EXPORTED = [
     "ncclAllReduce", "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
-    "vcclCommLaunchStats",
+    "vcclCommLaunchStats", "vcclCommNetStats",
 ]
 ALGO_NAMES = {0: "ring", 1: "ll", 2: "direct", 3: "one_rank"}
 
@@ -246,6 +246,13 @@ class Comm:
         check(lib().vcclCommLaunchStats(self.handle, ctypes.byref(a), ctypes.byref(b)),
               "vcclCommLaunchStats")
         return a.value, b.value
+
+    def net_stats(self) -> tuple[int, int, int]:
+        """vcclCommNetStats: (bytes sent, bytes received, connections) of the net proxy."""
+        a, b, n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        check(lib().vcclCommNetStats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)),
+              "vcclCommNetStats")
+        return a.value, b.value, n.value
 
     def create_premulsum(self, scalar_ptr: int, dtype: int, residence: int) -> int:
         op = ctypes.c_int()
