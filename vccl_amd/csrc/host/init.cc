@@ -258,7 +258,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // through the proxy, a few are enough (NCCL's net defaults use 2-4).
     c->llMaxBytes = 0;
     c->directMaxBytes = 0;
-    c->nChannels = std::max(1, std::min(c->nChannels, (int)param_int("NET_NCHANNELS", 4)));
+    c->nChannels = std::max(1, std::min(c->nChannels, (int)param_int("NET_NCHANNELS", 8)));
     VINFO("rank %d: inter-node ring through the net proxy, %d channels", c->rank, c->nChannels);
   }
   for (int r = 0; r < n; r++) {

@@ -23,10 +23,11 @@
 // channel and direction): data {uint64 bytes, bytes of slot payload} in step
 // order one way, credits {uint64 head} the other way.
 //
-// Threads: a sender (ships posted slots, blocking sends) and a receiver
-// (poll()s every socket: lands data, applies credits, forwards the GPU's
-// consumed counts).  Splitting them keeps a full socket in one direction from
-// ever stopping the other, so the ring of proxies cannot deadlock.  Socket
+// Threads: one per connection end.  A send end ships posted slots (blocking
+// sends) and applies credits read without blocking; a receive end lands
+// slots and forwards the GPU's consumed counts as 8-byte credits.  A blocked
+// data send never stops a receive end, and credits are tiny (a 4 MiB socket
+// buffer holds half a million), so the ring of proxies cannot deadlock.  Socket
 // failures raise the comm's error flag: the GPU's bounded spins end and
 // ncclCommGetAsyncError reports ncclRemoteError.
 #include <arpa/inet.h>
@@ -88,7 +89,7 @@ struct NetProxy {
   int64_t stride = 0;        // slot stride in bytes
   char* host = nullptr;      // one hipHostMalloc block: flags, then slots
   std::atomic<bool> stop{false};
-  std::thread tSend, tRecv;
+  std::vector<std::thread> threads;  // one per connection end
   volatile int* errorFlag = nullptr;  // the comm's host-mapped error word
   std::atomic<uint64_t> bytesSent{0}, bytesRecv{0};
 };
@@ -119,83 +120,88 @@ bool io_all(NetProxy* P, int fd, void* p, size_t n, bool out) {
   return true;
 }
 
-void send_loop(NetProxy* P) {
+// One thread per connection end, so the staged rate scales with channels
+// (one sending thread's socket copy tops out near 10 GB/s).
+void idle_wait(bool busy, int* idle) {
+  if (busy) *idle = 0;
+  else if (++*idle > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+}
+
+// Send end: ship every posted slot {bytes, payload} in step order; apply the
+// receiver's credits (8-byte head values, read without blocking).
+void send_loop(NetProxy* P, Conn* c) {
   int idle = 0;
+  uint64_t credit = 0;
+  size_t have = 0;  // bytes of `credit` received so far
   while (!P->stop.load(std::memory_order_relaxed)) {
     bool busy = false;
-    for (Conn& c : P->send) {
-      const uint64_t posted = ld_acq(&c.flags->sendTail.v);
-      while (c.done < posted && !P->stop.load(std::memory_order_relaxed)) {
-        const int slot = (int)(c.done % kSteps);
-        uint64_t bytes = __atomic_load_n(&c.flags->sendSizes[slot], __ATOMIC_ACQUIRE);
-        bytes = std::min<uint64_t>(bytes, (uint64_t)P->stride);
-        if (!io_all(P, c.fd, &bytes, sizeof(bytes), true) ||
-            (bytes && !io_all(P, c.fd, c.buf + slot * P->stride, bytes, true))) {
-          fail(P, "send", c.ch);
-          return;
-        }
-        P->bytesSent += bytes;
-        c.done++;
-        busy = true;
+    const uint64_t posted = ld_acq(&c->flags->sendTail.v);
+    while (c->done < posted && !P->stop.load(std::memory_order_relaxed)) {
+      const int slot = (int)(c->done % kSteps);
+      uint64_t bytes = __atomic_load_n(&c->flags->sendSizes[slot], __ATOMIC_ACQUIRE);
+      bytes = std::min<uint64_t>(bytes, (uint64_t)P->stride);
+      if (!io_all(P, c->fd, &bytes, sizeof(bytes), true) ||
+          (bytes && !io_all(P, c->fd, c->buf + slot * P->stride, bytes, true))) {
+        fail(P, "send", c->ch);
+        return;
       }
+      P->bytesSent += bytes;
+      c->done++;
+      busy = true;
     }
-    if (busy) idle = 0;
-    else if (++idle > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    for (;;) {
+      const ssize_t k = ::recv(c->fd, (char*)&credit + have, sizeof(credit) - have, MSG_DONTWAIT);
+      if (k > 0) {
+        have += (size_t)k;
+        if (have == sizeof(credit)) {
+          st_rel(&c->flags->sendHead.v, credit);
+          have = 0;
+        }
+        busy = true;
+        continue;
+      }
+      if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) break;
+      fail(P, "credit recv", c->ch);
+      return;
+    }
+    idle_wait(busy, &idle);
   }
 }
 
-void recv_loop(NetProxy* P) {
-  // pollfds: [recv conns (data in)] ++ [send conns (credits in)]
-  std::vector<pollfd> pfd;
-  for (Conn& c : P->recv) pfd.push_back({c.fd, POLLIN, 0});
-  for (Conn& c : P->send) pfd.push_back({c.fd, POLLIN, 0});
-  const size_t nr = P->recv.size();
+// Receive end: forward the GPU's consumed count as a credit; land each
+// arriving slot whole, then raise the tail the GPU waits on.
+void recv_loop(NetProxy* P, Conn* c) {
   int idle = 0;
   while (!P->stop.load(std::memory_order_relaxed)) {
     bool busy = false;
-    // Forward the GPU's consumed counts to the senders (8-byte credits).
-    for (Conn& c : P->recv) {
-      const uint64_t head = ld_acq(&c.flags->recvHead.v);
-      if (head > c.credited) {
-        if (!io_all(P, c.fd, (void*)&head, sizeof(head), true)) {
-          fail(P, "credit send", c.ch);
-          return;
-        }
-        c.credited = head;
-        busy = true;
+    const uint64_t head = ld_acq(&c->flags->recvHead.v);
+    if (head > c->credited) {
+      if (!io_all(P, c->fd, (void*)&head, sizeof(head), true)) {
+        fail(P, "credit send", c->ch);
+        return;
       }
+      c->credited = head;
+      busy = true;
     }
-    const int ready = poll(pfd.data(), (nfds_t)pfd.size(), idle > 256 ? 1 : 0);
+    pollfd pf{c->fd, POLLIN, 0};
+    const int ready = poll(&pf, 1, 0);
     if (ready < 0 && errno != EINTR) {
-      fail(P, "poll", -1);
+      fail(P, "poll", c->ch);
       return;
     }
-    for (size_t i = 0; ready > 0 && i < pfd.size(); i++) {
-      if (!(pfd[i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
-      busy = true;
-      if (i < nr) {  // one whole slot lands, then the GPU may read it
-        Conn& c = P->recv[i];
-        uint64_t bytes = 0;
-        if (!io_all(P, c.fd, &bytes, sizeof(bytes), false) || bytes > (uint64_t)P->stride ||
-            (bytes && !io_all(P, c.fd, c.buf + (c.done % kSteps) * P->stride, bytes, false))) {
-          fail(P, "recv", c.ch);
-          return;
-        }
-        P->bytesRecv += bytes;
-        c.done++;
-        st_rel(&c.flags->recvTail.v, c.done);
-      } else {  // a credit for one of my send ends
-        Conn& c = P->send[i - nr];
-        uint64_t head = 0;
-        if (!io_all(P, c.fd, &head, sizeof(head), false)) {
-          fail(P, "credit recv", c.ch);
-          return;
-        }
-        st_rel(&c.flags->sendHead.v, head);
+    if (ready > 0 && (pf.revents & (POLLIN | POLLHUP | POLLERR))) {
+      uint64_t bytes = 0;
+      if (!io_all(P, c->fd, &bytes, sizeof(bytes), false) || bytes > (uint64_t)P->stride ||
+          (bytes && !io_all(P, c->fd, c->buf + (c->done % kSteps) * P->stride, bytes, false))) {
+        fail(P, "recv", c->ch);
+        return;
       }
+      P->bytesRecv += bytes;
+      c->done++;
+      st_rel(&c->flags->recvTail.v, c->done);
+      busy = true;
     }
-    if (busy) idle = 0;
-    else idle++;
+    idle_wait(busy, &idle);
   }
 }
 
@@ -327,8 +333,8 @@ ncclResult_t net_connect(ncclComm* c, const std::vector<std::vector<int>>& rings
     d.recvTail = (uint64_t*)devp(&k.flags->recvTail.v);
     d.prevSendHead = (uint64_t*)devp(&k.flags->recvHead.v);
   }
-  P->tSend = std::thread(send_loop, P);
-  P->tRecv = std::thread(recv_loop, P);
+  for (Conn& k : P->send) P->threads.emplace_back(send_loop, P, &k);
+  for (Conn& k : P->recv) P->threads.emplace_back(recv_loop, P, &k);
   VINFO("rank %d: net proxy up, %zu send / %zu recv connections", c->rank, P->send.size(),
         P->recv.size());
   return ncclSuccess;
@@ -342,8 +348,7 @@ void net_stop(ncclComm* c) {
   P->stop.store(true);
   for (Conn& k : P->send) shutdown(k.fd, SHUT_RDWR);
   for (Conn& k : P->recv) shutdown(k.fd, SHUT_RDWR);
-  if (P->tSend.joinable()) P->tSend.join();
-  if (P->tRecv.joinable()) P->tRecv.join();
+  for (std::thread& t : P->threads) t.join();
   for (Conn& k : P->send) close(k.fd);
   for (Conn& k : P->recv) close(k.fd);
   if (P->host) (void)hipHostFree(P->host);
