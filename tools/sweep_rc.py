@@ -39,6 +39,11 @@ def main():
             grid = (n * 4 + hunk - 1) // hunk
             variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
                              "ntLoads": ld, "ntStores": st, "order": order})
+    elif mode == "lds":  # LDS-DMA double-buffered staging (order 2) vs the register path
+        tiles = n * 4 // (256 * 2 * 16)
+        for grid, st in itertools.product((256, 512, 1024, 1280, 2048, tiles), (1, 2)):
+            variants.append({"blockSize": 256, "unroll": 2, "gridBlocks": grid,
+                             "ntLoads": 1, "ntStores": st, "order": 2})
     elif mode == "fine":  # small hunks, one per workgroup (nt loads, sc0 sc1 stores)
         for block, unroll in itertools.product((64, 128, 256, 512), (1, 2, 4)):
             hunk = block * unroll * 16

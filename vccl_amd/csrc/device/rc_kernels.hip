@@ -20,6 +20,66 @@ __global__ __launch_bounds__(1024) void k_reduce_copy(RCArgs a, int64_t nElts, u
                                                            threadIdx.x, blockDim.x);
 }
 
+// LDS-staged variant (benchmark sweep only, `order` 2): the north-star's
+// "LDS double-buffered staging" measured against the register path.  Each
+// wave moves its sources HBM -> LDS with global_load_lds_dwordx4 (LDS-DMA,
+// no VGPR destination) two tiles deep: while tile t+1's DMA is in flight the
+// wave reads tile t back (ds_read_b128, each lane its own 16 bytes, so no
+// workgroup barrier is needed), reduces and stores.  A lane's LDS slot is
+// wave base + lane x 16 (the DMA's fixed destination pattern).  Full tiles
+// only (the launcher falls back to the register path otherwise).
+constexpr int kLdsU = 2;  // packs per lane per source per tile
+template <class Fn, int NS, int ST>
+__global__ __launch_bounds__(256) void k_reduce_copy_lds(RCArgs a, int64_t nTiles, uint64_t redArg) {
+  using T = typename Fn::EltType;
+  (void)sizeof(T);
+  __shared__ __attribute__((aligned(16))) char lds[2][NS][kLdsU][256 * 16];
+  Fn fn(load_op_arg(a.argPtr, a.argBytes, redArg));
+  const int tid = threadIdx.x, wbase = (tid >> 6) * 64 * 16;
+  constexpr int64_t kTilePacks = 256 * kLdsU;
+  auto issue = [&](int64_t tile, int buf) {
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+#pragma unroll
+      for (int u = 0; u < kLdsU; u++) {
+        const int64_t pack = tile * kTilePacks + u * 256 + tid;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(a.srcs[s] + pack * 16),
+            (__attribute__((address_space(3))) void*)(&lds[buf][s][u][wbase]), 16, 0, 2 /*nt*/);
+      }
+  };
+  int64_t t = blockIdx.x;
+  if (t >= nTiles) return;
+  issue(t, 0);
+  for (int buf = 0; t < nTiles; t += gridDim.x, buf ^= 1) {
+    const bool more = t + gridDim.x < nTiles;
+    if (more) issue(t + gridDim.x, buf ^ 1);
+    // tile t's DMA (and everything issued before it) complete; the next
+    // tile's NS x kLdsU DMAs stay in flight
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS * kLdsU) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < kLdsU; u++) {
+      u32x4 acc = *(const u32x4*)(&lds[buf][0][u][wbase + (tid & 63) * 16]);
+      if constexpr (Fn::kPreOp) {
+        if (a.preOpSrcs > 0) acc = pack_preop(fn, acc);
+      }
+#pragma unroll
+      for (int s = 1; s < NS; s++) {
+        u32x4 v = *(const u32x4*)(&lds[buf][s][u][wbase + (tid & 63) * 16]);
+        acc = pack_reduce(fn, acc, v);
+      }
+      if constexpr (Fn::kPostOp) {
+        if (a.postOp) acc = pack_postop(fn, acc);
+      }
+      const int64_t pack = t * kTilePacks + u * 256 + tid;
+      st16<ST>(a.dsts[0], pack * 16, acc);
+    }
+    // this wave's ds_reads of `buf` must finish before its DMA refills it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 // Launch one instantiation.
 template <class Fn, int NS, int ND, int U, int L, int S, int O>
 static hipError_t launch_one(const RCArgs& a, int64_t nElts, uint64_t redArg, const LaunchGeom& lg,
@@ -34,6 +94,23 @@ static hipError_t launch_one(const RCArgs& a, int64_t nElts, uint64_t redArg, co
 template <class Fn, int NS, int ND, int U>
 static hipError_t sweep_ls(const RCArgs& a, int64_t n, uint64_t r, const LaunchGeom& lg,
                            hipStream_t s) {
+  if constexpr (NS >= 1 && ND == 1) {
+    using T = typename Fn::EltType;
+    const int64_t bytes = n * (int64_t)sizeof(T);
+    const int64_t tileBytes = 256 * kLdsU * 16;
+    bool aligned = true;
+    for (int i = 0; i < NS; i++) aligned &= ((uintptr_t)a.srcs[i] & 15) == 0;
+    aligned &= ((uintptr_t)a.dsts[0] & 15) == 0;
+    if (lg.order == 2 && aligned && bytes % tileBytes == 0) {
+      const int64_t nTiles = bytes / tileBytes;
+      const int grid = (int)std::min<int64_t>(nTiles, lg.grid);  // persistent: pass gridBlocks
+      if (lg.ntStores == 2)
+        hipLaunchKernelGGL((k_reduce_copy_lds<Fn, NS, kSys>), dim3(grid), dim3(256), 0, s, a, nTiles, r);
+      else
+        hipLaunchKernelGGL((k_reduce_copy_lds<Fn, NS, kNT>), dim3(grid), dim3(256), 0, s, a, nTiles, r);
+      return hipGetLastError();
+    }
+  }
   auto by_order = [&]<int L, int S>() -> hipError_t {
     if (lg.order == 1) return launch_one<Fn, NS, ND, U, L, S, 1>(a, n, r, lg, s);
     return launch_one<Fn, NS, ND, U, L, S, 0>(a, n, r, lg, s);
