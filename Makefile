@@ -19,7 +19,14 @@ RING_OBJS := $(foreach k,$(KTS),$(OBJ)/ring_kernels_$(k).o)
 API_OBJS := $(OBJ)/rc_api.o
 HOST_OBJS := $(patsubst $(HOST)/%.cc,$(OBJ)/host_%.o,$(wildcard $(HOST)/*.cc))
 
-all: $(LIB) oracle
+PERF := vccl_amd/lib/coll_perf
+
+all: $(LIB) $(PERF) oracle
+
+# nccl-tests-style driver linked against the C API only (tools/coll_perf.hip)
+$(PERF): tools/coll_perf.hip include/nccl.h $(LIB)
+	$(HIPCC) -std=c++20 -O2 --offload-arch=$(ARCH) -I include $< -o $@ -L vccl_amd/lib -lvccl \
+	  -Wl,-rpath,'$$ORIGIN'
 
 $(LIB): $(RC_OBJS) $(RING_OBJS) $(API_OBJS) $(HOST_OBJS)
 	@mkdir -p $(dir $@)
@@ -45,7 +52,7 @@ oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(PERF)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean
