@@ -11,7 +11,7 @@ OBJ := build/obj$(VARIANT)
 LIB := vccl_amd/lib/libvccl$(VARIANT).so
 DEV := vccl_amd/csrc/device
 HOST := vccl_amd/csrc/host
-KTS := 0 1 2 3 4 5 6
+KTS := 0 1 2 3 4 5 6 7 8
 HDRS := $(wildcard $(DEV)/*.hpp) $(wildcard $(HOST)/*.h) $(wildcard include/*.h)
 
 RC_OBJS := $(foreach k,$(KTS),$(OBJ)/rc_kernels_$(k).o)

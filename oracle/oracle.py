@@ -24,9 +24,11 @@ _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
 NP_DTYPE = {
     0: np.int8, 1: np.uint8, 2: np.int32, 3: np.uint32, 4: np.int64, 5: np.uint64,
     6: np.float16, 7: np.float32, 8: np.float64, 9: np.uint16,  # bf16 stored as raw bits
+    10: np.uint8, 11: np.uint8,  # fp8 e4m3 / e5m2 stored as raw bits
 }
 TYPE_NAMES = {0: "i8", 1: "u8", 2: "i32", 3: "u32", 4: "i64", 5: "u64",
-              6: "f16", 7: "f32", 8: "f64", 9: "bf16"}
+              6: "f16", 7: "f32", 8: "f64", 9: "bf16",
+              10: "f8e4m3", 11: "f8e5m2"}
 OP_NAMES = {0: "sum", 1: "prod", 2: "max", 3: "min", 4: "avg"}
 DEV_SUM, DEV_PROD, DEV_MINMAX, DEV_PREMULSUM, DEV_SUMPOSTDIV = range(5)
 
@@ -54,6 +56,10 @@ def lib() -> ctypes.CDLL:
         L.ref_f32_to_f16.argtypes = [ctypes.c_float]
         L.ref_f32_to_bf16.restype = ctypes.c_uint16
         L.ref_f32_to_bf16.argtypes = [ctypes.c_float]
+        L.ref_fp8_to_f32.restype = ctypes.c_float
+        L.ref_fp8_to_f32.argtypes = [i32, ctypes.c_uint8]
+        L.ref_f32_to_fp8.restype = ctypes.c_uint8
+        L.ref_f32_to_fp8.argtypes = [i32, ctypes.c_float]
         _lib = L
     return _lib
 
@@ -128,3 +134,20 @@ def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
 
 def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
     return (np.ascontiguousarray(b, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+_FP8_TABLES = {}
+
+
+def fp8_bits_to_f32(t: int, b: np.ndarray) -> np.ndarray:
+    """Exact fp8 (type 10 e4m3 / 11 e5m2) -> f32 through ref_fp8_to_f32."""
+    if t not in _FP8_TABLES:
+        _FP8_TABLES[t] = np.array([lib().ref_fp8_to_f32(t, i) for i in range(256)], np.float32)
+    return _FP8_TABLES[t][np.asarray(b, dtype=np.uint8)]
+
+
+def f32_to_fp8_bits(t: int, x: np.ndarray) -> np.ndarray:
+    """RN-even satfinite f32 -> fp8 bits (ref_f32_to_fp8), element by element."""
+    L = lib()
+    x = np.asarray(x, dtype=np.float32).ravel()
+    return np.array([L.ref_f32_to_fp8(t, float(v)) for v in x], dtype=np.uint8)

@@ -12,7 +12,7 @@
 
 int ref_type_size(int type) {
   switch (type) {
-    case R_I8: case R_U8: return 1;
+    case R_I8: case R_U8: case R_F8E4M3: case R_F8E5M2: return 1;
     case R_F16: case R_BF16: return 2;
     case R_I32: case R_U32: case R_F32: return 4;
     case R_I64: case R_U64: case R_F64: return 8;
@@ -78,6 +78,43 @@ uint16_t ref_f32_to_bf16(float f) {
   return (uint16_t)((u + 0x7fffu + lsb) >> 16);
 }
 
+/* fp8: E5M2 is binary16 truncated to 8 bits; E4M3 is decoded field by field. */
+float ref_fp8_to_f32(int type, uint8_t b) {
+  if (type == R_F8E5M2) return ref_f16_to_f32((uint16_t)(b << 8));
+  uint32_t e = (b >> 3) & 15u, m = b & 7u;
+  float v;
+  if (e == 15 && m == 7) return u2f(0x7fc00000u);
+  if (e == 0) v = ldexpf((float)m, -9);
+  else v = ldexpf((float)(8 + m), (int)e - 10);
+  return (b & 0x80u) ? -v : v;
+}
+
+/* RN-even of a finite f32 to `mbits` mantissa bits, exponent bias `bias`,
+ * computed on the 24-bit integer significand. */
+uint8_t ref_f32_to_fp8(int type, float f) {
+  const int mbits = type == R_F8E4M3 ? 3 : 2, bias = type == R_F8E4M3 ? 7 : 15;
+  const uint32_t maxCode = type == R_F8E4M3 ? 0x7eu : 0x7bu;
+  uint32_t u = f2u(f), sign = (u >> 24) & 0x80u, a = u & 0x7fffffffu;
+  if (a > 0x7f800000u) return 0x7fu;
+  if (a == 0) return (uint8_t)sign;
+  int e = (int)(a >> 23) - 127, emin = 1 - bias;
+  uint64_t m = (a & 0x7fffffu) | 0x800000u;
+  if ((a >> 23) == 0) { m = a & 0x7fffffu; e = -126; }  /* f32 subnormal */
+  int ue = (e > emin ? e : emin) - mbits;                 /* result unit 2^ue */
+  int shift = ue - (e - 23);
+  uint64_t q = 0;
+  if (shift < 60) {
+    uint64_t rem = m & ((1ull << shift) - 1), half = 1ull << (shift - 1);
+    q = m >> shift;
+    if (rem > half || (rem == half && (q & 1))) q++;
+  }
+  uint64_t code;
+  if (e >= emin) code = ((uint64_t)(e + bias) << mbits) + q - (1ull << mbits);
+  else code = q;                                        /* subnormal; may reach min normal */
+  if (e > 30 || code > maxCode) code = maxCode;
+  return (uint8_t)(sign | code);
+}
+
 /* IEEE minNum / maxNum (fminf/fmaxf, __hmin/__hmax: NaN-avoiding). */
 static double minnum(double x, double y, int isMin) {
   if (isnan(x)) return y;
@@ -110,6 +147,7 @@ int ref_host_to_dev_redop(int op, int type, int nranks, int* devOp, uint64_t* op
         double inv = 1.0 / nranks;
         if (type == R_F16) *opArg = ref_f32_to_f16((float)inv);
         else if (type == R_BF16) *opArg = ref_f32_to_bf16((float)inv);
+        else if (type == R_F8E4M3 || type == R_F8E5M2) *opArg = ref_f32_to_fp8(type, (float)inv);
         else if (type == R_F32) *opArg = f2u((float)inv);
         else *opArg = d2u(inv);
       }
@@ -153,6 +191,18 @@ uint64_t ref_reduce1(int devOp, int type, uint64_t opArg, uint64_t a, uint64_t b
     }
   }
   if (type == R_F16 || type == R_BF16) return narrow_op(devOp, type, opArg, a, b);
+  if (type == R_F8E4M3 || type == R_F8E5M2) {
+    /* reduce_kernel.h:309-321: fp8(__hop(half(a), half(b))) — the op in f32
+     * is exact for fp8 operands, then RN to binary16, then RN-satfinite to
+     * fp8 (two roundings, as the reference). */
+    float x = ref_fp8_to_f32(type, (uint8_t)a), y = ref_fp8_to_f32(type, (uint8_t)b), r;
+    switch (devOp) {
+      case R_PROD: r = x * y; break;
+      case R_MINMAX: r = (float)minnum(x, y, (opArg & 1) == 0); break;
+      default: r = x + y; break;
+    }
+    return ref_f32_to_fp8(type, ref_f16_to_f32(ref_f32_to_f16(r)));
+  }
   if (type == R_F32) {
     float x = u2f((uint32_t)a), y = u2f((uint32_t)b), r;
     switch (devOp) {

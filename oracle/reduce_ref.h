@@ -28,7 +28,7 @@ extern "C" {
 #endif
 
 /* ncclDataType_t values (nccl.h.in:239-252) */
-enum { R_I8 = 0, R_U8, R_I32, R_U32, R_I64, R_U64, R_F16, R_F32, R_F64, R_BF16 };
+enum { R_I8 = 0, R_U8, R_I32, R_U32, R_I64, R_U64, R_F16, R_F32, R_F64, R_BF16, R_F8E4M3, R_F8E5M2 };
 /* ncclDevRedOp_t values (src/include/device.h:34-38) */
 enum { R_SUM = 0, R_PROD, R_MINMAX, R_PREMULSUM, R_SUMPOSTDIV };
 /* ncclRedOp_t values (nccl.h.in:221-236) */
@@ -44,6 +44,12 @@ float ref_f16_to_f32(uint16_t h);
 uint16_t ref_f32_to_f16(float f);
 float ref_bf16_to_f32(uint16_t h);
 uint16_t ref_f32_to_bf16(float f);
+/* OCP FP8 E4M3 ("fn", bias 7, max 448, NaN S.1111.111) and E5M2 (bias 15,
+ * max 57344).  Widening is exact; narrowing is __nv_cvt_float_to_fp8(x,
+ * __NV_SATFINITE, fmt): RN-even, |x| past max finite (infinity included) ->
+ * max finite, NaN -> 0x7f. */
+float ref_fp8_to_f32(int type, uint8_t b);
+uint8_t ref_f32_to_fp8(int type, float f);
 
 /* Element primitives on raw bits (value in the low sizeof(T) bytes). */
 uint64_t ref_reduce1(int devOp, int type, uint64_t opArg, uint64_t a, uint64_t b);

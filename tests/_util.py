@@ -10,16 +10,20 @@
 import numpy as np
 
 TYPE_IDS = {"i8": 0, "u8": 1, "i32": 2, "u32": 3, "i64": 4, "u64": 5,
-            "f16": 6, "f32": 7, "f64": 8, "bf16": 9}
+            "f16": 6, "f32": 7, "f64": 8, "bf16": 9,
+            "f8e4m3": 10, "f8e5m2": 11}
 OP_IDS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
-FLOAT_TYPES = (6, 7, 8, 9)
-UNIT_ROUNDOFF = {6: 2.0**-11, 7: 2.0**-24, 8: 2.0**-53, 9: 2.0**-8}
+FLOAT_TYPES = (6, 7, 8, 9, 10, 11)
+UNIT_ROUNDOFF = {6: 2.0**-11, 7: 2.0**-24, 8: 2.0**-53, 9: 2.0**-8, 10: 2.0**-4, 11: 2.0**-3}
 
 
 def to_f64(t, a):
     a = np.asarray(a)
     if t == 9:
         return (a.astype(np.uint16).astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    if t in (10, 11):
+        from oracle import oracle as O
+        return O.fp8_bits_to_f32(t, a).astype(np.float64)
     return a.astype(np.float64)
 
 

@@ -35,7 +35,27 @@ CASES = [
     ("ag_f16_odd", "ag", 0, 6, 3_001),
     ("ag_f32", "ag", 0, 7, 4_099),
     ("ag_u8_odd", "ag", 0, 1, 1_001),
+    # fp8 (OCP e4m3 / e5m2 through half, reduce_kernel.h:309-321): LL, direct, ring
+    ("ar_f8e4m3_sum", "ar", 0, 10, 100_003),
+    ("ar_f8e5m2_avg_direct", "ar", 4, 11, 2_000_001),
+    ("ar_f8e4m3_max_direct", "ar", 2, 10, 1_500_007),
+    ("rs_f8e4m3_sum_odd", "rs", 0, 10, 20_001),
+    ("rs_f8e5m2_prod", "rs", 1, 11, 9_999),
 ]
+
+
+def _fp8_codes(dt, x):
+    """Vectorised RN-even f32 -> fp8 for |x| < 2 (no saturation or NaN in
+    range): the code whose value is nearest, ties to the even code."""
+    vals = O.fp8_bits_to_f32(dt, np.arange(128, dtype=np.uint8))
+    vals = np.where(np.isnan(vals), np.inf, vals)
+    a = np.abs(x)
+    hi = np.searchsorted(vals, a)  # vals[hi-1] < a <= vals[hi]
+    hi = np.clip(hi, 1, 127)
+    lo = hi - 1
+    dlo, dhi = a - vals[lo], vals[hi] - a
+    pick = np.where((dhi < dlo) | ((dhi == dlo) & (hi % 2 == 0)), hi, lo)
+    return (pick | np.where(np.signbit(x), 0x80, 0)).astype(np.uint8)
 
 
 def gen_input(case_idx, rank, n_ranks):
@@ -49,6 +69,8 @@ def gen_input(case_idx, rank, n_ranks):
         return rng.integers(0, 2**62, total, dtype=np.int64).astype(np.uint64).view(np.int64).astype(npdt)
     if dt == 9:
         return O.f32_to_bf16_bits(rng.uniform(-1, 1, total).astype(np.float32))
+    if dt in (10, 11):  # fp8 codes of uniform values (every code of the range)
+        return _fp8_codes(dt, rng.uniform(-2, 2, total).astype(np.float32))
     return rng.uniform(-1, 1, total).astype(O.NP_DTYPE[dt])
 
 

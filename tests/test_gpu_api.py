@@ -50,11 +50,15 @@ def test_config1_allreduce_1kib_identity(comm1):
 
 @pytest.mark.parametrize("dt,tdt", [(nccl.ncclFloat32, torch.float32), (nccl.ncclFloat16, torch.float16),
                                     (nccl.ncclBfloat16, torch.bfloat16), (nccl.ncclFloat64, torch.float64),
-                                    (nccl.ncclInt32, torch.int32), (nccl.ncclUint8, torch.uint8)])
+                                    (nccl.ncclInt32, torch.int32), (nccl.ncclUint8, torch.uint8),
+                                    (nccl.ncclFloat8e4m3, torch.float8_e4m3fn),
+                                    (nccl.ncclFloat8e5m2, torch.float8_e5m2)])
 @pytest.mark.parametrize("op", [0, 1, 2, 3, 4])
 def test_one_rank_all_ops(comm1, dt, tdt, op):
     n = 4099
-    if tdt.is_floating_point:
+    if tdt in (torch.float8_e4m3fn, torch.float8_e5m2):  # finite codes only (avg: x * 1.0)
+        x = torch.randn(n).to(tdt).cuda()
+    elif tdt.is_floating_point:
         x = torch.randn(n, device="cuda").to(tdt)
     else:
         x = torch.randint(0, 100, (n,), device="cuda").to(tdt)
@@ -118,6 +122,25 @@ def test_user_premulsum(comm1):
         comm1.destroy_op(op)
 
 
+def test_user_premulsum_fp8(comm1):
+    """ncclRedOpCreatePreMulSum on fp8 (scalar = 1 fp8 byte; preOp =
+    fp8(half(x) * half(scalar)), reduce_kernel.h:586-624) vs the oracle."""
+    codes = torch.arange(256, dtype=torch.uint8)
+    for dt in (nccl.ncclFloat8e4m3, nccl.ncclFloat8e5m2):
+        x = codes.cuda()
+        y = torch.empty_like(x)
+        scalar = ctypes.c_uint8(0x2B if dt == nccl.ncclFloat8e4m3 else 0x35)  # ~1/3
+        op = comm1.create_premulsum(ctypes.addressof(scalar), dt, nccl.ncclScalarHostImmediate)
+        comm1.all_reduce(x.data_ptr(), y.data_ptr(), 256, dt, op, stream_ptr())
+        torch.cuda.synchronize()
+        exp = O.reduce_copy(3, dt, scalar.value, [codes.numpy()], pre_op_args=[scalar.value])[0]
+        got = y.cpu().numpy()
+        nan = O.fp8_bits_to_f32(dt, exp) != O.fp8_bits_to_f32(dt, exp)
+        assert np.array_equal(got[~nan], exp[~nan])
+        assert np.all(np.isnan(O.fp8_bits_to_f32(dt, got[nan])))
+        comm1.destroy_op(op)
+
+
 def test_arg_errors(comm1):
     L = nccl.lib()
     x = torch.zeros(16, device="cuda")
@@ -126,7 +149,8 @@ def test_arg_errors(comm1):
     assert L.ncclAllReduce(p, p, 16, 7, 17, comm1.handle, None) == nccl.ncclInvalidArgument  # unknown op
     assert L.ncclAllReduce(p, p, 16, 7, -1, comm1.handle, None) == nccl.ncclInvalidArgument
     assert L.ncclAllReduce(p, p, 16, 7, 0, None, None) == nccl.ncclInvalidArgument  # NULL comm
-    assert L.ncclAllReduce(p, p, 16, nccl.ncclFloat8e4m3, 0, comm1.handle, None) == nccl.ncclInvalidArgument
+    # fp8 is native on gfx950 (the reference rejects it below sm90, enqueue.cc:2379-2384)
+    assert L.ncclAllReduce(p, p, 16, nccl.ncclFloat8e4m3, 0, comm1.handle, None) == nccl.ncclSuccess
     assert L.ncclAllReduce(p, p, 0, 7, 0, comm1.handle, None) == nccl.ncclSuccess  # empty: no-op
     assert L.ncclGroupEnd() == nccl.ncclInvalidUsage  # not in a group
     assert nccl.lib().ncclGetErrorString(4) == b"invalid argument (run with NCCL_DEBUG=WARN for details)"

@@ -66,10 +66,12 @@ def _rand(rng, t, n):
         return rng.integers(0, 2**63, size=n, dtype=np.int64).astype(np.uint64).view(np.int64).astype(dt)
     if t == 9:
         return O.f32_to_bf16_bits(rng.uniform(-2, 2, n).astype(np.float32))
+    if t in (10, 11):  # every fp8 code: NaN, saturating magnitudes, subnormals
+        return rng.integers(0, 256, n).astype(np.uint8)
     return rng.uniform(-2, 2, n).astype(O.NP_DTYPE[t])
 
 
-@pytest.mark.parametrize("t", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("t", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("op", [0, 1, 2, 3, 4])
 def test_ragged_sizes_vs_oracle(t, op):
     rng = np.random.default_rng(100 * t + op)
@@ -82,7 +84,7 @@ def test_ragged_sizes_vs_oracle(t, op):
         assert_bitexact(t, got, exp, minmax=op in (2, 3), what=f"t{t} op{op} n{n}")
 
 
-@pytest.mark.parametrize("t", [1, 6, 7, 8, 9])
+@pytest.mark.parametrize("t", [1, 6, 7, 8, 9, 10])
 def test_misaligned_and_multi_dst(t):
     rng = np.random.default_rng(7 + t)
     n = 100_003
@@ -104,7 +106,7 @@ SHIFT_OFFSETS = {1: ([1, 7, 15], [3, 3]), 2: ([2, 6, 14], [10, 10]),
                  4: ([0, 4, 12], [8, 8]), 8: ([8, 0, 8], [8, 8])}
 
 
-@pytest.mark.parametrize("t", [0, 1, 2, 4, 6, 7, 8, 9])
+@pytest.mark.parametrize("t", [0, 1, 2, 4, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("op", [0, 1, 2, 4])
 def test_shifted_sources(t, op):
     rng = np.random.default_rng(900 + 10 * t + op)
@@ -211,3 +213,16 @@ def test_abi_errors():
     assert L.vcclReduceCopy(0, 12, 0, 0, 0, 1, s, 1, d, 16, None) == nccl.ncclInvalidArgument
     # count 0 is a successful no-op even with bogus pointers
     assert L.vcclReduceCopy(0, 7, 0, 0, 0, 1, s, 1, d, 0, None) == nccl.ncclSuccess
+
+
+@pytest.mark.parametrize("t", [10, 11])
+def test_fp8_all_code_pairs(t):
+    """Every (a, b) fp8 code pair through the device for sum/prod/min/max and
+    the avg preOp: bit-exact to the oracle (NaN by NaN-ness, +-0 for min/max)."""
+    codes = np.arange(256, dtype=np.uint8)
+    a, b = np.repeat(codes, 256), np.tile(codes, 256)
+    for op in (0, 1, 2, 3, 4):
+        dev_op, arg, pre, post = _dev_args(op, t, 2)
+        got = _run(dev_op, t, arg, [a, b], pre=pre, post=post)[0]
+        exp = O.reduce_copy(dev_op, t, arg, [a, b], pre_op_args=[arg] * pre, post_op=post)[0]
+        assert_bitexact(t, got, exp, minmax=op in (2, 3), what=f"fp8 t{t} op{op}")

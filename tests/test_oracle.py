@@ -111,10 +111,10 @@ def test_functable_signed_maps_to_unsigned():
     table = json.load(open(os.path.join(ROOT, "tests", "golden", "functable.json")))
     devop = {"Sum": 0, "Prod": 1, "MinMax": 2, "PreMulSum": 3, "SumPostDiv": 4}
     tyid = {"i8": 0, "u8": 1, "i32": 2, "u32": 3, "i64": 4, "u64": 5, "f16": 6, "f32": 7,
-            "f64": 8, "bf16": 9}
+            "f64": 8, "bf16": 9, "f8e4m3": 10, "f8e5m2": 11}
     by_key = {}
     for r in table["rows"]:
-        if r["coll"] == "AllGather" or r["type"] in ("f8e4m3", "f8e5m2"):
+        if r["coll"] == "AllGather":
             continue
         by_key.setdefault((r["coll"], r["redop"], r["algo"], r["proto"]), []).append(r)
     kt = lambda r: nccl.kernel_type_of(devop[r["redop"]], tyid[r["type"]])  # noqa: E731
@@ -143,3 +143,70 @@ def test_oracle_chain_fold_order():
                 exp = (exp + xs[p]).astype(npdt)
             got = O.chain_fold(O.DEV_SUM, dt, 0, False, xs)
             assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (dt, n)
+
+
+# ---------------------------------------------------------------- fp8
+# The reference reduces fp8 through __half (reduce_kernel.h:309-321) with
+# CUDA's cuda_fp8.h conversions (absent here).  The oracle's conversions and
+# its two-rounding arithmetic are pinned against torch-CPU's independent
+# float8_e4m3fn / float8_e5m2 implementation (RN-even; torch does NOT saturate,
+# so out-of-range results are checked against the satfinite rule separately).
+FP8_TORCH = {10: torch.float8_e4m3fn, 11: torch.float8_e5m2}
+FP8_MAX = {10: 448.0, 11: 57344.0}
+
+
+@pytest.mark.parametrize("t", [10, 11])
+def test_fp8_decode_all_codes_against_torch(t):
+    codes = np.arange(256, dtype=np.uint8)
+    ours = O.fp8_bits_to_f32(t, codes)
+    ref = torch.from_numpy(codes).view(FP8_TORCH[t]).float().numpy()
+    nan = np.isnan(ref)
+    assert np.array_equal(np.isnan(ours), nan)
+    assert np.array_equal(ours[~nan].view(np.uint32), ref[~nan].view(np.uint32))
+
+
+@pytest.mark.parametrize("t", [10, 11])
+def test_fp8_encode_every_half_against_torch(t):
+    L = O.lib()
+    h = np.arange(0, 1 << 16, dtype=np.uint32).astype(np.uint16).view(np.float16).astype(np.float32)
+    ours = np.array([L.ref_f32_to_fp8(t, float(x)) for x in h], dtype=np.uint8)
+    ref = torch.from_numpy(h).to(FP8_TORCH[t]).view(torch.uint8).numpy()
+    fin = np.isfinite(h) & (np.abs(h) <= FP8_MAX[t])
+    assert np.array_equal(ours[fin], ref[fin])
+    big = np.isfinite(h) & (np.abs(h) > FP8_MAX[t]) | np.isinf(h)  # satfinite: +-max
+    maxcode = 0x7E if t == 10 else 0x7B
+    assert np.array_equal(ours[big], np.where(h[big] < 0, 0x80 | maxcode, maxcode).astype(np.uint8))
+    assert np.all(ours[np.isnan(h)] == 0x7F)
+
+
+@pytest.mark.parametrize("t", [10, 11])
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_fp8_all_pairs_against_torch_half(t, op):
+    """Every (a, b) code pair: oracle == fp8(half(a) (op) half(b)) computed
+    with torch half arithmetic and torch's fp8 narrowing (+ satfinite)."""
+    codes = np.arange(256, dtype=np.uint8)
+    a = np.repeat(codes, 256)
+    b = np.tile(codes, 256)
+    dev_op, arg = O.host_to_dev_redop(op, t, 2)
+    ours = O.reduce_copy(dev_op, t, arg, [a, b])[0]
+    ta = torch.from_numpy(a).view(FP8_TORCH[t]).half()
+    tb = torch.from_numpy(b).view(FP8_TORCH[t]).half()
+    r = {0: ta + tb, 1: ta * tb, 2: torch.fmax(ta, tb), 3: torch.fmin(ta, tb)}[op].float()
+    rn = r.numpy()
+    ref = r.to(FP8_TORCH[t]).view(torch.uint8).numpy()
+    fin = np.isfinite(rn) & (np.abs(rn) <= FP8_MAX[t])
+    assert np.array_equal(ours[fin], ref[fin]) or (op in (2, 3) and np.array_equal(
+        O.fp8_bits_to_f32(t, ours[fin]), O.fp8_bits_to_f32(t, ref[fin])))
+    maxcode = 0x7E if t == 10 else 0x7B
+    big = ~np.isnan(rn) & ~fin
+    assert np.array_equal(ours[big], np.where(rn[big] < 0, 0x80 | maxcode, maxcode).astype(np.uint8))
+    assert np.all(ours[np.isnan(rn)] == 0x7F)
+
+
+def test_fp8_avg_scalar_encoding():
+    # enqueue.cc:2265-2272: __nv_cvt_float_to_fp8(float(1.0/n), SATFINITE, fmt)
+    for t in (10, 11):
+        for n in (2, 3, 5, 7, 8):
+            dev_op, arg = O.host_to_dev_redop(4, t, n)
+            ref = torch.tensor([1.0 / n], dtype=torch.float32).to(FP8_TORCH[t]).view(torch.uint8).item()
+            assert (dev_op, arg) == (3, ref)

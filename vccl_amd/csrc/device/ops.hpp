@@ -26,12 +26,65 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 
 struct bf16_t { uint16_t bits; };  // storage-only tag type
 
+// ---------------------------------------------------------------- fp8 bits
+// OCP FP8 (gfx950's native formats): E4M3 ("fn": bias 7, no infinity, NaN =
+// S.1111.111, max 448) and E5M2 (bias 15, IEEE-like, max 57344).  The
+// reference reduces fp8 through __half (reduce_kernel.h:309-321): widen to
+// half (exact), __hadd/__hmul/__hmin/__hmax in half (one RN-even rounding),
+// narrow with __NV_SATFINITE (RN-even; beyond max finite -> max finite,
+// infinity -> max finite, NaN -> NaN).  Here the same two roundings run on
+// _Float16 (v_add_f16 / v_mul_f16 are correctly rounded) plus integer
+// narrowing on the half bits.
+struct f8e4m3_t { uint8_t bits; };
+struct f8e5m2_t { uint8_t bits; };
+
+__device__ __forceinline__ _Float16 h_of_bits(uint16_t b) { return __builtin_bit_cast(_Float16, b); }
+__device__ __forceinline__ uint16_t bits_of_h(_Float16 h) { return __builtin_bit_cast(uint16_t, h); }
+
+// E5M2 is binary16 with the low 8 mantissa bits dropped: widening is a shift.
+__device__ __forceinline__ _Float16 f8_to_h(f8e5m2_t x) { return h_of_bits((uint16_t)(x.bits << 8)); }
+// E4M3 magnitude bits placed in binary16 with exponent bias 15 are the value
+// times 2^-8 (subnormals included), so one exact multiply by 256 rebiases.
+__device__ __forceinline__ _Float16 f8_to_h(f8e4m3_t x) {
+  const uint32_t a = x.bits & 0x7fu;
+  if (a == 0x7fu) return h_of_bits(0x7fffu);
+  const _Float16 v = h_of_bits((uint16_t)(a << 7)) * (_Float16)256.0f;
+  return (x.bits & 0x80u) ? -v : v;
+}
+// binary16 -> E5M2, RN-even on the dropped 8 bits, saturating.
+__device__ __forceinline__ uint8_t h_to_e5m2(_Float16 h) {
+  const uint32_t b = bits_of_h(h), a = b & 0x7fffu, s = (b >> 8) & 0x80u;
+  if (a > 0x7c00u) return 0x7fu;
+  uint32_t r = (a + 0x7fu + ((a >> 8) & 1u)) >> 8;
+  if (r > 0x7bu) r = 0x7bu;
+  return (uint8_t)(s | r);
+}
+// binary16 -> E4M3, RN-even, saturating.  Normal E4M3 results (half exponent
+// >= 9) drop 7 mantissa bits and rebias by 8 exponents; below 2^-6 the result
+// counts units of 2^-9: rint(|h| * 512) (exact scaling in f32).
+__device__ __forceinline__ uint8_t h_to_e4m3(_Float16 h) {
+  const uint32_t b = bits_of_h(h), a = b & 0x7fffu, s = (b >> 8) & 0x80u;
+  if (a > 0x7c00u) return 0x7fu;
+  uint32_t code;
+  if (a >= (9u << 10)) code = ((a + 0x3fu + ((a >> 7) & 1u)) >> 7) - (8u << 3);
+  else code = (uint32_t)__builtin_rintf((float)h_of_bits((uint16_t)a) * 512.0f);
+  if (code > 0x7eu) code = 0x7eu;
+  return (uint8_t)(s | code);
+}
+__device__ __forceinline__ f8e4m3_t f8_from_h(_Float16 h, f8e4m3_t) { return {h_to_e4m3(h)}; }
+__device__ __forceinline__ f8e5m2_t f8_from_h(_Float16 h, f8e5m2_t) { return {h_to_e5m2(h)}; }
+
 // ---------------------------------------------------------------- helpers
 template <typename T> struct IsFloat { static constexpr bool value = false; };
 template <> struct IsFloat<_Float16> { static constexpr bool value = true; };
 template <> struct IsFloat<float> { static constexpr bool value = true; };
 template <> struct IsFloat<double> { static constexpr bool value = true; };
 template <> struct IsFloat<bf16_t> { static constexpr bool value = true; };
+template <> struct IsFloat<f8e4m3_t> { static constexpr bool value = true; };
+template <> struct IsFloat<f8e5m2_t> { static constexpr bool value = true; };
+template <typename T> struct IsF8 { static constexpr bool value = false; };
+template <> struct IsF8<f8e4m3_t> { static constexpr bool value = true; };
+template <> struct IsF8<f8e5m2_t> { static constexpr bool value = true; };
 
 template <typename T>
 __device__ __forceinline__ T from_arg(uint64_t arg) {
@@ -187,6 +240,60 @@ template <> struct FnPreMulSum<bf16_t> {
   }
   __device__ __forceinline__ bf16_t postOp(bf16_t a) const { return a; }
 };
+
+// ---------------------------------------------------------------- fp8 ops
+// reduce_kernel.h:309-321 (Sum / Prod / MinMax through __half) and :489-511,
+// :586-624 (PreMulSum: the scalar arrives as fp8 bits, widened to half once;
+// preOp = fp8(__hmul(half(x), scalar))).
+#define VCCL_F8_FUNCTORS(F8)                                                              \
+  template <> struct FnSum<F8> {                                                          \
+    using EltType = F8;                                                                   \
+    static constexpr bool kPreOp = false, kPostOp = false;                                \
+    __device__ FnSum(uint64_t = 0) {}                                                     \
+    __device__ __forceinline__ F8 reduce(F8 a, F8 b) const {                              \
+      return f8_from_h(f8_to_h(a) + f8_to_h(b), F8{});                                    \
+    }                                                                                     \
+    __device__ __forceinline__ F8 preOp(F8 a) const { return a; }                         \
+    __device__ __forceinline__ F8 postOp(F8 a) const { return a; }                        \
+  };                                                                                      \
+  template <> struct FnProd<F8> {                                                         \
+    using EltType = F8;                                                                   \
+    static constexpr bool kPreOp = false, kPostOp = false;                                \
+    __device__ FnProd(uint64_t = 0) {}                                                    \
+    __device__ __forceinline__ F8 reduce(F8 a, F8 b) const {                              \
+      return f8_from_h(f8_to_h(a) * f8_to_h(b), F8{});                                    \
+    }                                                                                     \
+    __device__ __forceinline__ F8 preOp(F8 a) const { return a; }                         \
+    __device__ __forceinline__ F8 postOp(F8 a) const { return a; }                        \
+  };                                                                                      \
+  template <> struct FnMinMax<F8> {                                                       \
+    using EltType = F8;                                                                   \
+    static constexpr bool kPreOp = false, kPostOp = false;                                \
+    bool isMin;                                                                           \
+    __device__ FnMinMax(uint64_t arg = 0) : isMin((arg & 1) == 0) {}                      \
+    __device__ __forceinline__ F8 reduce(F8 a, F8 b) const {                              \
+      return f8_from_h((_Float16)minmax_f32((float)f8_to_h(a), (float)f8_to_h(b), isMin), \
+                       F8{});                                                             \
+    }                                                                                     \
+    __device__ __forceinline__ F8 preOp(F8 a) const { return a; }                         \
+    __device__ __forceinline__ F8 postOp(F8 a) const { return a; }                        \
+  };                                                                                      \
+  template <> struct FnPreMulSum<F8> {                                                    \
+    using EltType = F8;                                                                   \
+    static constexpr bool kPreOp = true, kPostOp = false;                                 \
+    _Float16 scalar;                                                                      \
+    __device__ FnPreMulSum(uint64_t arg = 0) : scalar(f8_to_h(F8{(uint8_t)arg})) {}       \
+    __device__ __forceinline__ F8 reduce(F8 a, F8 b) const {                              \
+      return f8_from_h(f8_to_h(a) + f8_to_h(b), F8{});                                    \
+    }                                                                                     \
+    __device__ __forceinline__ F8 preOp(F8 a) const {                                     \
+      return f8_from_h(f8_to_h(a) * scalar, F8{});                                        \
+    }                                                                                     \
+    __device__ __forceinline__ F8 postOp(F8 a) const { return a; }                        \
+  };
+VCCL_F8_FUNCTORS(f8e4m3_t)
+VCCL_F8_FUNCTORS(f8e5m2_t)
+#undef VCCL_F8_FUNCTORS
 
 // ---------------------------------------------------------------- SumPostDiv
 // reduce_kernel.h:641-688: integer avg = sum, then truncating divide at the

@@ -11,7 +11,7 @@ using namespace vccl;
 
 static int elt_size_of_kt(int k) {
   switch (k) {
-    case K_U8: return 1;
+    case K_U8: case K_F8E4M3: case K_F8E5M2: return 1;
     case K_F16: case K_BF16: return 2;
     case K_U32: case K_F32: return 4;
     default: return 8;
@@ -49,6 +49,8 @@ hipError_t reduce_copy_launch(int devOp, int datatype, uint64_t redArg, RCArgs a
     case K_F32: return rc_launch<K_F32>(devOp, a, nElts, redArg, lg, stream);
     case K_F64: return rc_launch<K_F64>(devOp, a, nElts, redArg, lg, stream);
     case K_BF16: return rc_launch<K_BF16>(devOp, a, nElts, redArg, lg, stream);
+    case K_F8E4M3: return rc_launch<K_F8E4M3>(devOp, a, nElts, redArg, lg, stream);
+    case K_F8E5M2: return rc_launch<K_F8E5M2>(devOp, a, nElts, redArg, lg, stream);
   }
   return hipErrorInvalidValue;
 }

@@ -53,6 +53,29 @@ static int type_size(ncclDataType_t t) {
   }
 }
 
+// __nv_cvt_float_to_fp8(f, __NV_SATFINITE, fmt) for the avg scalar
+// (enqueue.cc:2265-2272): RN-even to `mbits` mantissa bits with exponent bias
+// `bias`, magnitudes past max finite saturate, NaN -> 0x7f.
+static uint8_t f32_to_fp8_satfinite(float f, int mbits, int bias, uint32_t maxCode) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  const uint32_t s = (u >> 24) & 0x80u, a = u & 0x7fffffffu;
+  if (a > 0x7f800000u) return 0x7fu;
+  const int e = (int)(a >> 23) - 127, emin = 1 - bias;
+  if (a == 0) return (uint8_t)s;
+  const uint64_t m = (a & 0x7fffffu) | 0x800000u;
+  const int shift = (e >= emin ? e : emin) - mbits - e + 23;  // >= 23 - mbits
+  uint64_t q = 0;
+  if (shift < 40) {
+    q = m >> shift;
+    const uint64_t rem = m & ((1ull << shift) - 1), half = 1ull << (shift - 1);
+    if (rem > half || (rem == half && (q & 1))) q++;
+  }
+  uint64_t code = e >= emin ? ((uint64_t)(e + bias) << mbits) + (q - (1ull << mbits)) : q;
+  if (e > 15 + bias || code > maxCode) code = maxCode;
+  return (uint8_t)(s | code);
+}
+
 // hostToDevRedOp (enqueue.cc:2217-2310) for built-in ops.
 static ncclResult_t host_to_dev_redop(ncclRedOp_t op, ncclDataType_t dt, int nRanks, int* devOp,
                                       uint64_t* arg) {
@@ -108,6 +131,14 @@ static ncclResult_t host_to_dev_redop(ncclRedOp_t op, ncclDataType_t dt, int nRa
           memcpy(arg, &d, 8);
           return ncclSuccess;
         }
+        case ncclFloat8e4m3:
+          *devOp = OP_PREMULSUM;
+          *arg = f32_to_fp8_satfinite((float)(1.0 / nRanks), 3, 7, 0x7eu);
+          return ncclSuccess;
+        case ncclFloat8e5m2:
+          *devOp = OP_PREMULSUM;
+          *arg = f32_to_fp8_satfinite((float)(1.0 / nRanks), 2, 15, 0x7bu);
+          return ncclSuccess;
       }
       return ncclInvalidArgument;
   }
@@ -149,10 +180,7 @@ static ncclResult_t args_check(ncclComm* comm, const char* name, ncclDataType_t 
       return ncclInvalidArgument;
     }
   }
-  if (dt == ncclFloat8e4m3 || dt == ncclFloat8e5m2) {  // enqueue.cc:2379-2384
-    VWARN("%s : fp8 reductions are not built in this release", name);
-    return ncclInvalidArgument;
-  }
+  // fp8 (enqueue.cc:2379-2384 requires sm90 in the reference): native on gfx950
   return ncclSuccess;
 }
 
@@ -240,6 +268,8 @@ static ncclResult_t launch_ring(const Task& t) {
     case K_F32: e = ring_launch<K_F32>(coll, devOp, w, comm->nThreads, t.stream); break;
     case K_F64: e = ring_launch<K_F64>(coll, devOp, w, comm->nThreads, t.stream); break;
     case K_BF16: e = ring_launch<K_BF16>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_F8E4M3: e = ring_launch<K_F8E4M3>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_F8E5M2: e = ring_launch<K_F8E5M2>(coll, devOp, w, comm->nThreads, t.stream); break;
   }
   if (e != hipSuccess) {
     VWARN("ring kernel launch failed: %s", hipGetErrorString(e));
@@ -298,6 +328,8 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
     case K_F32: e = ll_launch<K_F32>(t.devOp, w, grid, t.stream); break;
     case K_F64: e = ll_launch<K_F64>(t.devOp, w, grid, t.stream); break;
     case K_BF16: e = ll_launch<K_BF16>(t.devOp, w, grid, t.stream); break;
+    case K_F8E4M3: e = ll_launch<K_F8E4M3>(t.devOp, w, grid, t.stream); break;
+    case K_F8E5M2: e = ll_launch<K_F8E5M2>(t.devOp, w, grid, t.stream); break;
   }
   if (e != hipSuccess) {
     VWARN("LL kernel launch failed: %s", hipGetErrorString(e));
@@ -350,6 +382,8 @@ static ncclResult_t launch_direct(const Task& t) {
     case K_F32: e = direct_launch<K_F32>(t.devOp, w, t.stream); break;
     case K_F64: e = direct_launch<K_F64>(t.devOp, w, t.stream); break;
     case K_BF16: e = direct_launch<K_BF16>(t.devOp, w, t.stream); break;
+    case K_F8E4M3: e = direct_launch<K_F8E4M3>(t.devOp, w, t.stream); break;
+    case K_F8E5M2: e = direct_launch<K_F8E5M2>(t.devOp, w, t.stream); break;
     default: return ncclInvalidArgument;
   }
   if (e != hipSuccess) {
@@ -565,7 +599,7 @@ VCCL_EXPORT ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar,
   NCCLCHECK(comm_check(comm, "ncclRedOpCreatePreMulSum"));
   if (!op || !scalar) return ncclInvalidArgument;
   const int sz = type_size(datatype);
-  if (sz < 1 || datatype == ncclFloat8e4m3 || datatype == ncclFloat8e5m2) return ncclInvalidArgument;
+  if (sz < 1) return ncclInvalidArgument;
   int ix = -1;
   for (int i = 0; i < (int)comm->userOps.size(); i++)
     if (comm->userOps[i].freeNext != -1) { ix = i; break; }
