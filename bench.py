@@ -119,7 +119,56 @@ def bench_reduce_copy(args):
         out["cpu_baseline"] = cpu_baseline(n)
     if not args.no_extras:
         out["extras"] = {"config1_allreduce_1KiB_world1": bench_one_rank_latency()}
+        del a, b, d
+        try:
+            out["extras"]["reduce_copy_by_dtype"] = bench_rc_dtypes(n * 4)
+        except Exception as e:  # noqa: BLE001 - reported, not fatal to the headline
+            out["extras"]["reduce_copy_by_dtype_error"] = repr(e)
     return out
+
+
+def bench_rc_dtypes(nbytes, steps=20, warmup=3):
+    """Config 2's shape (2 sources -> 1 destination, `nbytes` per buffer) for
+    each element type's sum kernel: GB/s (3 x nbytes per launch / event time
+    on the launch stream) and the HBM-roofline fraction.  Not `value`."""
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    L = nccl.lib()
+    rows = []
+    for name, dt in (("f32", nccl.ncclFloat32), ("f16", nccl.ncclFloat16), ("bf16", nccl.ncclBfloat16),
+                     ("f8e4m3", nccl.ncclFloat8e4m3), ("f8e5m2", nccl.ncclFloat8e5m2),
+                     ("i32", nccl.ncclInt32), ("u8", nccl.ncclUint8), ("f64", nccl.ncclFloat64)):
+        esz = {nccl.ncclFloat16: 2, nccl.ncclBfloat16: 2, nccl.ncclFloat8e4m3: 1,
+               nccl.ncclFloat8e5m2: 1, nccl.ncclUint8: 1, nccl.ncclFloat64: 8}.get(dt, 4)
+        n = nbytes // esz
+        a = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
+        b = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
+        if dt in (nccl.ncclFloat8e4m3, nccl.ncclFloat8e5m2):  # finite codes (no NaN/inf)
+            a &= 0x77
+            b &= 0x77
+        d = torch.empty_like(a)
+        srcs = (ctypes.c_void_p * 2)(a.data_ptr(), b.data_ptr())
+        dsts = (ctypes.c_void_p * 1)(d.data_ptr())
+
+        def step():
+            rc = L.vcclReduceCopy(0, dt, 0, 0, 0, 2, srcs, 1, dsts, n, sp)
+            if rc:
+                raise nccl.VcclError(rc, "vcclReduceCopy")
+
+        for _ in range(warmup):
+            step()
+        e0, e1 = _evt(), _evt()
+        e0.record(stream)
+        for _ in range(steps):
+            step()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / 1e3 / steps
+        gbs = 3 * nbytes / t / 1e9
+        rows.append({"dtype": name, "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "avg_launch_us": round(t * 1e6, 2)})
+        del a, b, d
+    return rows
 
 
 def bench_one_rank_latency(iters=1000):

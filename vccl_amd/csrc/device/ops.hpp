@@ -399,6 +399,69 @@ __device__ __forceinline__ u32x4 pack_reduce(const FnMinMax<uint8_t>& fn, u32x4 
   return r;
 }
 
+// fp8 sum on packed half pairs.  Each 32-bit word's even and odd bytes are
+// widened into two 16-bit lanes and added with v_pk_add_f16 (RN-even, the
+// __hadd2 of reduce_kernel.h:310/317).
+//  E5M2: byte << 8 IS the binary16 value.
+//  E4M3: magnitude << 7 (+ sign << 8) is the binary16 value times 2^-8, for
+//        subnormals too; the scaled sum is exact where the unscaled half sum
+//        would be (results < 2^-6 are multiples of 2^-9 with <= 3 significant
+//        bits; above, both live in half's normal range), and the scaled half's
+//        exponent field equals E4M3's, so narrowing is RN-even on the low 7 bits
+//        for every result.  NaN codes (S.1111.111) are forced to 0x7f.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+template <bool E4M3>
+__device__ __forceinline__ uint32_t f8x2_widen(uint32_t lanes) {  // two bytes in 16-bit lanes
+  if constexpr (E4M3) return ((lanes & 0x007f007fu) << 7) | ((lanes & 0x00800080u) << 8);
+  return lanes << 8;
+}
+template <bool E4M3>
+__device__ __forceinline__ uint32_t f8x2_narrow(uint32_t h) {  // two halves -> two codes in lanes
+  const u16x2 mag = as_u16x2(h & 0x7fff7fffu);
+  const uint32_t sign = (h >> 8) & 0x00800080u;
+  if constexpr (E4M3) {
+    u16x2 r = (mag + (u16x2)0x3f + ((mag >> 7) & (u16x2)1)) >> 7;
+    r = __builtin_elementwise_min(r, (u16x2)0x7e);
+    return as_u32(r) | sign;
+  } else {
+    u16x2 r = (mag + (u16x2)0x7f + ((mag >> 8) & (u16x2)1)) >> 8;
+    r = __builtin_elementwise_min(r, (u16x2)0x7b);  // infinity and NaN -> 0x7b
+    // bit 15 of mag + 0x3ff is set iff mag > 0x7c00 (NaN): no compare, no VCC
+    const uint32_t nanb = as_u32(mag + (u16x2)0x3ffu) & 0x80008000u;
+    return as_u32(r) | (nanb >> 13) | (sign & ~(nanb >> 8));  // NaN: 0x7b | 0x04 = 0x7f, no sign
+  }
+}
+template <bool E4M3>
+__device__ __forceinline__ uint32_t f8x4_add(uint32_t a, uint32_t b) {
+  const uint32_t alo = f8x2_widen<E4M3>(a & 0x00ff00ffu), ahi = f8x2_widen<E4M3>((a >> 8) & 0x00ff00ffu);
+  const uint32_t blo = f8x2_widen<E4M3>(b & 0x00ff00ffu), bhi = f8x2_widen<E4M3>((b >> 8) & 0x00ff00ffu);
+  const f16x2 slo = __builtin_bit_cast(f16x2, alo) + __builtin_bit_cast(f16x2, blo);
+  const f16x2 shi = __builtin_bit_cast(f16x2, ahi) + __builtin_bit_cast(f16x2, bhi);
+  uint32_t r = f8x2_narrow<E4M3>(__builtin_bit_cast(uint32_t, slo)) |
+               (f8x2_narrow<E4M3>(__builtin_bit_cast(uint32_t, shi)) << 8);
+  if constexpr (E4M3) {  // byte-wise NaN mask: (code & 0x7f) == 0x7f in either input
+    const uint32_t na = ((a & 0x7f7f7f7fu) + 0x01010101u) & 0x80808080u;
+    const uint32_t nb = ((b & 0x7f7f7f7fu) + 0x01010101u) & 0x80808080u;
+    const uint32_t n = na | nb, n7f = n - (n >> 7);  // 0x7f in every NaN byte
+    r = (r & ~(n | n7f)) | n7f;
+  }
+  return r;
+}
+template <bool E4M3>
+__device__ __forceinline__ u32x4 f8_pack_add(u32x4 a, u32x4 b) {
+  return u32x4{f8x4_add<E4M3>(a.x, b.x), f8x4_add<E4M3>(a.y, b.y), f8x4_add<E4M3>(a.z, b.z),
+               f8x4_add<E4M3>(a.w, b.w)};
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnSum<f8e4m3_t>&, u32x4 a, u32x4 b) {
+  return f8_pack_add<true>(a, b);
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnPreMulSum<f8e4m3_t>&, u32x4 a, u32x4 b) {
+  return f8_pack_add<true>(a, b);
+}
+// E5M2 keeps the per-element functor: hipcc's lowering of it measured faster
+// on config 2's shape (7.1 vs 6.2 TB/s, profiles/r01v) than
+// f8_pack_add<false> (bit-exact in the same run's all-pairs test; unused).
+
 template <class Fn>
 __device__ __forceinline__ u32x4 pack_preop(const Fn& fn, u32x4 a) {
   using T = typename Fn::EltType;
