@@ -452,15 +452,75 @@ __device__ __forceinline__ u32x4 f8_pack_add(u32x4 a, u32x4 b) {
   return u32x4{f8x4_add<E4M3>(a.x, b.x), f8x4_add<E4M3>(a.y, b.y), f8x4_add<E4M3>(a.z, b.z),
                f8x4_add<E4M3>(a.w, b.w)};
 }
+// E4M3 sum on gfx950's fp8 conversion units: v_cvt_pk_f32_fp8 widens two
+// codes exactly, v_pk_add_f32 adds exactly (4-bit significands, exponents
+// 2^-9 .. 2^8), v_med3_f32 clamps to +-448 (satfinite) and v_cvt_pk_fp8_f32
+// narrows RN-even.  One rounding of the exact sum equals the reference's
+// fp8(RN_half(a + b)): a sum needing more than half's 11 bits has operands
+// >= 8 binades apart, so the smaller one moves the result less than 2^-7 of
+// the larger — never to or across an E4M3 rounding midpoint (checked
+// exhaustively: all 65,536 code pairs, test_fp8_all_code_pairs).  NaN codes
+// are patched with the byte-wise mask (med3 does not keep NaN).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t e4m3x4_add_cvt(uint32_t a, uint32_t b) {
+  const f32x2 lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)a, false) + __builtin_amdgcn_cvt_pk_f32_fp8((int)b, false);
+  const f32x2 hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)a, true) + __builtin_amdgcn_cvt_pk_f32_fp8((int)b, true);
+  const float m = 448.0f;
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(lo.x, -m, m),
+                                         __builtin_amdgcn_fmed3f(lo.y, -m, m), 0, false);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(hi.x, -m, m),
+                                     __builtin_amdgcn_fmed3f(hi.y, -m, m), r, true);
+  const uint32_t na = ((a & 0x7f7f7f7fu) + 0x01010101u) & 0x80808080u;
+  const uint32_t nb = ((b & 0x7f7f7f7fu) + 0x01010101u) & 0x80808080u;
+  const uint32_t n = na | nb, n7f = n - (n >> 7);
+  return ((uint32_t)r & ~(n | n7f)) | n7f;
+}
+__device__ __forceinline__ u32x4 e4m3_pack_add(u32x4 a, u32x4 b) {
+  return u32x4{e4m3x4_add_cvt(a.x, b.x), e4m3x4_add_cvt(a.y, b.y), e4m3x4_add_cvt(a.z, b.z),
+               e4m3x4_add_cvt(a.w, b.w)};
+}
 __device__ __forceinline__ u32x4 pack_reduce(const FnSum<f8e4m3_t>&, u32x4 a, u32x4 b) {
+#ifdef VCCL_F8_HALF_PAIRS
   return f8_pack_add<true>(a, b);
+#else
+  return e4m3_pack_add(a, b);
+#endif
 }
 __device__ __forceinline__ u32x4 pack_reduce(const FnPreMulSum<f8e4m3_t>&, u32x4 a, u32x4 b) {
-  return f8_pack_add<true>(a, b);
+  return pack_reduce(FnSum<f8e4m3_t>(), a, b);
 }
-// E5M2 keeps the per-element functor: hipcc's lowering of it measured faster
-// on config 2's shape (7.1 vs 6.2 TB/s, profiles/r01v) than
-// f8_pack_add<false> (bit-exact in the same run's all-pairs test; unused).
+// E5M2 the same way (v_cvt_pk_f32_bf8 / v_cvt_pk_bf8_f32; 3-bit significands,
+// so the f32 sum is exact and the single-rounding argument holds with margin;
+// the clamp to +-57344 also maps infinity to max finite, as satfinite does).
+// NaN: a NaN input (magnitude code > 0x7c) or +inf + -inf, by byte-wise masks.
+__device__ __forceinline__ uint32_t e5m2x4_add_cvt(uint32_t a, uint32_t b) {
+  const f32x2 lo = __builtin_amdgcn_cvt_pk_f32_bf8((int)a, false) + __builtin_amdgcn_cvt_pk_f32_bf8((int)b, false);
+  const f32x2 hi = __builtin_amdgcn_cvt_pk_f32_bf8((int)a, true) + __builtin_amdgcn_cvt_pk_f32_bf8((int)b, true);
+  const float m = 57344.0f;
+  int r = __builtin_amdgcn_cvt_pk_bf8_f32(__builtin_amdgcn_fmed3f(lo.x, -m, m),
+                                         __builtin_amdgcn_fmed3f(lo.y, -m, m), 0, false);
+  r = __builtin_amdgcn_cvt_pk_bf8_f32(__builtin_amdgcn_fmed3f(hi.x, -m, m),
+                                     __builtin_amdgcn_fmed3f(hi.y, -m, m), r, true);
+  const uint32_t ma = a & 0x7f7f7f7fu, mb = b & 0x7f7f7f7fu;
+  const uint32_t nanIn = ((ma + 0x03030303u) | (mb + 0x03030303u)) & 0x80808080u;
+  const uint32_t infA = ~((ma ^ 0x7c7c7c7cu) + 0x7f7f7f7fu) & 0x80808080u;  // exact byte == 0x7c
+  const uint32_t infB = ~((mb ^ 0x7c7c7c7cu) + 0x7f7f7f7fu) & 0x80808080u;
+  const uint32_t n = nanIn | (infA & infB & (a ^ b)), n7f = n - (n >> 7);
+  return ((uint32_t)r & ~(n | n7f)) | n7f;
+}
+// Off by default: the per-element lowering measured faster for E5M2
+// (6.56-6.79 vs 6.28-6.49 TB/s interleaved, profiles/r01w/ab_fp8.log; the
+// cvt form needs 76 VGPRs against E4M3's 61).  -DVCCL_F8_E5M2_CVT selects it.
+#ifdef VCCL_F8_E5M2_CVT
+__device__ __forceinline__ u32x4 pack_reduce(const FnSum<f8e5m2_t>&, u32x4 a, u32x4 b) {
+  return u32x4{e5m2x4_add_cvt(a.x, b.x), e5m2x4_add_cvt(a.y, b.y), e5m2x4_add_cvt(a.z, b.z),
+               e5m2x4_add_cvt(a.w, b.w)};
+}
+__device__ __forceinline__ u32x4 pack_reduce(const FnPreMulSum<f8e5m2_t>&, u32x4 a, u32x4 b) {
+  return pack_reduce(FnSum<f8e5m2_t>(), a, b);
+}
+#endif
+// (f8_pack_add<false>, the E5M2 form, measured 6.2 TB/s and is unused.)
 
 template <class Fn>
 __device__ __forceinline__ u32x4 pack_preop(const Fn& fn, u32x4 a) {
