@@ -1,5 +1,5 @@
 set -e
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r01s; mkdir -p $O
+R=$GRAFT_REPO_ROOT; RUN=${RUN:-r01s}; O=$R/gpurun_out/$RUN; mkdir -p $O
 cd $R
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
