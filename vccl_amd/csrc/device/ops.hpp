@@ -490,27 +490,27 @@ __device__ __forceinline__ u32x4 pack_reduce(const FnPreMulSum<f8e4m3_t>&, u32x4
   return pack_reduce(FnSum<f8e4m3_t>(), a, b);
 }
 // E5M2 the same way (v_cvt_pk_f32_bf8 / v_cvt_pk_bf8_f32; 3-bit significands,
-// so the f32 sum is exact and the single-rounding argument holds with margin;
-// the clamp to +-57344 also maps infinity to max finite, as satfinite does).
-// NaN: a NaN input (magnitude code > 0x7c) or +inf + -inf, by byte-wise masks.
+// so the f32 sum is exact and the single-rounding argument holds with margin),
+// but narrowed WITHOUT a clamp: the converter rounds RN-even and returns the
+// infinity code 0x7c for anything past max finite and a NaN code (magnitude
+// > 0x7c) for NaN (probed on the box: tools/probe_fp8_cvt.hip,
+// profiles/r01y/probe.log), so satfinite and the canonical NaN are byte-wise
+// fix-ups on the result alone: 0x7c -> 0x7b (sign kept), NaN -> 0x7f.
 __device__ __forceinline__ uint32_t e5m2x4_add_cvt(uint32_t a, uint32_t b) {
   const f32x2 lo = __builtin_amdgcn_cvt_pk_f32_bf8((int)a, false) + __builtin_amdgcn_cvt_pk_f32_bf8((int)b, false);
   const f32x2 hi = __builtin_amdgcn_cvt_pk_f32_bf8((int)a, true) + __builtin_amdgcn_cvt_pk_f32_bf8((int)b, true);
-  const float m = 57344.0f;
-  int r = __builtin_amdgcn_cvt_pk_bf8_f32(__builtin_amdgcn_fmed3f(lo.x, -m, m),
-                                         __builtin_amdgcn_fmed3f(lo.y, -m, m), 0, false);
-  r = __builtin_amdgcn_cvt_pk_bf8_f32(__builtin_amdgcn_fmed3f(hi.x, -m, m),
-                                     __builtin_amdgcn_fmed3f(hi.y, -m, m), r, true);
-  const uint32_t ma = a & 0x7f7f7f7fu, mb = b & 0x7f7f7f7fu;
-  const uint32_t nanIn = ((ma + 0x03030303u) | (mb + 0x03030303u)) & 0x80808080u;
-  const uint32_t infA = ~((ma ^ 0x7c7c7c7cu) + 0x7f7f7f7fu) & 0x80808080u;  // exact byte == 0x7c
-  const uint32_t infB = ~((mb ^ 0x7c7c7c7cu) + 0x7f7f7f7fu) & 0x80808080u;
-  const uint32_t n = nanIn | (infA & infB & (a ^ b)), n7f = n - (n >> 7);
-  return ((uint32_t)r & ~(n | n7f)) | n7f;
+  int ri = __builtin_amdgcn_cvt_pk_bf8_f32(lo.x, lo.y, 0, false);
+  ri = __builtin_amdgcn_cvt_pk_bf8_f32(hi.x, hi.y, ri, true);
+  uint32_t r = (uint32_t)ri;
+  const uint32_t mag = r & 0x7f7f7f7fu;
+  const uint32_t inf = ~((mag ^ 0x7c7c7c7cu) + 0x7f7f7f7fu) & 0x80808080u;  // exact byte == 0x7c
+  const uint32_t n = (mag + 0x03030303u) & 0x80808080u, n7f = n - (n >> 7);  // byte > 0x7c
+  r -= inf >> 7;  // 0x7c -> 0x7b in those bytes (no borrow: the byte is >= 0x7c)
+  return (r & ~(n | n7f)) | n7f;
 }
-// Off by default: the per-element lowering measured faster for E5M2
-// (6.56-6.79 vs 6.28-6.49 TB/s interleaved, profiles/r01w/ab_fp8.log; the
-// cvt form needs 76 VGPRs against E4M3's 61).  -DVCCL_F8_E5M2_CVT selects it.
+// Off by default: measured level with the per-element lowering for E5M2
+// (6.62-6.75 TB/s either way, interleaved, profiles/r01z/ab_fp8.log; bit-exact
+// in that run's tests under VCCL_LIB).  -DVCCL_F8_E5M2_CVT selects it.
 #ifdef VCCL_F8_E5M2_CVT
 __device__ __forceinline__ u32x4 pack_reduce(const FnSum<f8e5m2_t>&, u32x4 a, u32x4 b) {
   return u32x4{e5m2x4_add_cvt(a.x, b.x), e5m2x4_add_cvt(a.y, b.y), e5m2x4_add_cvt(a.z, b.z),
