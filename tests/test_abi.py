@@ -44,9 +44,14 @@ def test_version_and_errors():
 
 def test_host_to_dev_redop_matches_oracle():
     for op in range(5):
-        for t in range(10):
+        for t in range(12):
             for n in (1, 2, 3, 8):
                 assert nccl.host_to_dev_redop(op, t, n) == O.host_to_dev_redop(op, t, n), (op, t, n)
+    # fp8 avg scalar fp8(float(1/n)) (enqueue.cc:2265-2272) over every rank
+    # count up to 4096 (RN-even ties, subnormal scalars, the E4M3 zero)
+    for t in (10, 11):
+        for n in range(1, 4097):
+            assert nccl.host_to_dev_redop(4, t, n) == O.host_to_dev_redop(4, t, n), (t, n)
     assert nccl.lib().vcclHostToDevRedOp(0, 12, 1, ctypes.byref(ctypes.c_int()),
                                          ctypes.byref(ctypes.c_uint64())) == nccl.ncclInvalidArgument
 
