@@ -36,6 +36,13 @@ def main():
         elif coll == "ar_inplace":
             comm.all_reduce(xb.data_ptr(), xb.data_ptr(), count, dt, op, s)
             yb = xb
+        elif coll == "ar_mis":
+            so, ro = RC.mis_offsets(dt)
+            xm = torch.zeros(xb.numel() + 16, dtype=torch.uint8, device="cuda")
+            xm[so:so + xb.numel()] = xb
+            ym = torch.zeros(yb.numel() + 16, dtype=torch.uint8, device="cuda")
+            comm.all_reduce(xm.data_ptr() + so, ym.data_ptr() + ro, count, dt, op, s)
+            yb = ym[ro:ro + yb.numel()]
         elif coll == "rs":
             comm.reduce_scatter(xb.data_ptr(), yb.data_ptr(), count, dt, op, s)
         else:

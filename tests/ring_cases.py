@@ -41,7 +41,21 @@ CASES = [
     ("ar_f8e4m3_max_direct", "ar", 2, 10, 1_500_007),
     ("rs_f8e4m3_sum_odd", "rs", 0, 10, 20_001),
     ("rs_f8e5m2_prod", "rs", 1, 11, 9_999),
+    # user buffers off 16-byte alignment (send and receive by different
+    # amounts, MIS_OFFSETS): LL, direct (engine realignment + staged output)
+    ("ar_f32_sum_mis_direct", "ar_mis", 0, 7, 786_433),
+    ("ar_bf16_avg_mis_direct", "ar_mis", 4, 9, 1_200_001),
+    ("ar_u8_max_mis_direct", "ar_mis", 2, 1, 3_000_001),
+    ("ar_f64_sum_mis_direct", "ar_mis", 0, 8, 300_001),
+    ("ar_f16_sum_mis_ll", "ar_mis", 0, 6, 20_001),
 ]
+
+
+def mis_offsets(dt):
+    """(send, recv) byte offsets of the "ar_mis" buffers: element-aligned,
+    off 16-byte alignment, different from each other where possible."""
+    esz = np.dtype(O.NP_DTYPE[dt]).itemsize
+    return esz % 16, (3 * esz) % 16
 
 
 def _fp8_codes(dt, x):
@@ -125,7 +139,7 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
     ones the ring (owner-map ring fold)."""
     name, coll, op, dt, count = CASES[case_idx]
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
-    if coll in ("ar", "ar_inplace"):
+    if coll in ("ar", "ar_inplace", "ar_mis"):
         e = expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk)
         return [e] * n_ranks
     if coll == "rs":

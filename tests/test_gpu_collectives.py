@@ -102,6 +102,13 @@ def test_single_process_ranks(n, monkeypatch):
             nout = RC.out_count(ci, n)
             yb = [torch.empty(nout * xs[0].dtype.itemsize, dtype=torch.uint8, device="cuda")
                   for _ in range(n)]
+            keep = []
+            if coll == "ar_mis":  # the same bytes at (send, recv) offsets off 16-byte alignment
+                so, ro = RC.mis_offsets(dt)
+                for r in range(n):
+                    xm = torch.zeros(xb[r].numel() + 16, dtype=torch.uint8, device="cuda")
+                    xm[so:so + xb[r].numel()] = xb[r]
+                    keep.append((xm, torch.zeros(yb[r].numel() + 16, dtype=torch.uint8, device="cuda")))
             torch.cuda.synchronize()
             nccl.group_start()
             for r, c in enumerate(comms):
@@ -110,6 +117,10 @@ def test_single_process_ranks(n, monkeypatch):
                     c.all_reduce(xb[r].data_ptr(), yb[r].data_ptr(), count, dt, op, sp)
                 elif coll == "ar_inplace":
                     c.all_reduce(xb[r].data_ptr(), xb[r].data_ptr(), count, dt, op, sp)
+                elif coll == "ar_mis":
+                    xm, ym = keep[r]
+                    c.all_reduce(xm.data_ptr() + so, ym.data_ptr() + ro, count, dt, op, sp)
+                    yb[r] = ym[ro:ro + yb[r].numel()]
                 elif coll == "rs":
                     c.reduce_scatter(xb[r].data_ptr(), yb[r].data_ptr(), count, dt, op, sp)
                 else:

@@ -1,0 +1,4 @@
+set -e
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r01aa; mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests/test_gpu_collectives.py -x -v --timeout 300 --timeout-method thread > $O/pytest_coll.log 2>&1

@@ -108,7 +108,28 @@ __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)
 #pragma unroll
   for (int d = 0; d < kDirectMaxRanks; d++)
     if (d < nD) bits |= (uintptr_t)dst[d];
-  const int64_t nPacks = (bits & 15) == 0 ? nElts * (int64_t)sizeof(T) / 16 : 0;
+  if (bits & 15) {
+    // Misaligned user buffers: the reduce-copy engine (reduce_copy.hpp) keeps
+    // 16-byte packs whenever the destinations share one misalignment —
+    // sources at other offsets are realigned by wavefront shuffle + funnel
+    // shift.  The callers below arrange that (a misaligned own output is
+    // staged through the aligned inbox).  Stores all write-through here.
+    RCArgs a;
+#pragma unroll
+    for (int q = 0; q < kDirectMaxRanks; q++) {
+      a.srcs[q] = q < nS ? src[q] : src[0];
+      a.dsts[q] = q < nD ? dst[q] : dst[0];
+    }
+    a.nSrcs = nS;
+    a.nDsts = nD;
+    a.preOpSrcs = preN;
+    a.postOp = post ? 1 : 0;
+    a.argPtr = nullptr;
+    a.argBytes = 0;
+    reduce_copy<Fn, 0, 0, 1, uniform_pol(LDP, kSys), 0, true>(fn, a, nElts, 0, 1, tid, nthreads);
+    return;
+  }
+  const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;
   const int64_t hunk = (int64_t)nthreads * U;
   for (int64_t base = 0; base < nPacks; base += hunk) {
     u32x4 v[kDirectMaxRanks][U];
@@ -151,7 +172,7 @@ __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)
       }
     }
   }
-  // Element path: misaligned operands or the < 16-byte tail.
+  // Element path: the < 16-byte tail.
   for (int64_t i = nPacks * 16 / (int64_t)sizeof(T) + tid; i < nElts; i += nthreads) {
     T acc = ldT<LDP, T>(src[0], i);
     if (Fn::kPreOp && preN > 0) acc = fn.preOp(acc);
@@ -246,6 +267,9 @@ __device__ void direct_allreduce(const DirectWork& w) {
     const char* in = (const char*)w.sendbuff + c0 * (int64_t)sizeof(T);
     char* out = (char*)w.recvbuff + c0 * (int64_t)sizeof(T);
     const int64_t inOff = (int64_t)b * w.blkElts * (int64_t)sizeof(T);  // block offset in a region
+    // Block offsets are 16-byte multiples, so every block of `out` shares the
+    // chunk base's misalignment (the inbox regions are 16-byte aligned).
+    const bool outMis = ((uintptr_t)out & 15) != 0;
     auto block_of = [&](int o, int64_t* off, int64_t* len) {
       int64_t shardEnd = (int64_t)(o + 1) * shardElts;
       shardEnd = shardEnd < cc ? shardEnd : cc;
@@ -274,7 +298,9 @@ __device__ void direct_allreduce(const DirectWork& w) {
       int64_t off, len;
       block_of(me, &off, &len);
       // Operand j < n-1: peer (me + j + 1) mod n; operand n-1: my own input /
-      // output.  Filled with compile-time indices only (no scratch array).
+      // output (staged in my own aligned region (1, me) when the output is
+      // off 16-byte alignment, copied out in phase 3 with the other blocks).
+      // Filled with compile-time indices only (no scratch array).
       const char* s[kDirectMaxRanks];
       char* d[kDirectMaxRanks];
 #pragma unroll
@@ -285,7 +311,8 @@ __device__ void direct_allreduce(const DirectWork& w) {
           d[j] = P.buf[src] + direct_region_off(1, me, n, w.regionBytes) + inOff;
         } else {
           s[j] = in + off * (int64_t)sizeof(T);
-          d[j] = out + off * (int64_t)sizeof(T);
+          d[j] = outMis ? myBuf + direct_region_off(1, me, n, w.regionBytes) + inOff
+                        : out + off * (int64_t)sizeof(T);
         }
       }
       direct_rc<Fn, kDirectUnroll, kSys, kSys, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, n, len,
@@ -293,9 +320,9 @@ __device__ void direct_allreduce(const DirectWork& w) {
     }
     direct_post(w, P, 1, b, e);
 
-    // Phase 3: gather the other owners' reduced blocks.
+    // Phase 3: gather the other owners' reduced blocks (and my own, if staged).
     if (direct_wait(w, myFlags, 1, b, e, &shFail)) {
-      for (int k = 1; k < n; k++) {
+      for (int k = outMis ? 0 : 1; k < n; k++) {
         const int o = me + k < n ? me + k : me + k - n;
         int64_t off, len;
         block_of(o, &off, &len);
