@@ -108,7 +108,13 @@ __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)
 #pragma unroll
   for (int d = 0; d < kDirectMaxRanks; d++)
     if (d < nD) bits |= (uintptr_t)dst[d];
+#ifdef VCCL_DIRECT_MIS_ELEMENTS  // A/B: the element path for any misalignment
+  const bool elemOnly = (bits & 15) != 0;
+  if (false) {
+#else
+  const bool elemOnly = false;
   if (bits & 15) {
+#endif
     // Misaligned user buffers: the reduce-copy engine (reduce_copy.hpp) keeps
     // 16-byte packs whenever the destinations share one misalignment —
     // sources at other offsets are realigned by wavefront shuffle + funnel
@@ -126,10 +132,13 @@ __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)
     a.postOp = post ? 1 : 0;
     a.argPtr = nullptr;
     a.argBytes = 0;
-    reduce_copy<Fn, 0, 0, 1, uniform_pol(LDP, kSys), 0, true>(fn, a, nElts, 0, 1, tid, nthreads);
+    if (nS == 1 && nD == 1)  // scatter / gather copies: batched shifted loads, 2 packs per thread
+      reduce_copy<Fn, 1, 1, 2, uniform_pol(LDP, kSys), 0, false>(fn, a, nElts, 0, 1, tid, nthreads);
+    else
+      reduce_copy<Fn, 0, 0, 1, uniform_pol(LDP, kSys), 0, true>(fn, a, nElts, 0, 1, tid, nthreads);
     return;
   }
-  const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;
+  const int64_t nPacks = elemOnly ? 0 : nElts * (int64_t)sizeof(T) / 16;
   const int64_t hunk = (int64_t)nthreads * U;
   for (int64_t base = 0; base < nPacks; base += hunk) {
     u32x4 v[kDirectMaxRanks][U];
@@ -269,7 +278,11 @@ __device__ void direct_allreduce(const DirectWork& w) {
     const int64_t inOff = (int64_t)b * w.blkElts * (int64_t)sizeof(T);  // block offset in a region
     // Block offsets are 16-byte multiples, so every block of `out` shares the
     // chunk base's misalignment (the inbox regions are 16-byte aligned).
+#ifdef VCCL_DIRECT_MIS_ELEMENTS
+    const bool outMis = false;
+#else
     const bool outMis = ((uintptr_t)out & 15) != 0;
+#endif
     auto block_of = [&](int o, int64_t* off, int64_t* len) {
       int64_t shardEnd = (int64_t)(o + 1) * shardElts;
       shardEnd = shardEnd < cc ? shardEnd : cc;
