@@ -72,6 +72,19 @@ def bench_reduce_copy(args):
         if rc:
             raise nccl.VcclError(rc, "vcclReduceCopy")
 
+    # Untimed pre-roll (reported as `preroll`, never counted): a fresh box's
+    # GPU starts the timed region cold otherwise — a 5-launch warmup is ~0.6
+    # ms of work, too short for the clocks to ramp, and the driver's round-1
+    # line read 0.890 of peak while the same kernel in the same run (after
+    # the CPU leg) read 0.911.  Fixed wall-clock budget of back-to-back
+    # launches, then the caller's --warmup and --steps unchanged.
+    pre_n, pre_t0 = 0, time.perf_counter()
+    while time.perf_counter() - pre_t0 < args.preroll_s:
+        for _ in range(64):
+            step()
+        torch.cuda.synchronize()
+        pre_n += 64
+    preroll = {"launches": pre_n, "s": round(time.perf_counter() - pre_t0, 3)}
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -114,7 +127,7 @@ def bench_reduce_copy(args):
            "config": {"workload": "reduce_copy 2-src fp32 sum, 256 MiB buffers (BASELINE config 2)",
                       "bytes_per_buffer": n * 4, "n_srcs": 2, "n_dsts": 1,
                       "launch": cfg or "library default"},
-           "roofline": roof}
+           "roofline": roof, "preroll": preroll}
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(n)
     if not args.no_extras:
@@ -214,27 +227,48 @@ def _pmc_traffic(workload, algo_bytes):
     return None
 
 
-def cpu_baseline(n_full):
-    """Oracle restatement (oracle/reduce_ref.c, -O3) on the host cores: the
-    same 2-src f32 sum shape, bounded to ~10 s of CPU work."""
+def _nproc():
+    """CPUs this process may run on (what `nproc` prints)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(n_full, seconds=8.0):
+    """SURVEY.md §8(d) CPU baseline: the oracle's C restatement (oracle/
+    reduce_ref.c, -O3) of the same 2-src f32 sum over the SAME shape as the
+    device step (2 x 256 MiB -> 256 MiB) in pinned host memory (torch
+    pin_memory = hipHostMalloc), on 1 core and on every core of the box
+    (`nproc` threads), each for a bounded sample of ~`seconds`.  `value` is the
+    all-cores figure; the 1-core figure rides along.  A reported baseline only
+    (the reference has no CPU reduce path)."""
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
-    n = min(n_full, 1 << 24)  # 64 MiB per buffer sample
-    rng = np.random.default_rng(1)
-    a = rng.uniform(-1, 1, n).astype(np.float32)
-    b = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
-    d = [np.empty_like(a)]
-    O.reduce_copy(0, 7, 0, [a, b], out=d, nthreads=threads)  # warm / page in
-    assert np.array_equal(d[0], a + b)
-    iters, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < 10.0:
-        O.reduce_copy(0, 7, 0, [a, b], out=d, nthreads=threads)
-        iters += 1
-    dt = time.perf_counter() - t0
-    gbs = 3 * n * 4 * iters / dt / 1e9
-    return {"value": round(gbs, 2), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{iters} x 2-src f32 sum over {n} elems (3 x {n*4 >> 20} MiB host buffers), "
-                      f"{dt:.1f} s, oracle/reduce_ref.c {threads} pthreads"}
+    n = n_full
+    a_t = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    b_t = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    d_t = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    a, b, d = a_t.numpy(), b_t.numpy(), d_t.numpy()
+    a[:] = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
+    b[:] = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
+    nproc = _nproc()
+    res = {}
+    for name, threads in (("one_core", 1), ("all_cores", nproc)):
+        O.reduce_copy(0, 7, 0, [a, b], out=[d], nthreads=threads)  # page in / warm
+        iters, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            O.reduce_copy(0, 7, 0, [a, b], out=[d], nthreads=threads)
+            iters += 1
+        dt = time.perf_counter() - t0
+        res[name] = {"GB/s": round(3 * n * 4 * iters / dt / 1e9, 2), "threads": threads,
+                     "iters": iters, "s": round(dt, 2)}
+    assert np.array_equal(d, a + b), "cpu baseline mismatch"
+    return {"value": res["all_cores"]["GB/s"], "unit": "GB/s", "cores": nproc, "kind": "port",
+            "sample": f"2-src f32 sum over {n} elems (3 x {n * 4 >> 20} MiB pinned host buffers), "
+                      f"oracle/reduce_ref.c -O3: {res['all_cores']['iters']} calls in "
+                      f"{res['all_cores']['s']} s on {nproc} pthreads (= nproc); "
+                      f"{res['one_core']['iters']} calls in {res['one_core']['s']} s on 1 thread",
+            "one_core": res["one_core"]["GB/s"], "nproc": nproc}
 
 
 def _dist_setup():
@@ -337,37 +371,183 @@ def peer_copy_bench(dist, rank, world, nbytes=256 << 20, steps=10):
     return res
 
 
-def allreduce_check(dist, comm, rank, world, nbytes=64 << 20):
-    """Exactness check on the real topology: integer-valued fp32 inputs
-    (sums exact in any fold order), every rank regenerates all inputs.
-    Checks one LL-protocol size (64 KiB) and one ring size (``nbytes``)."""
-    return all(_allreduce_check_one(dist, comm, rank, world, b) for b in (64 << 10, nbytes))
+# ----------------------------------------------------------------- checks
+# Every path the N > 1 line times gets a correctness verdict on the real
+# topology from integer-valued inputs, whose sums are exact in any fold order
+# (|partial sums| <= 16 n <= 128: exact in f32, f16 and bf16), so a transport
+# fault (lost, duplicated, misplaced or stale data) shows as a mismatch
+# whatever algorithm ran.  Rank r's element i is LUT_r[g(i)] with g a 32-bit
+# avalanche hash of the global index (no period a misplaced block could hide
+# in) and LUT_r[v] = ((v + 7 r) & 31) - 16; the expected reduction is
+# LUT_sum[g(i)] — one gather per element, sliced so 4 GiB buckets need no
+# 4 GiB temporaries.
+_SLICE = 1 << 26
+_TDT = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16}
+_CODE = {"f32": nccl.ncclFloat32, "f16": nccl.ncclFloat16, "bf16": nccl.ncclBfloat16}
 
 
-def _allreduce_check_one(dist, comm, rank, world, nbytes):
+def _hash32(lo, hi, device="cuda"):
+    """5-bit digest of a 32-bit avalanche hash (murmur3 finaliser) of every
+    index in [lo, hi), computed in int64 with explicit 32-bit wrap."""
+    m = 0xFFFFFFFF
+    h = torch.arange(lo, hi, device=device, dtype=torch.int64) & m
+    h = (h * 0x9E3779B1) & m
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & m
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & m
+    h = h ^ (h >> 16)
+    return h & 31
+
+
+def _luts(world):
+    v = torch.arange(32, device="cuda")
+    per = [((v + 7 * r) & 31) - 16 for r in range(world)]
+    return per, sum(per)
+
+
+def pattern_fill(buf, r, world, base=0):
+    """Fill the 1-D tensor `buf` with rank r's pattern for global indices
+    [base, base + numel)."""
+    per, _ = _luts(world)
+    n = buf.numel()
+    for lo in range(0, n, _SLICE):
+        hi = min(n, lo + _SLICE)
+        buf[lo:hi] = per[r][_hash32(base + lo, base + hi)].to(buf.dtype)
+
+
+def pattern_ok(buf, world, base=0):
+    """buf == the reduction of every rank's pattern over [base, base + numel)."""
+    _, tot = _luts(world)
+    n = buf.numel()
+    for lo in range(0, n, _SLICE):
+        hi = min(n, lo + _SLICE)
+        if not torch.equal(buf[lo:hi], tot[_hash32(base + lo, base + hi)].to(buf.dtype)):
+            return False
+    return True
+
+
+def _all_ok(dist, ok):
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def check_ar(dist, comm, rank, world, nbytes, dtype="f32", algo=None):
+    """One all-reduce of `nbytes` (out of place) on the path `algo` (None =
+    the library's choice) with pattern inputs; True on every rank iff every
+    rank's output is exact and no spin timed out."""
+    tdt = _TDT[dtype]
+    n = max(1, nbytes // torch.tensor([], dtype=tdt).element_size())
+    x = torch.empty(n, dtype=tdt, device="cuda")
+    y = torch.full((n,), float("nan"), dtype=tdt, device="cuda")
+    pattern_fill(x, rank, world)
     sp = torch.cuda.current_stream().cuda_stream
-    n = nbytes // 4
-    ref = torch.zeros(n, device="cuda")
-    mine = None
-    for r in range(world):
-        g = torch.Generator(device="cuda").manual_seed(4242 + r)
-        v = torch.randint(-64, 64, (n,), device="cuda", generator=g).float()
-        ref += v
-        if r == rank:
-            mine = v
-    out = torch.empty_like(ref)
-    comm.all_reduce(mine.data_ptr(), out.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+    comm.set_algo(algo)
+    try:
+        torch.cuda.synchronize()
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), n, _CODE[dtype], nccl.ncclSum, sp)
+        torch.cuda.synchronize()
+    finally:
+        comm.set_algo(None)
+    ok = pattern_ok(y, world) and comm.async_error() == 0
+    del x, y
+    return _all_ok(dist, ok)
+
+
+def check_rs_ag(dist, comm, rank, world, nbytes, dtype="bf16"):
+    """Reduce-scatter of an `nbytes` bucket, then all-gather of the shards back
+    (the ZeRO bucket path of config 4): (rs_ok, ag_ok) on every rank."""
+    tdt = _TDT[dtype]
+    n = nbytes // torch.tensor([], dtype=tdt).element_size()
+    rc = n // world
+    x = torch.empty(rc * world, dtype=tdt, device="cuda")
+    pattern_fill(x, rank, world)
+    shard = torch.full((rc,), float("nan"), dtype=tdt, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
     torch.cuda.synchronize()
-    ok = torch.tensor([1 if torch.equal(out, ref) and comm.async_error() == 0 else 0])
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    return bool(ok.item())
+    comm.reduce_scatter(x.data_ptr(), shard.data_ptr(), rc, _CODE[dtype], nccl.ncclSum, sp)
+    torch.cuda.synchronize()
+    rs_ok = pattern_ok(shard, world, base=rank * rc) and comm.async_error() == 0
+    x.fill_(float("nan"))  # reuse as the all-gather output
+    comm.all_gather(shard.data_ptr(), x.data_ptr(), rc, _CODE[dtype], sp)
+    torch.cuda.synchronize()
+    ag_ok = pattern_ok(x, world) and comm.async_error() == 0
+    del x, shard
+    torch.cuda.empty_cache()
+    return _all_ok(dist, rs_ok), _all_ok(dist, ag_ok)
+
+
+def check_group(dist, comm, rank, world, nbytes, k):
+    """k all-reduces of `nbytes` in one ncclGroupStart/End (fused LL launches)."""
+    n = nbytes // 4
+    xs = [torch.empty(n, device="cuda") for _ in range(k)]
+    ys = [torch.full((n,), float("nan"), device="cuda") for _ in range(k)]
+    for j, x in enumerate(xs):
+        pattern_fill(x, rank, world, base=j << 24)
+    sp = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    nccl.group_start()
+    for x, y in zip(xs, ys):
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+    nccl.group_end()
+    torch.cuda.synchronize()
+    ok = all(pattern_ok(y, world, base=j << 24) for j, y in enumerate(ys))
+    return _all_ok(dist, ok and comm.async_error() == 0)
+
+
+def run_checks(dist, comm, rank, world, plan):
+    """Run every check of `plan` ({name: (kind, args)}) with the fences off
+    (the default) and again with system-scope fences on (vcclCommSetFences,
+    the VCCL_FENCES=1 path); returns {"fences_off": {...}, "fences_on": {...}}."""
+    res = {}
+    for mode, fences in (("fences_off", False), ("fences_on", True)):
+        comm.set_fences(fences)
+        r = {}
+        for name, (kind, kw) in plan.items():
+            try:
+                if kind == "ar":
+                    r[name] = check_ar(dist, comm, rank, world, **kw)
+                elif kind == "group":
+                    r[name] = check_group(dist, comm, rank, world, **kw)
+                else:
+                    rs_ok, ag_ok = check_rs_ag(dist, comm, rank, world, **kw)
+                    r[name + "_rs"], r[name + "_ag"] = rs_ok, ag_ok
+            except Exception as e:  # noqa: BLE001 - a failed check is a verdict, not a crash
+                r[name] = f"error: {e!r}"
+        res[mode] = r
+    comm.set_fences(False)
+    return res
+
+
+def initall_check(world_devices, timeout=240):
+    """Single-process ncclCommInitAll over every visible GPU (the reference
+    test-harness shape; peer access instead of IPC), run in a
+    child process (tests/mp_initall_worker.py) so a fault there cannot take the
+    bench line with it.  Returns the worker's JSON verdict."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "mp_initall_worker.py"), str(world_devices)]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
+                           env={**os.environ, "VCCL_SPIN_TIMEOUT_S": "30"})
+    except subprocess.TimeoutExpired:
+        return {"ok": False, "error": f"timeout {timeout} s"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"ok": False, "rc": p.returncode, "error": (p.stderr or p.stdout)[-400:]}
+    return json.loads(lines[-1])
+
+
+def _flatten_ok(checks):
+    vals = [v for m in checks.values() for v in m.values()]
+    return all(v is True for v in vals)
 
 
 def bench_allreduce(args):
+    t_line = time.perf_counter()
     dist, rank, world, comm = _dist_setup()
     sp = torch.cuda.current_stream().cuda_stream
     xgmi = peer_copy_bench(dist, rank, world) if not args.no_peer else None
-    correct = allreduce_check(dist, comm, rank, world)
     sizes = [1 << p for p in range(3, 31)] if args.sweep else [args.bytes or (1 << 30)]
     rows = []
     for S in sizes:
@@ -384,15 +564,42 @@ def bench_allreduce(args):
         busbw = algbw * 2 * (world - 1) / world
         rows.append({"bytes": n * 4, "us": dt / steps * 1e6, "algbw": algbw, "busbw": busbw,
                      "algo": comm.coll_algo(0, n, nccl.ncclFloat32)})
+        del x, y
         if rank == 0 and args.sweep:
             print(f"# allreduce {n*4:>12d} B  {dt/steps*1e6:10.1f} us  algbw {algbw:8.2f}  "
                   f"busbw {busbw:8.2f} GB/s  {rows[-1]['algo']}", file=sys.stderr, flush=True)
     extras = None if args.sweep or args.no_extras else bench_extras(dist, comm, rank, world, args)
+    # Correctness of everything timed above, on this topology (fences off and on).
+    t_chk = time.perf_counter()
+    head = rows[-1]["bytes"]
+    plan = {f"ar_default_{head}": ("ar", {"nbytes": head})}
+    if not args.sweep and not args.no_extras:
+        for S in EXTRA_F32_SIZES:
+            plan[f"ar_default_{S}"] = ("ar", {"nbytes": S})
+        for S in EXTRA_F16_SIZES:
+            plan[f"ar_f16_{S}"] = ("ar", {"nbytes": S, "dtype": "f16"})
+        for algo in ("ring", "direct"):
+            for S in (64 << 20, head):
+                plan[f"ar_{algo}_{S}"] = ("ar", {"nbytes": S, "algo": algo})
+        for S in EXTRA_GROUP_SIZES:
+            plan[f"group16_{S}"] = ("group", {"nbytes": S, "k": 16})
+        plan[f"rs_ag_bf16_{args.rs_ag_bytes}"] = ("rs_ag", {"nbytes": args.rs_ag_bytes})
+    checks = run_checks(dist, comm, rank, world, plan)
     err = comm.async_error()
     comm.destroy()
+    initall = None
+    if not args.no_initall and world > 1 and torch.cuda.device_count() > 1:
+        # one process drives every GPU while the other ranks wait at the barrier
+        initall = initall_check(torch.cuda.device_count()) if rank == 0 else None
+        dist.barrier()
+    t_chk = time.perf_counter() - t_chk
+    line_s = time.perf_counter() - t_line
     last = rows[-1]
     links = {2: 1, 4: 3, 8: 7}.get(world, 1)
-    peak = links * XGMI_LINK_GBS
+    measured_link = (xgmi or {}).get("one_peer_GBs")
+    per_link = measured_link if measured_link else XGMI_LINK_GBS
+    peak = links * per_link
+    correct_all = _flatten_ok(checks) and (initall is None or initall.get("ok") is True)
     out = {"metric": "device reduce-copy GB/s vs HBM peak; all-reduce busbw at 1/2/4/8 GPUs",
            "value": round(last["busbw"] * world, 2), "unit": "GB/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(last["us"] / 1e3, 4),
@@ -403,17 +610,29 @@ def bench_allreduce(args):
                       "algorithm": last["algo"],
                       "bytes_per_rank": last["bytes"], "busbw_per_rank": round(last["busbw"], 2),
                       "algbw": round(last["algbw"], 2), "parallelism": f"{last['algo']} x{world}",
-                      "async_error": err, "correct": correct},
-           "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": peak,
+                      "async_error": err, "correct": correct_all},
+           "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": round(peak, 2),
                         "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
-                        "note": f"per-rank busbw vs {links} links x {XGMI_LINK_GBS} GB/s/direction (spec)",
-                        "measured_peer_copy": xgmi}}
+                        "note": (f"per-rank busbw vs {links} links x {per_link:.1f} GB/s per link and "
+                                 "direction, " + ("measured (one-peer copy below)" if measured_link
+                                                 else f"spec {XGMI_LINK_GBS} GB/s (no measurement)")),
+                        "spec_peak": round(links * XGMI_LINK_GBS, 2),
+                        "measured_peer_copy": xgmi},
+           "correct": {"all": correct_all, **checks, "initall_single_process": initall,
+                       "check_s": round(t_chk, 2), "line_s": round(line_s, 2),
+                       "check_frac": round(t_chk / line_s, 3),
+                       "inputs": "integer-valued pattern (exact in any fold order), per timed path"}}
     if extras is not None:
         out["extras"] = extras
     if args.sweep:
         out["sweep"] = [{k: round(v, 3) if isinstance(v, float) else v for k, v in r.items()} for r in rows]
     dist.destroy_process_group()
     return out if rank == 0 else None
+
+
+EXTRA_F32_SIZES = (8, 1 << 10, 8 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20)
+EXTRA_F16_SIZES = (8, 1 << 10, 16 << 10, 128 << 10)
+EXTRA_GROUP_SIZES = (4 << 10, 32 << 10)
 
 
 def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
@@ -458,19 +677,20 @@ def _group_row(dist, comm, rank, world, S, k, steps=20, warmup=3):
 
 def bench_extras(dist, comm, rank, world, args):
     """Secondary BASELINE configs measured in the same multi-GPU run (reported
-    beside the headline, never as ``value``): config 3 at a few sizes (fp32,
-    SIMPLE ring and LL), config 5 (fp16, LL sizes) and config 4 (RS + AG bf16,
-    4 GiB bucket).  Each part records its own error instead of aborting."""
+    beside the headline, never as ``value``): config 3 at a few sizes (fp32),
+    config 5 (fp16, LL sizes), the ring and the direct algorithm each forced,
+    group aggregation, and config 4 (RS + AG bf16, 4 GiB bucket).  Each part
+    records its own error instead of aborting; run_checks verifies each."""
     ex = {}
     try:
         ex["allreduce_f32_sizes"] = [_ar_size_row(dist, comm, rank, world, S, "f32", 20, 5)
-                                     for S in (8, 1 << 10, 8 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20)]
+                                     for S in EXTRA_F32_SIZES]
         ex["allreduce_f16_ll"] = [_ar_size_row(dist, comm, rank, world, S, "f16", 50, 5)
-                                  for S in (8, 1 << 10, 16 << 10, 128 << 10)]
+                                  for S in EXTRA_F16_SIZES]
     except Exception as e:  # noqa: BLE001 - reported, not fatal to the headline
         ex["allreduce_error"] = repr(e)
     try:
-        ex["group_fusion_f32"] = [_group_row(dist, comm, rank, world, S, 16) for S in (4 << 10, 32 << 10)]
+        ex["group_fusion_f32"] = [_group_row(dist, comm, rank, world, S, 16) for S in EXTRA_GROUP_SIZES]
     except Exception as e:  # noqa: BLE001
         ex["group_error"] = repr(e)
     try:  # each algorithm forced at two bucket sizes (vcclCommSetAlgo): the SIMPLE
@@ -514,13 +734,16 @@ def _rs_ag(dist, comm, rank, world, S, steps, warmup):
     torch.cuda.empty_cache()
     return {"bytes": S, "steps": steps, "rs_busbw": round(S * steps / t_rs / 1e9 * frac, 2),
             "ag_busbw": round(S * steps / t_ag / 1e9 * frac, 2),
-            "ms_per_rs_ag": round((t_rs + t_ag) / steps * 1e3, 3)}
+            "ms_per_rs_ag": round((t_rs + t_ag) / steps * 1e3, 3),
+            "algo_rs": comm.coll_algo(1, rc, nccl.ncclBfloat16),
+            "algo_ag": comm.coll_algo(2, rc, nccl.ncclBfloat16)}
 
 
 def bench_rs_ag(args):
     """BASELINE config 4: reduce-scatter + all-gather bf16 bucket."""
     dist, rank, world, comm = _dist_setup()
     r = _rs_ag(dist, comm, rank, world, args.bytes or (4 << 30), args.steps, args.warmup)
+    rs_ok, ag_ok = check_rs_ag(dist, comm, rank, world, args.bytes or (4 << 30))
     comm.destroy()
     dist.destroy_process_group()
     if rank:
@@ -531,7 +754,7 @@ def bench_rs_ag(args):
             "ms_per_step": r["ms_per_rs_ag"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"workload": f"RS+AG bf16 {r['bytes']} B bucket", "rs_busbw": r["rs_busbw"],
-                       "ag_busbw": r["ag_busbw"]}}
+                       "ag_busbw": r["ag_busbw"], "correct": {"rs": rs_ok, "ag": ag_ok}}}
 
 
 def main():
@@ -545,12 +768,14 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-peer", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-initall", action="store_true")
     ap.add_argument("--rs-ag-bytes", type=int, default=4 << 30)
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--nt-loads", type=int, default=0)
     ap.add_argument("--nt-stores", type=int, default=0)
+    ap.add_argument("--preroll-s", type=float, default=0.5)
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     workload = args.workload or ("reduce_copy" if world == 1 else "allreduce")

@@ -8,9 +8,12 @@
  * `ncclX` and as the profiling alias `pncclX` (reference: src/include/core.h:18-31).
  *
  * Scope: AllReduce / ReduceScatter / AllGather over the
- * repo's own ring (xGMI peer memory, no RCCL) and the comm lifecycle they need.
- * Calls outside that scope (Broadcast, Reduce, Send/Recv, Split, Register, ...)
- * are declared for ABI completeness and return ncclInvalidUsage.
+ * repo's own transport (xGMI peer memory, no RCCL) and the comm lifecycle they
+ * need.  The calls of the "out of scope" block at the end (Reduce, Bcast,
+ * Broadcast, Send, Recv, CommSplit) are declared and exported so a binary
+ * linked against libnccl still loads; each logs a WARN and returns
+ * ncclInvalidUsage.  Other reference entry points (Register, MemAlloc,
+ * InitRankScalable, ...) are not exported.
  */
 #ifndef VCCL_NCCL_H_
 #define VCCL_NCCL_H_
@@ -171,6 +174,36 @@ ncclResult_t  ncclGroupStart(void);
 ncclResult_t pncclGroupStart(void);
 ncclResult_t  ncclGroupEnd(void);
 ncclResult_t pncclGroupEnd(void);
+
+/* ---- out of scope: WARN + ncclInvalidUsage ---- */
+/* nccl.h.in:312-315 */
+ncclResult_t  ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
+/* nccl.h.in:326-329 */
+ncclResult_t  ncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root,
+    ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root,
+    ncclComm_t comm, hipStream_t stream);
+/* nccl.h.in:340-343 */
+ncclResult_t  ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    int root, ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    int root, ncclComm_t comm, hipStream_t stream);
+/* nccl.h.in:403-406 */
+ncclResult_t  ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer,
+    ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer,
+    ncclComm_t comm, hipStream_t stream);
+/* nccl.h.in:420-423 */
+ncclResult_t  ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int peer,
+    ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int peer,
+    ncclComm_t comm, hipStream_t stream);
+/* nccl.h.in:173-174 */
+ncclResult_t  ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
+ncclResult_t pncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
 
 #ifdef __cplusplus
 }  /* extern "C" */

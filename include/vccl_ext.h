@@ -23,6 +23,26 @@
  *                     VCCL_NET_FORCE=1) through host-pinned staging buffers
  *                     and TCP, as the reference's proxy + net transport
  *                     (src/proxy.cc:914-971, src/transport/net.cc:1293-1482).
+ *   vcclCommSetFences  switch the system-scope acquire/release fences around
+ *                     every FIFO slot / inbox hand-off on (1) or off (0, the
+ *                     default: write-through sc0 sc1 payload accesses need no
+ *                     fence) — the VCCL_FENCES=1 safety valve at run time, so
+ *                     one process can check a transport both ways.  Blocks
+ *                     until the device is idle; call with no collective of
+ *                     this communicator in flight.
+ *   vcclCommDebugSetEpochs  overwrite the device-resident call epochs of the
+ *                     one-shot LL and two-shot direct paths (tests of the
+ *                     32-bit wrap; the reference's TEST_LL_CLEANUP knob,
+ *                     src/include/device.h:70-77, serves the same purpose).
+ *                     Every rank must set the same values between calls.
+ *   vcclRingPartition  the channel partition the ring algorithm uses for a
+ *                     call (host only): VCCL's cbd split and chunking
+ *                     (scheduleCollTasksToPlan, src/enqueue.cc:518-644, for a
+ *                     plan of one collective) for `nChannels` channels and a
+ *                     FIFO slot of `slotBytes` (NCCL_BUFFSIZE / 8).  out[0..7]
+ *                     = channelLo, channelHi, countLo, countMid, countHi,
+ *                     chunkLo, chunkMid, chunkHi (elements; bytes for
+ *                     all-gather, which the reference runs as int8).
  */
 #ifndef VCCL_EXT_H_
 #define VCCL_EXT_H_
@@ -50,6 +70,10 @@ ncclResult_t vcclCommLaunchStats(ncclComm_t comm, unsigned long long* collective
                                  unsigned long long* fusedLaunches);
 ncclResult_t vcclCommNetStats(ncclComm_t comm, uint64_t* bytesSent, uint64_t* bytesReceived,
                               int* connections);
+ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences);
+ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoch, uint32_t directEpoch);
+ncclResult_t vcclRingPartition(int coll, size_t count, ncclDataType_t datatype, int nRanks,
+                               int nChannels, size_t slotBytes, int64_t* out);
 
 #ifdef __cplusplus
 }

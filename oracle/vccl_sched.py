@@ -1,0 +1,219 @@
+"""ORACLE — test infrastructure only (tests/ may import it; the product never does).
+
+Restatement of VCCL's channel partition and chunking for the RING collectives,
+i.e. which channel (hence which ring) and which chunk of which loop every
+element of an all-reduce / reduce-scatter / all-gather lands in.  With the
+per-channel ring, that fixes the fp fold order of every element, so together
+with the C oracle's ring_fold (oracle/reduce_ref.c) it gives VCCL's exact
+result for a given (ring set, channel count, buffer size).
+
+Followed, for a plan holding one collective (the ncclAllReduce /
+ncclReduceScatter / ncclAllGather call outside a group):
+  * taskAppend: AG counted in bytes as int8 (enqueue.cc:2398-2404);
+    trafficBytes = count * eltSize * trafficPerByte (enqueue.cc:2405,
+    ncclFuncTrafficPerByte enqueue.cc:67-74: AR 2, RS/AG nRanks)
+  * topoGetAlgoInfo ring channel tuning: nc = comm nChannels, decreased while
+    nBytes < nc * nt * threadThreshold (enqueue.cc:1902-1925), nBytes =
+    eltSize * ncclFuncMaxSendRecvCount (enqueue.cc:1955, enqueue.h:36-38),
+    nt = maxThreads[RING][proto] (tuning.cc:198-211: SIMPLE 512 unless the ring
+    is PCI-bound, LL 512, LL128 640), threadThreshold SIMPLE 64 / LL 8 * nRanks
+    / LL128 8 (comm.h:38-40, tuning.cc:489-493)
+  * scheduleCollTasksToPlan, the cbd cell split (enqueue.cc:518-565, 597-644)
+  * calcCollChunking for RING (enqueue.cc:1983-2093): chunkSize = stepSize *
+    chunkSteps (SIMPLE ring: 4 steps of buffSize/8, collectives.h:16-22), LL
+    halves it, LL128 keeps 15/16, rounded down to the protocol grain
+    (device.h:290-295: SIMPLE 512 B, LL 16 B, LL128 1920 B)
+  * ncclCollCbdPart (device.h:297-323) and the per-loop chunk layout of
+    runRing all-reduce with the short last loop's alignUp(divUp(rem, nranks),
+    16/sizeof(T)) (all_reduce.h:32-47), reduce-scatter (reduce_scatter.h:33-36)
+    and all-gather (all_gather.h:43-46).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+PROTO_LL, PROTO_LL128, PROTO_SIMPLE = 0, 1, 2   # nccl_common.h protocol ids
+NCCL_STEPS = 8                                   # device.h:24
+MIN_TRAFFIC_PER_CHANNEL = 16 << 10               # enqueue.cc:528
+DEFAULT_BUFFSIZE = {PROTO_LL: 8 * 512 * NCCL_STEPS * 16,        # init.cc:617
+                    PROTO_LL128: 120 * 640 * NCCL_STEPS * 8,    # init.cc:618
+                    PROTO_SIMPLE: 1 << 22}                      # init.cc:619
+MAX_THREADS = {PROTO_LL: 512, PROTO_LL128: 640, PROTO_SIMPLE: 512}
+THREAD_THRESHOLD = {PROTO_LL: 8, PROTO_LL128: 8, PROTO_SIMPLE: 64}
+CHUNK_STEPS = 4                                  # ALLREDUCE/REDUCESCATTER/ALLGATHER_CHUNKSTEPS
+LL128_LINEELEMS, LL128_DATAELEMS = 16, 15        # device.h:81-83
+
+
+def grain_size(proto):
+    """ncclProtoGrainSize (device.h:290-295); LL128 = 32 * 16 / 16 * 15 * 8."""
+    return {PROTO_LL: 16, PROTO_LL128: 1920, PROTO_SIMPLE: 512}[proto]
+
+
+def _div_up(x, y):
+    return (x + y - 1) // y
+
+
+def _align_up(x, a):
+    return _div_up(x, a) * a
+
+
+@dataclass
+class CbdWork:
+    """ncclDevWorkColl.cbd + channel range (device.h:258-287)."""
+    channel_lo: int
+    channel_hi: int
+    count_lo: int
+    count_mid: int
+    count_hi: int
+    chunk_grains_lo: int
+    chunk_grains_mid: int
+    chunk_grains_hi: int
+    proto: int
+    elt_size: int
+
+    def part(self, channel):
+        """ncclCollCbdPart: (partOffset, partCount, chunkCount) in elements."""
+        per_grain = grain_size(self.proto) // self.elt_size
+        n_mid = self.channel_hi - self.channel_lo - 1
+        if channel == self.channel_lo:
+            return 0, self.count_lo, self.chunk_grains_lo * per_grain
+        if channel == self.channel_hi:
+            return (self.count_lo + n_mid * self.count_mid, self.count_hi,
+                    self.chunk_grains_hi * per_grain)
+        mid = channel - self.channel_lo - 1
+        return self.count_lo + mid * self.count_mid, self.count_mid, self.chunk_grains_mid * per_grain
+
+
+def traffic_per_byte(coll, nranks):
+    return 2 if coll == "ar" else nranks
+
+
+def max_send_recv_count(coll, nranks, count):
+    return nranks * count if coll in ("ag", "rs") else count
+
+
+def chunk_size(proto, buff_size=None):
+    """calcCollChunking for the RING algorithm (enqueue.cc:2027-2032, 2093)."""
+    buff = DEFAULT_BUFFSIZE[proto] if buff_size is None else buff_size
+    step = buff // NCCL_STEPS
+    cs = step * (CHUNK_STEPS if proto == PROTO_SIMPLE else 1)
+    if proto == PROTO_LL:
+        cs //= 2
+    if proto == PROTO_LL128:
+        cs = cs // LL128_LINEELEMS * LL128_DATAELEMS
+    g = grain_size(proto)
+    return cs // g * g
+
+
+def ring_n_max_channels(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPLE,
+                        nthreads=None):
+    """topoGetAlgoInfo's ring channel count for this call (enqueue.cc:1902-1925)."""
+    nbytes = elt_size * max_send_recv_count(coll, nranks, count)
+    nt = MAX_THREADS[proto] if nthreads is None else nthreads
+    thr = THREAD_THRESHOLD[proto] * (nranks if proto == PROTO_LL else 1)
+    nc = comm_channels
+    while nbytes < nc * nt * thr:
+        if nc >= 2:
+            nc -= 1
+        else:
+            break
+    return nc
+
+
+def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPLE,
+                 buff_size=None, nthreads=None) -> CbdWork:
+    """scheduleCollTasksToPlan for a plan of one ring collective.
+
+    coll: "ar" | "rs" | "ag"; count: AR count, RS recvcount, AG sendcount (in
+    elements of elt_size; AG is rewritten to bytes here as taskAppend does)."""
+    if coll == "ag":
+        count, elt_size = count * elt_size, 1
+    tpb = traffic_per_byte(coll, nranks)
+    task_traffic = count * elt_size * tpb
+    n_task_ch = ring_n_max_channels(coll, count, elt_size, nranks, comm_channels, proto, nthreads)
+    traffic = max(MIN_TRAFFIC_PER_CHANNEL, task_traffic)
+    n_ch = min(n_task_ch, comm_channels)
+    n_max = comm_channels
+    traffic_per_channel = max(MIN_TRAFFIC_PER_CHANNEL, traffic // n_ch)
+    channel_id, current_traffic = 0, 0
+    if proto == PROTO_LL:
+        tpb *= 4
+    cell_size = _div_up(_div_up(MIN_TRAFFIC_PER_CHANNEL, tpb), 16) * 16
+    elements_per_cell = cell_size // elt_size
+    cells = _div_up(count * elt_size, cell_size)
+    traffic_per_cell = cell_size * tpb
+    cells_per_channel = min(cells, _div_up(traffic_per_channel, traffic_per_cell))
+    if channel_id + 1 == n_max:
+        cells_lo = cells
+    else:
+        cells_lo = min(cells, _div_up(traffic_per_channel - current_traffic, traffic_per_cell))
+    n_mid = (cells - cells_lo) // cells_per_channel
+    cells_hi = (cells - cells_lo) % cells_per_channel
+    n_channels = (1 if cells_lo else 0) + n_mid + (1 if cells_hi else 0)
+    if n_max < channel_id + n_channels:
+        n_mid = n_max - channel_id - 2
+        cells_per_channel = (cells - cells_lo) // (n_mid + 1)
+        cells_hi = cells_per_channel + (cells - cells_lo) % (n_mid + 1)
+    if cells_hi == 0 and n_mid != 0:
+        cells_hi = cells_per_channel
+        n_mid -= 1
+    if cells_lo == 0:
+        channel_id += 1
+        if n_mid == 0:
+            cells_lo, cells_hi = cells_hi, 0
+        else:
+            cells_lo = cells_per_channel
+            n_mid -= 1
+    count_mid = cells_per_channel * elements_per_cell if n_mid != 0 else 0
+    count_lo = cells_lo * elements_per_cell
+    count_hi = cells_hi * elements_per_cell
+    excess = cells * elements_per_cell - count
+    if count_hi != 0:
+        count_hi -= excess
+    else:
+        count_lo -= excess
+    n_channels = (1 if count_lo else 0) + n_mid + (1 if cells_hi else 0)
+    g = grain_size(proto)
+    cs = chunk_size(proto, buff_size)  # ring: independent of nBytes (enqueue.cc:2034-2082)
+    grains = cs // g
+    return CbdWork(channel_id, channel_id + n_channels - 1, count_lo, count_mid, count_hi,
+                   grains if count_lo else 0, grains if n_mid else 0, grains if count_hi else 0,
+                   proto, elt_size)
+
+
+def allreduce_owner(work: CbdWork, count, nranks):
+    """Per element: (channel, ring index of the rank that finishes it) for the
+    ring all-reduce (all_reduce.h:32-64: chunk k of every loop finishes at
+    ring index k)."""
+    chan = np.full(count, -1, np.int32)
+    owner = np.full(count, -1, np.int32)
+    elt_align = max(1, 16 // work.elt_size)
+    for c in range(work.channel_lo, work.channel_hi + 1):
+        off, length, chunk = work.part(c)
+        loop = nranks * chunk
+        eo = 0
+        while eo < length:
+            rem = length - eo
+            if rem < loop:
+                chunk = _align_up(_div_up(rem, nranks), elt_align)
+            for k in range(nranks):
+                lo = eo + k * chunk
+                hi = min(eo + (k + 1) * chunk, length)
+                if hi > lo:
+                    chan[off + lo:off + hi] = c
+                    owner[off + lo:off + hi] = k
+            eo += loop
+    assert (chan >= 0).all(), "partition does not cover the buffer"
+    return chan, owner
+
+
+def channel_of(work: CbdWork, count):
+    """Per element of a reduce-scatter block / all-gather block: its channel."""
+    chan = np.full(count, -1, np.int32)
+    for c in range(work.channel_lo, work.channel_hi + 1):
+        off, length, _ = work.part(c)
+        chan[off:off + length] = c
+    assert (chan >= 0).all(), "partition does not cover the block"
+    return chan

@@ -1,16 +1,19 @@
 """Test-side restatement of the ring data partition, to compute the exact
 expected result of a ring collective with the CPU oracle.
 
-Mirrors vccl_amd/csrc/host/init.cc (ring_orders, channel count) and
-vccl_amd/csrc/device/ring.hpp (channel_part, the all-reduce round/chunk
-layout of all_reduce.h:32-82).  The oracle's ring_fold then reproduces the
-fold order element by element, so multi-rank fp results are checked
-bit-exactly against OUR partition, and with the §8c tolerance against any
-other partition (e.g. the reference's, which differs).
+The ring's element -> (channel, chunk) partition is VCCL's own (the device
+follows it, host/enqueue.cc cbd_schedule; the tests take it from the oracle's
+independent restatement, oracle/vccl_sched.py); the ring set per channel and
+the channel count mirror vccl_amd/csrc/host/init.cc.  The oracle's ring_fold
+then reproduces the fold order element by element, so ring results are
+checked bit-exactly against VCCL's schedule on the same rings and channels,
+and the one-shot LL / two-shot direct paths (own fold orders) bit-exactly
+against their own order and within the §8c tolerance of VCCL's.
 """
 import numpy as np
 
 from oracle import oracle as O
+from oracle import vccl_sched as S
 
 RINGS = {
     8: [[0, 1, 2, 3, 4, 5, 6, 7], [0, 2, 1, 3, 5, 4, 7, 6], [0, 3, 1, 4, 6, 2, 7, 5],
@@ -41,47 +44,21 @@ def _div_up(x, a):
     return (x + a - 1) // a
 
 
-def channel_part(count, nch, c, elt_align):
-    per = _align_up(_div_up(count, nch), elt_align)
-    lo = min(per * c, count)
-    hi = min(per * (c + 1), count)
-    return lo, hi - lo
-
-
-def allreduce_owner(count, n, nch, slot_bytes, elt_size):
-    """(channel, owner ring position) per element for the ring all-reduce."""
-    elt_align = max(1, 16 // elt_size)
-    chan = np.zeros(count, np.int32)
-    owner = np.zeros(count, np.int32)
-    for c in range(nch):
-        off, length = channel_part(count, nch, c, elt_align)
-        chunk = slot_bytes // elt_size
-        loop = n * chunk
-        eo = 0
-        while eo < length:
-            rem = length - eo
-            if rem < loop:
-                chunk = _align_up(_div_up(rem, n), elt_align)
-            for k in range(n):
-                lo = eo + k * chunk
-                hi = min(eo + (k + 1) * chunk, length)
-                if hi > lo:
-                    chan[off + lo:off + hi] = c
-                    owner[off + lo:off + hi] = k
-            eo += loop
-    return chan, owner
-
-
-def expected_allreduce(op, dtype, inputs, nch, slot_bytes):
-    """Exact expected output (identical on every rank)."""
+def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None):
+    """Exact expected ring all-reduce output (identical on every rank): the
+    oracle's restatement of VCCL's channel partition and chunking
+    (oracle/vccl_sched.py) decides channel and finishing ring index per
+    element, channel c runs on rings[c % len(rings)], the C oracle folds."""
     n = len(inputs)
+    rings = rings or ring_orders(n)
     dev_op, arg = O.host_to_dev_redop(op, dtype, n)
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size
-    chan, owner = allreduce_owner(count, n, nch, slot_bytes, inputs[0].dtype.itemsize)
+    esz = inputs[0].dtype.itemsize
+    work = S.cbd_schedule("ar", count, esz, n, nch, buff_size=slot_bytes * S.NCCL_STEPS)
+    chan, owner = S.allreduce_owner(work, count, n)
     out = np.empty_like(inputs[0])
-    rings = ring_orders(n)
-    for c in range(nch):
+    for c in range(work.channel_lo, work.channel_hi + 1):
         idx = np.nonzero(chan == c)[0]
         if idx.size == 0:
             continue
@@ -91,24 +68,28 @@ def expected_allreduce(op, dtype, inputs, nch, slot_bytes):
     return out
 
 
-def expected_reducescatter(op, dtype, inputs, nch):
-    """Per-rank expected outputs; inputs[r] has n*recvcount elements."""
+def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=None):
+    """Per-rank expected outputs; inputs[r] has n*recvcount elements.  Rank
+    r's block is folded on the ring of each element's channel (VCCL's cbd
+    partition of the recvcount block), finishing at r."""
     n = len(inputs)
+    rings = rings or ring_orders(n)
     dev_op, arg = O.host_to_dev_redop(op, dtype, n)
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size // n
-    elt_align = max(1, 16 // inputs[0].dtype.itemsize)
-    rings = ring_orders(n)
+    work = S.cbd_schedule("rs", count, inputs[0].dtype.itemsize, n, nch,
+                          buff_size=slot_bytes * S.NCCL_STEPS)
+    chan = S.channel_of(work, count)
     outs = [np.empty(count, inputs[0].dtype) for _ in range(n)]
-    for c in range(nch):
-        off, length = channel_part(count, nch, c, elt_align)
-        if length == 0:
+    for c in range(work.channel_lo, work.channel_hi + 1):
+        idx = np.nonzero(chan == c)[0]
+        if idx.size == 0:
             continue
         ring = rings[c % len(rings)]
         for r in range(n):
-            ins = [inputs[q][r * count + off:r * count + off + length] for q in ring]
-            own = np.full(length, ring.index(r), np.int32)
-            outs[r][off:off + length] = O.ring_fold(dev_op, dtype, arg, pre, ins, own)
+            ins = [inputs[q][r * count + idx] for q in ring]
+            own = np.full(idx.size, ring.index(r), np.int32)
+            outs[r][idx] = O.ring_fold(dev_op, dtype, arg, pre, ins, own)
     return outs
 
 

@@ -4,7 +4,8 @@
 argv: rank nranks uid_hex
 Captures [LL all-reduce (small), direct all-reduce (mid), ring all-reduce
 (large), ring reduce-scatter]
-into one graph, replays it 4 times with new integer-valued inputs (exact in any
+into one graph on a side stream (after an eager call on the current stream,
+and followed by another), replays it 4 times with new integer-valued inputs (exact in any
 fold order) and checks every output; exit code 0 = all replays correct."""
 import os
 import sys
@@ -31,6 +32,13 @@ def main():
     ys, yl, yr = torch.empty_like(xs), torch.empty_like(xl), torch.empty(rc, device="cuda")
     s = torch.cuda.Stream()
     g = torch.cuda.CUDAGraph()
+    # An eager call on ANOTHER stream right before the capture: the capture
+    # must not wait on (or overwrite) the comm's eager ordering event, which
+    # was recorded outside it (enqueue.cc stream_order / stream_mark).
+    eager_x = torch.arange(4099, device="cuda", dtype=torch.float32) + rank
+    eager_y = torch.empty_like(eager_x)
+    comm.all_reduce(eager_x.data_ptr(), eager_y.data_ptr(), 4099, nccl.ncclFloat32, nccl.ncclSum,
+                    torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     with torch.cuda.graph(g, stream=s):
         sp = s.cuda_stream
@@ -53,6 +61,14 @@ def main():
         ok &= torch.equal(ym, sum(val(r, mid) for r in range(n)))
         ok &= torch.equal(yl, sum(val(r, large) for r in range(n)))
         ok &= torch.equal(yr, sum(val(r, rc * n) for r in range(n))[rank * rc:(rank + 1) * rc])
+    # eager again on the first stream after the replays
+    exp_eager = sum(torch.arange(4099, device="cuda", dtype=torch.float32) + r for r in range(n))
+    ok &= torch.equal(eager_y, exp_eager)
+    eager_y.zero_()
+    comm.all_reduce(eager_x.data_ptr(), eager_y.data_ptr(), 4099, nccl.ncclFloat32, nccl.ncclSum,
+                    torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ok &= torch.equal(eager_y, exp_eager)
     ok &= comm.async_error() == 0
     comm.destroy()
     sys.exit(0 if ok else 4)

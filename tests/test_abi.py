@@ -69,3 +69,36 @@ def test_null_comm_queries():
     assert L.ncclCommCount(None, ctypes.byref(v)) == nccl.ncclInvalidArgument
     assert L.ncclCommDestroy(None) == nccl.ncclSuccess
     assert L.ncclAllReduce(None, None, 1, 7, 0, None, None) == nccl.ncclInvalidArgument
+
+
+def test_out_of_scope_calls_are_invalid_usage():
+    """ncclReduce / Bcast / Broadcast / Send / Recv / CommSplit are exported
+    (include/nccl.h) so a libnccl-linked binary loads, and refuse loudly."""
+    L = nccl.lib()
+    vp = ctypes.c_void_p
+    assert L.ncclReduce(vp(0x10), vp(0x10), ctypes.c_size_t(4), 7, 0, 0, None, None) == nccl.ncclInvalidUsage
+    assert L.ncclBcast(vp(0x10), ctypes.c_size_t(4), 7, 0, None, None) == nccl.ncclInvalidUsage
+    assert L.ncclBroadcast(vp(0x10), vp(0x10), ctypes.c_size_t(4), 7, 0, None, None) == nccl.ncclInvalidUsage
+    assert L.ncclSend(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage
+    assert L.ncclRecv(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage
+    out = vp(0x1234)
+    assert L.ncclCommSplit(None, 0, 0, ctypes.byref(out), None) == nccl.ncclInvalidUsage
+    assert out.value is None
+    assert L.pncclSend(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage
+
+
+def test_group_with_failing_call_launches_nothing():
+    """ncclGroupErrCheck (enqueue.cc:2516) / group.cc:528,591: one invalid call
+    inside a group makes the outermost ncclGroupEnd fail; the next group is clean."""
+    L = nccl.lib()
+    nccl.group_start()
+    assert L.ncclAllReduce(None, None, 1, 7, 0, None, None) == nccl.ncclInvalidArgument
+    assert L.ncclGroupEnd() == nccl.ncclInvalidArgument
+    nccl.group_start()
+    nccl.group_end()
+    # nested: the error surfaces only at the outermost end
+    nccl.group_start()
+    nccl.group_start()
+    assert L.ncclReduceScatter(None, None, 1, 99, 0, None, None) == nccl.ncclInvalidArgument
+    assert L.ncclGroupEnd() == nccl.ncclSuccess
+    assert L.ncclGroupEnd() == nccl.ncclInvalidArgument

@@ -283,3 +283,72 @@ def test_graph_capture_replay():
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
     outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
     assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+
+
+def test_shared_device_ranks_beyond_hw_queues_rejected(monkeypatch):
+    """n ranks of one comm on one GPU in one process need n co-resident
+    kernels; with HIP's 4 hardware queues per process (one taken by the
+    process's own stream) n = 4 would deadlock until the spin timeout
+    (profiles/r01_diag_protocol.log), so init refuses it up front."""
+    monkeypatch.setenv("VCCL_ALLOW_SHARED_DEVICE", "1")
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+    with pytest.raises(nccl.VcclError) as e:
+        nccl.Comm.init_all([0, 0, 0, 0])
+    assert e.value.code == nccl.ncclInvalidUsage
+
+
+def test_epoch_wrap(monkeypatch):
+    """the LL parity and the direct flag values must survive the
+    32-bit epoch wrap (0xffffffff -> 2, never 0, parity alternating).  Epochs
+    seeded just below the wrap on both ranks (vcclCommDebugSetEpochs), then
+    LL and multi-chunk direct all-reduces run across it, integer-exact."""
+    for k, v in TEST_GEOM.items():
+        monkeypatch.setenv(k, v)
+    import bench
+    comms = nccl.Comm.init_all([0, 0])
+    try:
+        for c in comms:
+            c.debug_set_epochs(0xFFFFFFFD, 0xFFFFFFFE)
+        streams = [torch.cuda.Stream() for _ in comms]
+        # LL: 6 calls (epochs ...fffe, ...ffff, 2, 3, 4, 5); direct: 3 MiB
+        # buckets through 1 MiB inbox chunks (3 flag values per call)
+        for it, (nbytes, algo) in enumerate([(40 << 10, "ll")] * 6 + [(3 << 20, "direct")] * 4):
+            n = nbytes // 4
+            xs = [torch.empty(n, device="cuda") for _ in comms]
+            ys = [torch.full((n,), float("nan"), device="cuda") for _ in comms]
+            for r, x in enumerate(xs):
+                bench.pattern_fill(x, r, 2, base=it << 20)
+            for c in comms:
+                c.set_algo(algo)
+            torch.cuda.synchronize()
+            nccl.group_start()
+            for r, c in enumerate(comms):
+                c.all_reduce(xs[r].data_ptr(), ys[r].data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum,
+                             streams[r].cuda_stream)
+            nccl.group_end()
+            torch.cuda.synchronize()
+            for r, c in enumerate(comms):
+                assert c.async_error() == 0, f"call {it} ({algo}): spin timeout"
+                assert bench.pattern_ok(ys[r], 2, base=it << 20), f"call {it} ({algo}) rank {r}"
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_initall_single_process_worker():
+    """tests/mp_initall_worker.py (run by bench.py on multi-GPU boxes): one
+    process, ncclCommInitAll, LL / default / ring all-reduce and RS + AG in
+    groups.  On a one-GPU box it rehearses with two ranks on device 0; with
+    more GPUs it runs over every GPU (peer access, no IPC)."""
+    ndev = torch.cuda.device_count()
+    arg = str(ndev) if ndev > 1 else "0,0"
+    env = dict(os.environ)
+    if ndev == 1:
+        env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mp_initall_worker.py"), arg],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    import json
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["ok"], res

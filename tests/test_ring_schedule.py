@@ -1,5 +1,6 @@
-"""CPU step-simulation of the device ring schedules (ring.hpp) against the
-owner-map restatement (tests/_ring.py).  Two independent derivations of the
+"""CPU step-simulation of the device ring schedules (ring.hpp: cbd part per
+channel, chunk steps sliced into FIFO slots) against the owner-map
+restatement of VCCL's runRing (oracle/vccl_sched.py via tests/_ring.py).  Two independent derivations of the
 same fold order must agree bit-exactly, at n = 2..8, ragged counts and tiny
 slots (many rounds, empty chunks in the last round).  Also checks the ring
 sets: arc-disjoint for 8, every arc twice for 4."""
@@ -10,6 +11,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from oracle import vccl_sched as S
 from tests import _ring
 from tests._util import assert_bitexact
 
@@ -20,11 +22,14 @@ def _align_up(x, a):
     return (x + a - 1) // a * a
 
 
-def _prims_allreduce(n, pos, count, nch, c, slot_elems, elt_align):
-    """Yield (recv, send, src_off, dst_off, nelem, post) for one rank/channel,
-    exactly as ring_allreduce() in ring.hpp."""
-    goff, chcount = _ring.channel_part(count, nch, c, elt_align)
-    chunk = slot_elems
+def _prims_allreduce(n, pos, work, c, slot_elems, elt_align):
+    """Yield (recv, send, src_off, dst_off, nelem, post) slot transfers for one
+    rank/channel, exactly as ring_allreduce() / ring_step() in ring.hpp: the
+    channel's cbd part and chunk (VCCL's partition), each chunk step cut into
+    slot-sized slices (an empty step still moves one empty slot)."""
+    if not work.channel_lo <= c <= work.channel_hi:
+        return
+    goff, chcount, chunk = work.part(c)
     loop = n * chunk
     eo = 0
     while eo < chcount:
@@ -33,18 +38,21 @@ def _prims_allreduce(n, pos, count, nch, c, slot_elems, elt_align):
             chunk = _align_up(-(-rem // n), elt_align)
         off = lambda k: goff + eo + k * chunk  # noqa: E731
         ln = lambda k: max(0, min(chunk, rem - k * chunk))  # noqa: E731
-        k = (pos + n - 1) % n
-        yield (False, True, off(k), None, ln(k), False)
+
+        def step(recv, send, k, src, dst, post):
+            total = ln(k)
+            nsl = max(1, -(-total // slot_elems))
+            for s_ in range(nsl):
+                o = s_ * slot_elems
+                ne = max(0, min(slot_elems, total - o))
+                yield (recv, send, off(k) + o if src else None, off(k) + o if dst else None, ne, post)
+        yield from step(False, True, (pos + n - 1) % n, True, False, False)
         for j in range(2, n):
-            k = (pos + n - j) % n
-            yield (True, True, off(k), None, ln(k), False)
-        k = pos
-        yield (True, True, off(k), off(k), ln(k), True)
+            yield from step(True, True, (pos + n - j) % n, True, False, False)
+        yield from step(True, True, pos, True, True, True)
         for j in range(1, n - 1):
-            k = (pos + n - j) % n
-            yield (True, True, None, off(k), ln(k), False)
-        k = (pos + 1) % n
-        yield (True, False, None, off(k), ln(k), False)
+            yield from step(True, True, (pos + n - j) % n, False, True, False)
+        yield from step(True, False, (pos + 1) % n, False, True, False)
         eo += loop
 
 
@@ -55,9 +63,10 @@ def _simulate_allreduce(op, dt, inputs, nch, slot_bytes):
     elt_align = max(1, 16 // esz)
     rings = _ring.ring_orders(n)
     outs = [np.zeros_like(inputs[0]) for _ in range(n)]
+    work = S.cbd_schedule("ar", inputs[0].size, esz, n, nch, buff_size=slot_bytes * S.NCCL_STEPS)
     for c in range(nch):
         ring = rings[c % len(rings)]
-        progs = {r: list(_prims_allreduce(n, ring.index(r), inputs[0].size, nch, c,
+        progs = {r: list(_prims_allreduce(n, ring.index(r), work, c,
                                           slot_bytes // esz, elt_align)) for r in range(n)}
         fifo = {r: deque() for r in range(n)}  # fifo[r]: slots arriving at r
         pc = {r: 0 for r in range(n)}
@@ -97,14 +106,14 @@ def _simulate_allreduce(op, dt, inputs, nch, slot_bytes):
 @pytest.mark.parametrize("dt,op", [(7, 0), (9, 0), (6, 4), (2, 4), (7, 1)])
 def test_simulated_schedule_matches_owner_map(n, dt, op):
     rng = np.random.default_rng(n * 10 + dt)
-    count = 1000 + 37 * n
+    count = 150_000 + 37 * n  # several loops per channel, a short last loop
     if dt == 9:
         ins = [O.f32_to_bf16_bits(rng.uniform(-1, 1, count).astype(np.float32)) for _ in range(n)]
     elif dt == 2:
         ins = [rng.integers(-1000, 1000, count).astype(np.int32) for _ in range(n)]
     else:
         ins = [rng.uniform(-1, 1, count).astype(O.NP_DTYPE[dt]) for _ in range(n)]
-    slot = 64  # bytes: many rounds and a short last round
+    slot = 4096  # bytes: chunk = 4 slots = 16 KiB, sliced back into slots
     nch = 3
     sim = _simulate_allreduce(op, dt, ins, nch, slot)
     exp = _ring.expected_allreduce(op, dt, ins, nch, slot)

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session (run through gpurun from the repo root):
+#   tools/gpu_run.sh <label> <step> [<step> ...]
+# steps: test      pytest -m gpu (one process, per-test timeout)
+#        test:<k>  pytest -m gpu -k <k>
+#        bench     bench.py at N=1 (the driver's default invocation)
+#        prof      rocprofv3 --kernel-trace --stats of bench.py (no CPU leg)
+#        n2        bench.py N>1 rehearsal: 2 ranks sharing the one GPU
+#        smoke     __graft_entry__.smoke()
+#        py:<file> python <file> (a tool script)
+# Outputs go to gpurun_out/<label>/.  Every GPU step has its own time limit
+# and the chain stops at the first failure (no retries).
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+L=$1; shift
+O=$R/gpurun_out/$L; mkdir -p $O
+cd $R
+export TMPDIR=/tmp
+for s in "$@"; do
+  echo "== $s $(date +%T)"
+  case $s in
+    test) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 ;;
+    test:*) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#test:}" > $O/pytest_${s#test:}.log 2>&1 ;;
+    bench) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err ;;
+    prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --no-extras > $O/bench_prof.json 2> $O/bench_prof.err) ;;
+    n2) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 > $O/bench_n2.json 2> $O/bench_n2.err ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+    py:*) timeout -k 10 600 python -u ${s#py:} > $O/$(basename ${s#py:} .py).log 2>&1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"

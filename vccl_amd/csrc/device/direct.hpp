@@ -268,9 +268,10 @@ __device__ void direct_allreduce(const DirectWork& w) {
   using T = typename Fn::EltType;
   __shared__ int shFail;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
-  // Flag values: chunk c of this call raises base + c + 1; the last
-  // workgroup stores base + nChunks back (graph-replay safe, see epoch_next).
-  const uint32_t base = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // Flag values: chunk c of this call raises the (c+1)-th successor of the
+  // stored epoch (epoch_after: never 0, the never-written flag value); the
+  // last workgroup stores the final one back (graph-replay safe, epoch_next).
+  uint32_t e = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const DirectPeers& P = *w.peers;
   const int n = w.nRanks, me = w.rank, b = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -281,8 +282,9 @@ __device__ void direct_allreduce(const DirectWork& w) {
   if (tid == 0) shFail = 0;
   __syncthreads();
 
-  for (int c = 0; c < w.nChunks && shFail == 0; c++) {
-    const uint32_t e = base + (uint32_t)c + 1;
+  for (int c = 0; c < w.nChunks; c++) {
+    e = epoch_after(e);
+    if (shFail) continue;  // keep stepping e: every workgroup retires the same value
     const int64_t c0 = (int64_t)c * w.chunkElts;
     const int64_t rest = (int64_t)w.count - c0;
     const int64_t cc = rest < w.chunkElts ? rest : w.chunkElts;
@@ -360,7 +362,7 @@ __device__ void direct_allreduce(const DirectWork& w) {
     }
     __syncthreads();  // the region reads of this chunk precede the next chunk's posts
   }
-  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, base + (uint32_t)w.nChunks);
+  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
 }
 
 }  // namespace vccl

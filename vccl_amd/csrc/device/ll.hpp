@@ -117,12 +117,18 @@ __device__ __forceinline__ bool ll_read_line(const char* line, uint32_t epoch, c
   }
 }
 
-// Epoch of this call: *epochWord + 1 (wrapping past 0, the cleared state).
-// The last workgroup to finish (ticket in *doneWord) stores it back for the
-// next call, so the counter is device-resident and graph replays stay in step.
+// Successor of epoch e: e + 1, except that the wrap skips 0 (the cleared
+// state of every line and flag) AND 1, going 0xffffffff -> 2, so consecutive
+// epochs always alternate parity — the LL path's double buffering depends on
+// it (a peer one call ahead writes the other parity's slot).
+__host__ __device__ __forceinline__ uint32_t epoch_after(uint32_t e) {
+  return e + 1 == 0 ? 2u : e + 1;
+}
+// Epoch of this call: the successor of *epochWord.  The last workgroup to
+// finish (ticket in *doneWord) stores it back for the next call, so the
+// counter is device-resident and graph replays stay in step.
 __device__ __forceinline__ uint32_t epoch_next(const uint32_t* epochWord) {
-  uint32_t e = __hip_atomic_load(epochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  return e == 0 ? 1 : e;
+  return epoch_after(__hip_atomic_load(epochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 __device__ __forceinline__ void epoch_retire(uint32_t* epochWord, uint32_t* doneWord, uint32_t e) {
   __syncthreads();

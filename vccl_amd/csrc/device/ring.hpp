@@ -131,14 +131,47 @@ struct RingCtx {
 __device__ __forceinline__ int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 __device__ __forceinline__ int64_t div_up(int64_t x, int64_t a) { return (x + a - 1) / a; }
 
-// Channel part of [0, count): contiguous, 16-byte-aligned element ranges.
-__device__ __forceinline__ void channel_part(int64_t count, int nch, int c, int64_t eltAlign,
-                                             int64_t* off, int64_t* len) {
-  int64_t per = align_up(div_up(count, nch), eltAlign);
-  int64_t lo = per * c < count ? per * c : count;
-  int64_t hi = per * (c + 1) < count ? per * (c + 1) : count;
-  *off = lo;
-  *len = hi - lo;
+// ncclCollCbdPart (device.h:297-323): this channel's part of the call
+// (element offset, element count) and its chunk size; false = idle channel.
+__device__ __forceinline__ bool cbd_part(const RingWork& w, int c, int64_t* off, int64_t* len,
+                                         int64_t* chunk) {
+  if (c < w.channelLo || c > w.channelHi) return false;
+  const int64_t nMid = w.channelHi - w.channelLo - 1;
+  if (c == w.channelLo) {
+    *off = 0;
+    *len = w.countLo;
+    *chunk = w.chunkLo;
+  } else if (c == w.channelHi) {
+    *off = w.countLo + nMid * w.countMid;
+    *len = w.countHi;
+    *chunk = w.chunkHi;
+  } else {
+    *off = w.countLo + (int64_t)(c - w.channelLo - 1) * w.countMid;
+    *len = w.countMid;
+    *chunk = w.chunkMid;
+  }
+  return true;
+}
+
+// One ring step of `nelem` elements (a VCCL chunk, up to 4 slots): the chunk
+// crosses the FIFO slot by slot (the reference's slices, prims_simple.h:
+// 193-194); an empty step still hands over one (empty) slot, as the
+// reference's nelem <= 0 primitive calls do.  Sender and receiver of a chunk
+// always agree on its length, so they agree on the slice count.
+template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
+__device__ __forceinline__ void ring_step(RingCtx& r, const Fn& fn, const void* src, void* dst,
+                                          int64_t nelem, bool postOp, int recvOff = 0,
+                                          int sendOff = 0) {
+  using T = typename Fn::EltType;
+  const int64_t slotElts = (int64_t)r.slotBytes / (int64_t)sizeof(T);
+  const int64_t nSlices = nelem > 0 ? div_up(nelem, slotElts) : 1;
+  for (int64_t s = 0; s < nSlices; s++) {
+    const int64_t o = s * slotElts;
+    const int64_t len = nelem - o < slotElts ? nelem - o : slotElts;
+    r.prim<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, SRC ? (const void*)((const T*)src + o) : nullptr,
+                                             DST ? (void*)((T*)dst + o) : nullptr,
+                                             len > 0 ? len : 0, postOp, recvOff, sendOff);
+  }
 }
 
 // ----------------------------------------------------------------- AllReduce
@@ -149,37 +182,39 @@ __device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int 
   using T = typename Fn::EltType;
   const int n = w.nRanks;
   const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
-  int64_t gridOff, chCount;
-  channel_part((int64_t)w.count, w.nChannels, c, eltAlign, &gridOff, &chCount);
+  int64_t gridOff, chCount, chunkCount;
+  if (!cbd_part(w, c, &gridOff, &chCount, &chunkCount)) return;
   const T* in = (const T*)w.sendbuff;
   T* out = (T*)w.recvbuff;
   const int ringIx = r.ch->ringPos;
-  int64_t chunkCount = w.slotBytes / (int64_t)sizeof(T);
   const int64_t loopCount = (int64_t)n * chunkCount;
   auto modRanks = [n](int x) { return x >= n ? x - n : x; };
   for (int64_t eo = 0; eo < chCount; eo += loopCount) {
     const int64_t rem = chCount - eo;
-    if (rem < loopCount) chunkCount = align_up(div_up(rem, n), eltAlign);
+    if (rem < loopCount) chunkCount = align_up(div_up(rem, n), eltAlign);  // all_reduce.h:36
     auto off_of = [&](int chunk) { return gridOff + eo + chunk * chunkCount; };
     auto len_of = [&](int chunk) {
       int64_t l = rem - (int64_t)chunk * chunkCount;
       return l < chunkCount ? (l < 0 ? 0 : l) : chunkCount;
     };
     int chunk = modRanks(ringIx + n - 1);  // step 0: send own chunk
-    r.prim<Fn, false, true, true, false, UNROLL>(fn, in + off_of(chunk), nullptr, len_of(chunk), false);
+    ring_step<Fn, false, true, true, false, UNROLL>(r, fn, in + off_of(chunk), nullptr, len_of(chunk), false);
     for (int j = 2; j < n; ++j) {          // n-2 recv-reduce-send
       chunk = modRanks(ringIx + n - j);
-      r.prim<Fn, true, true, true, false, UNROLL>(fn, in + off_of(chunk), nullptr, len_of(chunk), false);
+      ring_step<Fn, true, true, true, false, UNROLL>(r, fn, in + off_of(chunk), nullptr, len_of(chunk),
+                                                     false);
     }
     chunk = ringIx;                         // final reduce: output + send
-    r.prim<Fn, true, true, true, true, UNROLL>(fn, in + off_of(chunk), out + off_of(chunk),
-                                               len_of(chunk), true);
+    ring_step<Fn, true, true, true, true, UNROLL>(r, fn, in + off_of(chunk), out + off_of(chunk),
+                                                  len_of(chunk), true);
     for (int j = 1; j < n - 1; ++j) {      // n-2 recv-copy-send
       chunk = modRanks(ringIx + n - j);
-      r.prim<Fn, true, true, false, true, UNROLL>(fn, nullptr, out + off_of(chunk), len_of(chunk), false);
+      ring_step<Fn, true, true, false, true, UNROLL>(r, fn, nullptr, out + off_of(chunk), len_of(chunk),
+                                                     false);
     }
     chunk = modRanks(ringIx + 1);          // final recv
-    r.prim<Fn, true, false, false, true, UNROLL>(fn, nullptr, out + off_of(chunk), len_of(chunk), false);
+    ring_step<Fn, true, false, false, true, UNROLL>(r, fn, nullptr, out + off_of(chunk), len_of(chunk),
+                                                    false);
   }
 }
 
@@ -190,14 +225,12 @@ template <class Fn, int UNROLL>
 __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
   using T = typename Fn::EltType;
   const int n = w.nRanks;
-  const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
   const int64_t count = (int64_t)w.count;
-  int64_t gridOff, chCount;
-  channel_part(count, w.nChannels, c, eltAlign, &gridOff, &chCount);
+  int64_t gridOff, chCount, chunkCount;
+  if (!cbd_part(w, c, &gridOff, &chCount, &chunkCount)) return;
   const T* in = (const T*)w.sendbuff;
   T* out = (T*)w.recvbuff;
   const int* ringRanks = r.ch->ringRanks;
-  const int64_t chunkCount = w.slotBytes / (int64_t)sizeof(T);
   // A chunk for rank k sits in its slots at k's block misalignment (the same
   // on every rank: dataOff is a 16-byte multiple), so the FIFO operand shares
   // the input block's alignment (reduce_copy_misaligned).
@@ -206,16 +239,16 @@ __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, 
     const int64_t nelem = chCount - eo < chunkCount ? chCount - eo : chunkCount;
     const int64_t dataOff = gridOff + eo;
     int rankDest = ringRanks[n - 1];
-    r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false,
-                                                 0, mis(rankDest));
+    ring_step<Fn, false, true, true, false, UNROLL>(r, fn, in + dataOff + rankDest * count, nullptr, nelem,
+                                                    false, 0, mis(rankDest));
     for (int j = 2; j < n; ++j) {
       rankDest = ringRanks[n - j];
-      r.prim<Fn, true, true, true, false, UNROLL>(fn, in + dataOff + rankDest * count, nullptr, nelem, false,
-                                                  mis(rankDest), mis(rankDest));
+      ring_step<Fn, true, true, true, false, UNROLL>(r, fn, in + dataOff + rankDest * count, nullptr,
+                                                     nelem, false, mis(rankDest), mis(rankDest));
     }
     rankDest = ringRanks[0];
-    r.prim<Fn, true, false, true, true, UNROLL>(fn, in + dataOff + rankDest * count, out + dataOff,
-                                                nelem, true, mis(rankDest), 0);
+    ring_step<Fn, true, false, true, true, UNROLL>(r, fn, in + dataOff + rankDest * count, out + dataOff,
+                                                   nelem, true, mis(rankDest), 0);
   }
 }
 
@@ -227,12 +260,11 @@ __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
   const Fn fn(0);
   const int n = w.nRanks;
   const int64_t count = (int64_t)w.count;  // bytes per rank
-  int64_t partOff, partCount;
-  channel_part(count, w.nChannels, c, 16, &partOff, &partCount);
+  int64_t partOff, partCount, chunkCount;
+  if (!cbd_part(w, c, &partOff, &partCount, &chunkCount)) return;
   const uint8_t* in = (const uint8_t*)w.sendbuff;
   uint8_t* out = (uint8_t*)w.recvbuff;
   const int* ringRanks = r.ch->ringRanks;
-  const int64_t chunkCount = w.slotBytes;
   // A block for rank k travels at k's output misalignment inside the slots
   // (same on every rank), so the slot and the output block share alignment.
   auto mis = [&](int k) { return (int)(((int64_t)k * count) & 15); };
@@ -242,20 +274,21 @@ __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
     int rankDest = ringRanks[0];
     int64_t off = dataOff + rankDest * count;
     if (in + dataOff == out + off)
-      r.prim<Fn, false, true, true, false, UNROLL>(fn, in + dataOff, nullptr, nelem, false, 0,
-                                                   mis(rankDest));
+      ring_step<Fn, false, true, true, false, UNROLL>(r, fn, in + dataOff, nullptr, nelem, false, 0,
+                                                      mis(rankDest));
     else
-      r.prim<Fn, false, true, true, true, UNROLL>(fn, in + dataOff, out + off, nelem, false, 0,
-                                                  mis(rankDest));
+      ring_step<Fn, false, true, true, true, UNROLL>(r, fn, in + dataOff, out + off, nelem, false, 0,
+                                                     mis(rankDest));
     for (int j = 1; j < n - 1; ++j) {
       rankDest = ringRanks[n - j];
       off = dataOff + rankDest * count;
-      r.prim<Fn, true, true, false, true, UNROLL>(fn, nullptr, out + off, nelem, false, mis(rankDest),
-                                                  mis(rankDest));
+      ring_step<Fn, true, true, false, true, UNROLL>(r, fn, nullptr, out + off, nelem, false, mis(rankDest),
+                                                     mis(rankDest));
     }
     rankDest = ringRanks[1];
     off = dataOff + rankDest * count;
-    r.prim<Fn, true, false, false, true, UNROLL>(fn, nullptr, out + off, nelem, false, mis(rankDest), 0);
+    ring_step<Fn, true, false, false, true, UNROLL>(r, fn, nullptr, out + off, nelem, false, mis(rankDest),
+                                                    0);
   }
 }
 

@@ -78,9 +78,19 @@ struct RingWork {
   const void* redArgPtr;             // ncclScalarDevice scalar (read on device)
   int redArgBytes;
   int preOp;                         // PreMulSum: scale own input
-  int nChannels;                     // channels used by this launch
+  int nChannels;                     // workgroups launched (= cbd.channelHi + 1)
   int slotBytes;
   int nRanks;
+  // VCCL's channel partition of this call (ncclDevWorkColl.cbd, device.h:
+  // 258-287, filled by the host's restatement of scheduleCollTasksToPlan,
+  // enqueue.cc:597-644): channels [channelLo, channelHi] carry parts of
+  // countLo / countMid... / countHi elements, moved in chunks of chunkLo /
+  // chunkMid / chunkHi elements per ring step (calcCollChunking: 4 FIFO slots
+  // for SIMPLE) — each chunk step crosses the FIFO as ceil(chunk / slot)
+  // slices.  Same partition => the same fold order per element as VCCL.
+  int channelLo, channelHi;
+  int64_t countLo, countMid, countHi;
+  int64_t chunkLo, chunkMid, chunkHi;
 };
 
 }  // namespace vccl

@@ -13,6 +13,7 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <chrono>
@@ -90,8 +91,16 @@ void root_main(int lfd, uint64_t nonce) {
     int fd = accept(lfd, nullptr, nullptr);
     if (fd < 0) continue;
     set_nodelay(fd);
+    // A connection that never sends its Hello (a stale rank, a port probe)
+    // must not stall the rendezvous: bounded read, then blocking again for
+    // the all-gather rounds (which legitimately wait for the slowest rank).
+    timeval tv{(time_t)param_int("BOOTSTRAP_HELLO_TIMEOUT_S", 10), 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
     Hello h;
-    if (!recv_all(fd, &h, sizeof(h)) || h.magic != kHelloMagic || h.nonce != nonce ||
+    const bool got = recv_all(fd, &h, sizeof(h));
+    timeval none{0, 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));
+    if (!got || h.magic != kHelloMagic || h.nonce != nonce ||
         h.nranks <= 0 || h.rank < 0 || h.rank >= h.nranks || (nranks >= 0 && h.nranks != nranks)) {
       close(fd);
       continue;

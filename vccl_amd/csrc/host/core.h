@@ -138,7 +138,15 @@ struct ncclComm {
   hipEvent_t joinEvent = nullptr;     // joins other streams into a fused group launch
   hipStream_t lastStream = nullptr;
   bool hasLastLaunch = false;         // lastLaunch/lastStream are valid
+  // the same ordering inside a stream capture (recorded in the graph)
+  hipEvent_t capEvent = nullptr;
+  unsigned long long capId = 0;
+  hipStream_t capLastStream = nullptr;
+  bool capHasLast = false;
   uint64_t fusedLaunches = 0;         // group launches that carried > 1 collective
+  // CTA (workgroup) bounds of every collective launch: ncclConfig_t
+  // minCTAs / maxCTAs or NCCL_MIN_CTAS / NCCL_MAX_CTAS (init.cc:1478-1540)
+  int minCTAs = 1, maxCTAs = 64;
   // state
   std::atomic<int> asyncError{0};
   std::vector<vccl::UserRedOp> userOps;

@@ -6,8 +6,8 @@
 // hostToDevRedOp :2217-2310 and the nRanks==1 shortcut ncclLaunchOneRank
 // onerank.cu:47-83), re-implemented for one node: the planner picks one of
 // three algorithms per call (choose_algo: one-shot LL, two-shot direct, SIMPLE
-// ring over xGMI); the ring's channel partition is done on the device
-// (ring.hpp channel_part).  Group semantics (group.cc:92-110, :393-506): calls
+// ring over xGMI); the ring's channel partition is VCCL's own cbd split
+// (cbd_schedule below, ring.hpp cbd_part).  Group semantics (group.cc:92-110, :393-506): calls
 // between ncclGroupStart/End are queued per thread and launched at the
 // outermost ncclGroupEnd in call order, runs of small all-reduces fused into
 // one LL launch (launch_group).
@@ -188,16 +188,57 @@ static ncclResult_t args_check(ncclComm* comm, const char* name, ncclDataType_t 
 // serialises through its internal strong stream, enqueue.cc:1445-1548).
 // The null stream (0) is a valid user stream, so "no launch yet" is a flag of
 // its own, not a null lastStream.
+//
+// Graph capture (the reference's strong streams track capture the same way,
+// misc/strongstream.cc): launches on a capturing stream are ordered only
+// against earlier launches of the SAME capture, through an event recorded
+// inside it (a fork/join inside the graph); they neither wait on the eager
+// lastLaunch event (recorded outside the capture) nor overwrite it, so eager
+// work before and after the capture keeps its own ordering.
+struct CaptureState {
+  bool active;
+  unsigned long long id;
+};
+static ncclResult_t capture_state(hipStream_t s, CaptureState* cs) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  HIPCHECK(hipStreamGetCaptureInfo(s, &st, &id));
+  cs->active = st == hipStreamCaptureStatusActive;
+  cs->id = id;
+  return ncclSuccess;
+}
 static ncclResult_t stream_order(ncclComm* comm, hipStream_t s) {
+  CaptureState cs;
+  NCCLCHECK(capture_state(s, &cs));
+  if (cs.active) {
+    if (comm->capHasLast && comm->capId == cs.id && comm->capLastStream != s)
+      HIPCHECK(hipStreamWaitEvent(s, comm->capEvent, 0));
+    return ncclSuccess;
+  }
   if (comm->hasLastLaunch && comm->lastStream != s)
     HIPCHECK(hipStreamWaitEvent(s, comm->lastLaunch, 0));
   return ncclSuccess;
 }
 static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s) {
+  CaptureState cs;
+  NCCLCHECK(capture_state(s, &cs));
+  if (cs.active) {
+    HIPCHECK(hipEventRecord(comm->capEvent, s));
+    comm->capId = cs.id;
+    comm->capLastStream = s;
+    comm->capHasLast = true;
+    return ncclSuccess;
+  }
   HIPCHECK(hipEventRecord(comm->lastLaunch, s));
   comm->lastStream = s;
   comm->hasLastLaunch = true;
   return ncclSuccess;
+}
+// The event stream_mark just recorded on s (for joining other streams).
+static hipEvent_t stream_last_event(ncclComm* comm, hipStream_t s) {
+  CaptureState cs{false, 0};
+  (void)capture_state(s, &cs);
+  return cs.active ? comm->capEvent : comm->lastLaunch;
 }
 
 // ncclLaunchOneRank (onerank.cu:47-83): a copy, or the PreMulSum kernel.
@@ -233,6 +274,76 @@ static ncclResult_t launch_one_rank(const Task& t) {
   return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
 }
 
+// VCCL's channel partition of one ring collective (scheduleCollTasksToPlan
+// for a plan holding one task, enqueue.cc:518-565 + 597-644, with the
+// channel tuning of topoGetAlgoInfo :1902-1925 and calcCollChunking's RING /
+// SIMPLE chunk :2027-2030, 2093), so every element lands on the same channel
+// and the same chunk of the same loop as in VCCL — hence the same ring and
+// fold order.  `count` / `eltSize` are already AG-rewritten to bytes.
+// Restated for the tests in oracle/vccl_sched.py.
+struct CbdPlan {
+  int channelLo, channelHi;
+  int64_t countLo, countMid, countHi;
+  int64_t chunkLo, chunkMid, chunkHi;  // elements
+};
+static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
+                            int64_t slotBytes) {
+  constexpr int64_t kMinTraffic = 16 << 10;         // enqueue.cc:528
+  constexpr int64_t kSimpleThreads = 512;          // maxThreads[RING][SIMPLE] (tuning.cc:198-200)
+  constexpr int64_t kSimpleThreshold = 64;         // NCCL_SIMPLE_THREAD_THRESHOLD (comm.h:40)
+  constexpr int64_t kGrain = 512;                  // ncclProtoGrainSize(SIMPLE) (device.h:290-295)
+  auto divUp = [](int64_t a, int64_t b) { return (a + b - 1) / b; };
+  const int64_t tpb = coll == kAllReduce ? 2 : nRanks;  // ncclFuncTrafficPerByte (enqueue.cc:67-74)
+  const int64_t nBytes = eltSize * (coll == kAllReduce ? count : (int64_t)nRanks * count);
+  int64_t nc = commChannels;                        // enqueue.cc:1921-1924
+  while (nBytes < nc * kSimpleThreads * kSimpleThreshold && nc >= 2) nc--;
+  const int64_t traffic = std::max(kMinTraffic, count * eltSize * tpb);
+  const int64_t nMax = commChannels;
+  const int64_t trafficPerChannel = std::max(kMinTraffic, traffic / std::min(nc, nMax));
+  int64_t channelId = 0;
+  const int64_t cellSize = divUp(divUp(kMinTraffic, tpb), 16) * 16;
+  const int64_t eltsPerCell = cellSize / eltSize;
+  const int64_t cells = divUp(count * eltSize, cellSize);
+  const int64_t trafficPerCell = cellSize * tpb;
+  int64_t cellsPerChannel = std::min(cells, divUp(trafficPerChannel, trafficPerCell));
+  int64_t cellsLo = channelId + 1 == nMax ? cells : std::min(cells, divUp(trafficPerChannel, trafficPerCell));
+  int64_t nMid = (cells - cellsLo) / cellsPerChannel;
+  int64_t cellsHi = (cells - cellsLo) % cellsPerChannel;
+  int64_t nCh = (cellsLo ? 1 : 0) + nMid + (cellsHi ? 1 : 0);
+  if (nMax < channelId + nCh) {
+    nMid = nMax - channelId - 2;
+    cellsPerChannel = (cells - cellsLo) / (nMid + 1);
+    cellsHi = cellsPerChannel + (cells - cellsLo) % (nMid + 1);
+  }
+  if (cellsHi == 0 && nMid != 0) {
+    cellsHi = cellsPerChannel;
+    nMid -= 1;
+  }
+  if (cellsLo == 0) {
+    channelId += 1;
+    if (nMid == 0) {
+      cellsLo = cellsHi;
+      cellsHi = 0;
+    } else {
+      cellsLo = cellsPerChannel;
+      nMid -= 1;
+    }
+  }
+  CbdPlan p{};
+  p.countMid = nMid != 0 ? cellsPerChannel * eltsPerCell : 0;
+  p.countLo = cellsLo * eltsPerCell;
+  p.countHi = cellsHi * eltsPerCell;
+  (p.countHi != 0 ? p.countHi : p.countLo) -= cells * eltsPerCell - count;
+  nCh = (p.countLo ? 1 : 0) + nMid + (cellsHi ? 1 : 0);
+  p.channelLo = (int)channelId;
+  p.channelHi = (int)(channelId + nCh - 1);
+  // RING / SIMPLE chunk: chunkSteps (4) FIFO steps of buffSize / NCCL_STEPS
+  // (= one slot here), rounded down to the 512 B grain; independent of size.
+  const int64_t chunkElts = (4 * slotBytes) / kGrain * kGrain / eltSize;
+  p.chunkLo = p.chunkMid = p.chunkHi = chunkElts;
+  return p;
+}
+
 static ncclResult_t launch_ring(const Task& t) {
   ncclComm* comm = t.comm;
   RingWork w{};
@@ -257,6 +368,22 @@ static ncclResult_t launch_ring(const Task& t) {
   }
   w.redArgPtr = t.argPtr;  // ncclScalarDevice: dereferenced by the kernel (nccl.h.in:255-262)
   w.redArgBytes = type_size(t.datatype);
+  {
+    const int64_t esz = t.coll == kAllGather ? 1 : type_size(t.datatype);
+    const CbdPlan p = cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
+                                   comm->slotBytes);
+    if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
+      return ncclInternalError;
+    w.channelLo = p.channelLo;
+    w.channelHi = p.channelHi;
+    w.countLo = p.countLo;
+    w.countMid = p.countMid;
+    w.countHi = p.countHi;
+    w.chunkLo = p.chunkLo;
+    w.chunkMid = p.chunkMid;
+    w.chunkHi = p.chunkHi;
+    w.nChannels = p.channelHi + 1;  // idle channels above channelHi are not launched
+  }
   const int coll = t.coll == kAllReduce ? kCollAllReduce
                    : t.coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
   hipError_t e = hipErrorInvalidValue;
@@ -318,7 +445,8 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   // for the peers' spins to complete; 256 x 4 waves is 1/8 of a GPU's
   // residency.  Tests that put 8 ranks on ONE GPU lower it.
   const int maxBlocks = (int)std::max<int64_t>(1, param_int("LL_MAX_BLOCKS", 256));
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((lines + 255) / 256, maxBlocks));
+  int grid = (int)std::max<int64_t>(1, std::min<int64_t>((lines + 255) / 256, maxBlocks));
+  grid = std::max(std::min(grid, comm->maxCTAs), comm->minCTAs);
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
     case K_U8: e = ll_launch<K_U8>(t.devOp, w, grid, t.stream); break;
@@ -366,8 +494,9 @@ static ncclResult_t launch_direct(const Task& t) {
   w.nChunks = (int)(((int64_t)t.count + w.chunkElts - 1) / w.chunkElts);
   const int64_t shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
   const int64_t minBlk = (16 << 10) / esz;
-  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((shard0 + minBlk - 1) / minBlk,
-                                                            comm->directMaxBlocks));
+  int64_t nb = std::min<int64_t>((shard0 + minBlk - 1) / minBlk, comm->directMaxBlocks);
+  nb = std::max<int64_t>(std::min<int64_t>(nb, comm->maxCTAs), comm->minCTAs);
+  nb = std::max<int64_t>(1, std::min<int64_t>(nb, kDirectMaxBlocks));
   w.blkElts = align_up((shard0 + nb - 1) / nb, eltAlign);
   w.nBlocks = (int)((shard0 + w.blkElts - 1) / w.blkElts);
   w.regionBytes = comm->dRegionBytes;
@@ -474,8 +603,9 @@ static ncclResult_t launch_ll_batch(const std::vector<Task>& ts) {
   }
   if (r == ncclSuccess) r = launch_ll(ts.data(), (int)ts.size());
   if (r == ncclSuccess) r = stream_mark(comm, s0);
+  const hipEvent_t done = stream_last_event(comm, s0);
   for (hipStream_t s : others)
-    if (r == ncclSuccess && hipStreamWaitEvent(s, comm->lastLaunch, 0) != hipSuccess)
+    if (r == ncclSuccess && hipStreamWaitEvent(s, done, 0) != hipSuccess)
       r = ncclUnhandledCudaError;
   comm->opCount += ts.size();
   comm->fusedLaunches++;
@@ -510,9 +640,9 @@ static ncclResult_t launch_group(std::vector<Task>& tasks) {
   return ret;
 }
 
-static ncclResult_t enqueue_check(int coll, const char* name, const void* sendbuff, void* recvbuff,
-                                  size_t count, ncclDataType_t dt, ncclRedOp_t op, ncclComm* comm,
-                                  hipStream_t stream) {
+static ncclResult_t enqueue_check_impl(int coll, const char* name, const void* sendbuff,
+                                       void* recvbuff, size_t count, ncclDataType_t dt,
+                                       ncclRedOp_t op, ncclComm* comm, hipStream_t stream) {
   NCCLCHECK(comm_check(comm, name));
   NCCLCHECK(args_check(comm, name, dt, op, coll != kAllGather));
   VINFO("%s: opCount %lx sendbuff %p recvbuff %p count %zu datatype %d op %d comm %p [nranks=%d] stream %p",
@@ -544,11 +674,54 @@ static ncclResult_t enqueue_check(int coll, const char* name, const void* sendbu
   return launch_task(t);
 }
 
+// ncclGroupErrCheck (enqueue.cc:2516): inside a group the first failing call
+// is remembered, and the outermost ncclGroupEnd then launches nothing of the
+// group and returns that error (group.cc:528, :591).
+static ncclResult_t enqueue_check(int coll, const char* name, const void* sendbuff, void* recvbuff,
+                                  size_t count, ncclDataType_t dt, ncclRedOp_t op, ncclComm* comm,
+                                  hipStream_t stream) {
+  const ncclResult_t r =
+      enqueue_check_impl(coll, name, sendbuff, recvbuff, count, dt, op, comm, stream);
+  if (r != ncclSuccess && tl_groupDepth > 0 && tl_groupError == ncclSuccess) tl_groupError = r;
+  return r;
+}
+
 }  // namespace vccl
 
 using namespace vccl;
 
 #define VCCL_EXPORT extern "C" __attribute__((visibility("default")))
+
+// Out-of-scope calls of the reference API (include/nccl.h):
+// exported so a binary linked against libnccl loads, never silently wrong.
+static ncclResult_t out_of_scope(const char* name) {
+  VWARN("%s is not part of this library's scope (AllReduce / ReduceScatter / AllGather only)",
+        name);
+  return ncclInvalidUsage;
+}
+VCCL_EXPORT ncclResult_t ncclReduce(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int,
+                                    ncclComm_t, hipStream_t) {
+  return out_of_scope("ncclReduce");
+}
+VCCL_EXPORT ncclResult_t ncclBcast(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) {
+  return out_of_scope("ncclBcast");
+}
+VCCL_EXPORT ncclResult_t ncclBroadcast(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
+                                       hipStream_t) {
+  return out_of_scope("ncclBroadcast");
+}
+VCCL_EXPORT ncclResult_t ncclSend(const void*, size_t, ncclDataType_t, int, ncclComm_t,
+                                  hipStream_t) {
+  return out_of_scope("ncclSend");
+}
+VCCL_EXPORT ncclResult_t ncclRecv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) {
+  return out_of_scope("ncclRecv");
+}
+VCCL_EXPORT ncclResult_t ncclCommSplit(ncclComm_t, int, int, ncclComm_t* newcomm, ncclConfig_t*) {
+  if (newcomm) *newcomm = nullptr;
+  return out_of_scope("ncclCommSplit");
+}
+
 #define VCCL_ALIAS(name) __attribute__((alias(#name), visibility("default")))
 
 VCCL_EXPORT ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count,
@@ -583,13 +756,16 @@ VCCL_EXPORT ncclResult_t ncclGroupEnd(void) {
     return ncclInvalidUsage;
   }
   if (--tl_groupDepth > 0) return ncclSuccess;
-  ncclResult_t ret = tl_groupError;
+  const ncclResult_t err = tl_groupError;
+  tl_groupError = ncclSuccess;
   std::vector<Task> tasks;
   tasks.swap(tl_tasks);
-  ncclResult_t r = launch_group(tasks);
-  if (ret == ncclSuccess) ret = r;
-  tl_groupError = ncclSuccess;
-  return ret;
+  if (err != ncclSuccess) {  // a call of the group failed: drop the whole group
+    VWARN("ncclGroupEnd: a call in the group failed (%d); %zu queued collectives not launched",
+          (int)err, tasks.size());
+    return err;
+  }
+  return launch_group(tasks);
 }
 
 VCCL_EXPORT ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar,
@@ -670,13 +846,24 @@ ncclResult_t pncclGroupEnd(void) VCCL_ALIAS(ncclGroupEnd);
 ncclResult_t pncclRedOpCreatePreMulSum(ncclRedOp_t*, void*, ncclDataType_t, ncclScalarResidence_t,
                                        ncclComm_t) VCCL_ALIAS(ncclRedOpCreatePreMulSum);
 ncclResult_t pncclRedOpDestroy(ncclRedOp_t, ncclComm_t) VCCL_ALIAS(ncclRedOpDestroy);
+ncclResult_t pncclReduce(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+                         hipStream_t) VCCL_ALIAS(ncclReduce);
+ncclResult_t pncclBcast(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)
+    VCCL_ALIAS(ncclBcast);
+ncclResult_t pncclBroadcast(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
+                            hipStream_t) VCCL_ALIAS(ncclBroadcast);
+ncclResult_t pncclSend(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)
+    VCCL_ALIAS(ncclSend);
+ncclResult_t pncclRecv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)
+    VCCL_ALIAS(ncclRecv);
+ncclResult_t pncclCommSplit(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*)
+    VCCL_ALIAS(ncclCommSplit);
 }
 
 extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count,
                                          ncclDataType_t datatype, int* algo) {
   NCCLCHECK(comm_check(comm, "vcclCommCollAlgo"));
-  if (!algo || coll < 0 || coll > 2 || (int)datatype < 0 || (int)datatype > 9)
-    return ncclInvalidArgument;
+  if (!algo || coll < 0 || coll > 2 || type_size(datatype) < 1) return ncclInvalidArgument;
   if (comm->nRanks == 1) {
     *algo = vcclAlgoOneRank;
     return ncclSuccess;
@@ -688,6 +875,22 @@ extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count
   t.datatype = datatype;
   const int a = choose_algo(t);
   *algo = a == kAlgoLL ? vcclAlgoLL : a == kAlgoDirect ? vcclAlgoDirect : vcclAlgoRing;
+  return ncclSuccess;
+}
+
+extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition(
+    int coll, size_t count, ncclDataType_t datatype, int nRanks, int nChannels, size_t slotBytes,
+    int64_t* out) {
+  if (!out || coll < 0 || coll > 2 || type_size(datatype) < 1 || nRanks < 1 ||
+      nChannels < 1 || nChannels > kMaxChannels || count == 0 || slotBytes < 4096)
+    return ncclInvalidArgument;
+  const int c = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : kAllGather;
+  const int64_t esz = c == kAllGather ? 1 : type_size(datatype);
+  const int64_t cnt = c == kAllGather ? (int64_t)count * type_size(datatype) : (int64_t)count;
+  const CbdPlan p = cbd_schedule(c, cnt, esz, nRanks, nChannels, (int64_t)slotBytes);
+  const int64_t v[8] = {p.channelLo, p.channelHi, p.countLo, p.countMid,
+                        p.countHi,   p.chunkLo,   p.chunkMid, p.chunkHi};
+  memcpy(out, v, sizeof(v));
   return ncclSuccess;
 }
 

@@ -10,9 +10,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstring>
 #include <thread>
 
+#include "../../../include/vccl_ext.h"
 #include "../device/direct.hpp"
 #include "core.h"
 
@@ -86,7 +88,8 @@ static void free_resources(ncclComm* c) {
   if (c->errorFlag) (void)hipHostFree(c->errorFlag);
   if (c->lastLaunch) (void)hipEventDestroy(c->lastLaunch);
   if (c->joinEvent) (void)hipEventDestroy(c->joinEvent);
-  c->joinEvent = nullptr;
+  if (c->capEvent) (void)hipEventDestroy(c->capEvent);
+  c->joinEvent = c->capEvent = nullptr;
   c->fifoBuf = c->flagBuf = nullptr;
   c->devComm = nullptr;
   c->devChannels = nullptr;
@@ -141,11 +144,17 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   // 8- and 4-GPU ring sets (56 / 48 workgroups), 32 for 2 GPUs.
   int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : 32);
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
+  // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490)
+  nch = std::max(c->minCTAs, std::min(nch, c->maxCTAs));
   nch = std::max(1, std::min(nch, kMaxChannels));
   c->nChannels = n > 1 ? nch : 0;
-  c->slotBytes = (int)param_int("SLOT_BYTES", 512 << 10);
+  // Slot = one FIFO step: NCCL_BUFFSIZE / NCCL_STEPS (init.cc:619-633, 4 MiB
+  // -> 512 KiB), or VCCL_SLOT_BYTES directly.
+  const int64_t buffSize = param_int("BUFFSIZE", -2);
+  c->slotBytes = (int)param_int("SLOT_BYTES", buffSize > 0 ? buffSize / kSteps : 512 << 10);
   if (c->slotBytes < 4096 || c->slotBytes % 4096 || c->slotBytes > (64 << 20)) {
-    VWARN("NCCL_SLOT_BYTES must be a multiple of 4096 up to 64 MiB, using 524288");
+    VWARN("slot size (NCCL_BUFFSIZE / 8 or VCCL_SLOT_BYTES) must be a multiple of 4096 up to "
+          "64 MiB, using 524288");
     c->slotBytes = 512 << 10;
   }
   {
@@ -166,6 +175,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   *c->errorFlag = 0;
   HIPCHECK(hipEventCreateWithFlags(&c->lastLaunch, hipEventDisableTiming));
   HIPCHECK(hipEventCreateWithFlags(&c->joinEvent, hipEventDisableTiming));
+  HIPCHECK(hipEventCreateWithFlags(&c->capEvent, hipEventDisableTiming));
 
   PeerMap me{};
   me.pid = (int)getpid();
@@ -261,14 +271,44 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     c->nChannels = std::max(1, std::min(c->nChannels, (int)param_int("NET_NCHANNELS", 8)));
     VINFO("rank %d: inter-node ring through the net proxy, %d channels", c->rank, c->nChannels);
   }
-  for (int r = 0; r < n; r++) {
-    if (netPeer[r]) continue;
-    // init.cc:732-735: two ranks on one GPU is invalid usage.  The escape
-    // hatch exists for protocol tests on a 1-GPU machine only.
-    if (r != c->rank && c->peers[r].busId == me.busId && !param_int("ALLOW_SHARED_DEVICE", 0)) {
-      VWARN("Duplicate GPU detected : rank %d and rank %d both on device %lx", c->rank, r,
-            (long)me.busId);
-      return ncclInvalidUsage;
+  // init.cc:732-735: two ranks on one GPU is invalid usage.  The escape hatch
+  // exists for protocol tests on a 1-GPU machine only.  Checked over every
+  // pair, so every rank fails together.
+  if (!param_int("ALLOW_SHARED_DEVICE", 0) && !netForce) {
+    for (int q = 0; q < n; q++)
+      for (int r = q + 1; r < n; r++)
+        if (c->peers[r].hostHash == c->peers[q].hostHash && c->peers[r].busId == c->peers[q].busId) {
+          VWARN("Duplicate GPU detected : rank %d and rank %d both on device %lx", q, r,
+                (long)c->peers[q].busId);
+          return ncclInvalidUsage;
+        }
+  }
+  {
+    // Ranks of this comm that share ONE device inside ONE process (allowed
+    // only through VCCL_ALLOW_SHARED_DEVICE) spin on each other, so their
+    // kernels must be co-resident.  HIP gives a process GPU_MAX_HW_QUEUES
+    // hardware queues (4 by default) and deals streams to them round-robin,
+    // one of them taken by the process's first (null / runtime) stream: with
+    // more sharing ranks than the remaining queues, two ranks' kernels
+    // serialise on one queue and every peer spins until the timeout
+    // (profiles/r01_diag_protocol.log).  Refuse that configuration up front.
+    // Every rank evaluates every (process, device) group from the same peer
+    // table, so all ranks fail together (none is left waiting at the final
+    // barrier).
+    const char* hq = getenv("GPU_MAX_HW_QUEUES");
+    const int hwQueues = hq && atoi(hq) > 0 ? atoi(hq) : 4;
+    for (int q = 0; q < n; q++) {
+      int sameDev = 0;
+      for (int r = 0; r < n; r++)
+        sameDev += c->peers[r].pid == c->peers[q].pid &&
+                   c->peers[r].hostHash == c->peers[q].hostHash &&
+                   c->peers[r].busId == c->peers[q].busId;
+      if (sameDev > 1 && sameDev > hwQueues - 1) {
+        VWARN("%d ranks of this communicator share device %lx in one process, but only %d of the "
+              "process's %d hardware queues can keep their kernels co-resident",
+              sameDev, (long)c->peers[q].busId, hwQueues - 1, hwQueues);
+        return ncclInvalidUsage;
+      }
     }
   }
 
@@ -367,8 +407,48 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   return ncclSuccess;
 }
 
+// ncclConfig_t + NCCL_* environment -> CTA bounds (envConfigOverride,
+// init.cc:1472-1545: env wins, non-positive values are ignored, both capped
+// at MAXCHANNELS, min > max sets min = max).  Non-blocking communicators are
+// not supported (SURVEY.md §8b allows blocking-only): a request for one is
+// reported with a WARN and the comm is created blocking.
+static ncclResult_t apply_config(ncclComm* c, const ncclConfig_t* config) {
+  int minC = NCCL_CONFIG_UNDEF_INT, maxC = NCCL_CONFIG_UNDEF_INT;
+  int blocking = NCCL_CONFIG_UNDEF_INT;
+  if (config) {
+    if (config->magic != 0xcafebeef) {
+      VWARN("ncclCommInitRankConfig: config not initialised with NCCL_CONFIG_INITIALIZER");
+      return ncclInvalidArgument;
+    }
+    if ((config->minCTAs != NCCL_CONFIG_UNDEF_INT && config->minCTAs <= 0) ||
+        (config->maxCTAs != NCCL_CONFIG_UNDEF_INT && config->maxCTAs <= 0) ||
+        (config->blocking != NCCL_CONFIG_UNDEF_INT && config->blocking != 0 &&
+         config->blocking != 1)) {
+      VWARN("ncclCommInitRankConfig: invalid config (blocking %d, minCTAs %d, maxCTAs %d)",
+            config->blocking, config->minCTAs, config->maxCTAs);
+      return ncclInvalidArgument;  // init.cc:1603-1612
+    }
+    minC = config->minCTAs;
+    maxC = config->maxCTAs;
+    blocking = config->blocking;
+  }
+  const int64_t envMin = param_int("MIN_CTAS", NCCL_CONFIG_UNDEF_INT);
+  const int64_t envMax = param_int("MAX_CTAS", NCCL_CONFIG_UNDEF_INT);
+  const int64_t envBlocking = param_int("COMM_BLOCKING", NCCL_CONFIG_UNDEF_INT);
+  if (envMin != NCCL_CONFIG_UNDEF_INT && envMin > 0) minC = (int)envMin;
+  if (envMax != NCCL_CONFIG_UNDEF_INT && envMax > 0) maxC = (int)envMax;
+  if (envBlocking == 0 || envBlocking == 1) blocking = (int)envBlocking;
+  c->minCTAs = minC == NCCL_CONFIG_UNDEF_INT ? 1 : std::min(minC, kMaxChannels);
+  c->maxCTAs = maxC == NCCL_CONFIG_UNDEF_INT ? kMaxChannels : std::min(maxC, kMaxChannels);
+  if (c->minCTAs > c->maxCTAs) c->minCTAs = c->maxCTAs;
+  if (blocking == 0)
+    VWARN("non-blocking communicator requested (config.blocking = 0 / NCCL_COMM_BLOCKING=0): "
+          "this library initialises and enqueues blocking; calls never return ncclInProgress");
+  return ncclSuccess;
+}
+
 ncclResult_t comm_init_rank(ncclComm_t* out, int nranks, const ncclUniqueId* id, int rank,
-                            int device) {
+                            int device, const ncclConfig_t* config) {
   if (!out) return ncclInvalidArgument;
   *out = nullptr;
   if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) {
@@ -381,6 +461,11 @@ ncclResult_t comm_init_rank(ncclComm_t* out, int nranks, const ncclUniqueId* id,
   c->nRanks = nranks;
   c->device = device;
   c->userOpFreeHead = 0;
+  if (ncclResult_t cr = apply_config(c, config); cr != ncclSuccess) {
+    c->magic = 0;
+    delete c;
+    return cr;
+  }
   ncclResult_t r = init_rank(c, id);
   if (r != ncclSuccess) {
     free_resources(c);
@@ -438,21 +523,15 @@ VCCL_EXPORT ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniq
                                           int rank) {
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
-  return comm_init_rank(comm, nranks, &commId, rank, dev);
+  return comm_init_rank(comm, nranks, &commId, rank, dev, nullptr);
 }
 
 VCCL_EXPORT ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks,
                                                 ncclUniqueId commId, int rank,
                                                 ncclConfig_t* config) {
-  if (config) {
-    if (config->magic != 0xcafebeef) {
-      VWARN("ncclCommInitRankConfig: config not initialised with NCCL_CONFIG_INITIALIZER");
-      return ncclInvalidArgument;
-    }
-    if (config->blocking != NCCL_CONFIG_UNDEF_INT && config->blocking == 0)
-      VINFO("non-blocking comm requested: this build always initialises blocking");
-  }
-  return ncclCommInitRank(comm, nranks, commId, rank);
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  return comm_init_rank(comm, nranks, &commId, rank, dev, config);
 }
 
 VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
@@ -479,7 +558,7 @@ VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
         res[i] = ncclUnhandledCudaError;
         return;
       }
-      res[i] = comm_init_rank(&comms[i], ndev, &id, i, d);
+      res[i] = comm_init_rank(&comms[i], ndev, &id, i, d, nullptr);
     });
   }
   for (auto& t : th) t.join();
@@ -561,6 +640,37 @@ VCCL_EXPORT ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
   NCCLCHECK(comm_check(comm, "ncclCommUserRank"));
   if (!rank) return ncclInvalidArgument;
   *rank = comm->rank;
+  return ncclSuccess;
+}
+
+// vccl_ext.h: run-time fence toggle and the epoch-wrap test hook.
+VCCL_EXPORT ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences) {
+  NCCLCHECK(comm_check(comm, "vcclCommSetFences"));
+  if (useFences != 0 && useFences != 1) return ncclInvalidArgument;
+  if (comm->nRanks < 2 || !comm->devComm) return ncclSuccess;
+  int old = -1;
+  (void)hipGetDevice(&old);
+  HIPCHECK(hipSetDevice(comm->device));
+  HIPCHECK(hipDeviceSynchronize());
+  HIPCHECK(hipMemcpy((char*)comm->devComm + offsetof(DevComm, useFences), &useFences, sizeof(int),
+                     hipMemcpyHostToDevice));
+  if (old >= 0) (void)hipSetDevice(old);
+  return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoch,
+                                                uint32_t directEpoch) {
+  NCCLCHECK(comm_check(comm, "vcclCommDebugSetEpochs"));
+  if (comm->nRanks < 2 || !comm->devComm) return ncclSuccess;
+  int old = -1;
+  (void)hipGetDevice(&old);
+  HIPCHECK(hipSetDevice(comm->device));
+  HIPCHECK(hipDeviceSynchronize());
+  HIPCHECK(hipMemcpy((char*)comm->devComm + offsetof(DevComm, llEpoch), &llEpoch, sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy((char*)comm->devComm + offsetof(DevComm, dEpoch), &directEpoch,
+                     sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (old >= 0) (void)hipSetDevice(old);
   return ncclSuccess;
 }
 

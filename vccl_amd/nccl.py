@@ -39,7 +39,10 @@ EXPORTED = [
     "ncclAllReduce", "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
-    "vcclCommLaunchStats", "vcclCommNetStats",
+    "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
+    "vcclRingPartition",
+    # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
+    "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
 ]
 ALGO_NAMES = {0: "ring", 1: "ll", 2: "direct", 3: "one_rank"}
 
@@ -100,6 +103,10 @@ def lib() -> ctypes.CDLL:
         "vcclHostToDevRedOp": [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(u64)],
         "vcclKernelTypeOf": [c_int, c_int],
         "vcclBootstrapAllGather": [ctypes.POINTER(ncclUniqueId), c_int, c_int, vp, c_size],
+        "vcclCommSetFences": [vp, c_int],
+        "vcclRingPartition": [c_int, c_size, c_int, c_int, c_int, c_size,
+                              ctypes.POINTER(ctypes.c_int64)],
+        "vcclCommDebugSetEpochs": [vp, ctypes.c_uint32, ctypes.c_uint32],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -160,6 +167,16 @@ def host_to_dev_redop(op: int, dtype: int, nranks: int) -> tuple[int, int]:
 
 def kernel_type_of(dev_op: int, dtype: int) -> int:
     return lib().vcclKernelTypeOf(dev_op, dtype)
+
+
+def ring_partition(coll: int, count: int, dtype: int, nranks: int, nchannels: int,
+                   slot_bytes: int) -> tuple[int, ...]:
+    """vcclRingPartition: (channelLo, channelHi, countLo, countMid, countHi,
+    chunkLo, chunkMid, chunkHi) of the ring's cbd partition (host only)."""
+    out = (ctypes.c_int64 * 8)()
+    check(lib().vcclRingPartition(coll, count, dtype, nranks, nchannels, slot_bytes, out),
+          "vcclRingPartition")
+    return tuple(out)
 
 
 def reduce_copy(dev_op: int, dtype: int, red_arg: int, srcs, dsts, n_elts: int, stream: int = 0,
@@ -253,6 +270,15 @@ class Comm:
         check(lib().vcclCommNetStats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)),
               "vcclCommNetStats")
         return a.value, b.value, n.value
+
+    def set_fences(self, on: bool):
+        """vcclCommSetFences: system-scope fences around every slot hand-off (VCCL_FENCES)."""
+        check(lib().vcclCommSetFences(self.handle, int(bool(on))), "vcclCommSetFences")
+
+    def debug_set_epochs(self, ll_epoch: int, direct_epoch: int):
+        """vcclCommDebugSetEpochs: overwrite the LL / direct call epochs (wrap tests)."""
+        check(lib().vcclCommDebugSetEpochs(self.handle, ll_epoch, direct_epoch),
+              "vcclCommDebugSetEpochs")
 
     def create_premulsum(self, scalar_ptr: int, dtype: int, residence: int) -> int:
         op = ctypes.c_int()
