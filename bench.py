@@ -29,6 +29,8 @@ import os
 import sys
 import time
 
+_T_START = time.perf_counter()  # before torch import: the line's wall time includes it
+
 import numpy as np
 import torch
 
@@ -400,6 +402,23 @@ def _hash32(lo, hi, device="cuda"):
     return h & 31
 
 
+_DIGEST = {}
+
+
+def _digest(lo, hi):
+    """_hash32 over [lo, hi), served from a per-device uint8 cache of the
+    prefix [0, 2^k) (computed once, the checks then cost one gather each)."""
+    dev = torch.cuda.current_device()
+    g = _DIGEST.get(dev)
+    if g is None or g.numel() < hi:
+        size = 1 << max(20, (hi - 1).bit_length())
+        g = torch.empty(size, dtype=torch.uint8, device="cuda")
+        for a in range(0, size, _SLICE):
+            g[a:a + _SLICE] = _hash32(a, min(size, a + _SLICE)).to(torch.uint8)
+        _DIGEST[dev] = g
+    return g[lo:hi]
+
+
 def _luts(world):
     v = torch.arange(32, device="cuda")
     per = [((v + 7 * r) & 31) - 16 for r in range(world)]
@@ -410,19 +429,21 @@ def pattern_fill(buf, r, world, base=0):
     """Fill the 1-D tensor `buf` with rank r's pattern for global indices
     [base, base + numel)."""
     per, _ = _luts(world)
+    lut = per[r].to(buf.dtype)
     n = buf.numel()
     for lo in range(0, n, _SLICE):
         hi = min(n, lo + _SLICE)
-        buf[lo:hi] = per[r][_hash32(base + lo, base + hi)].to(buf.dtype)
+        buf[lo:hi] = lut[_digest(base + lo, base + hi).long()]
 
 
 def pattern_ok(buf, world, base=0):
     """buf == the reduction of every rank's pattern over [base, base + numel)."""
     _, tot = _luts(world)
+    lut = tot.to(buf.dtype)
     n = buf.numel()
     for lo in range(0, n, _SLICE):
         hi = min(n, lo + _SLICE)
-        if not torch.equal(buf[lo:hi], tot[_hash32(base + lo, base + hi)].to(buf.dtype)):
+        if not torch.equal(buf[lo:hi], lut[_digest(base + lo, base + hi).long()]):
             return False
     return True
 
@@ -455,9 +476,18 @@ def check_ar(dist, comm, rank, world, nbytes, dtype="f32", algo=None):
     return _all_ok(dist, ok)
 
 
-def check_rs_ag(dist, comm, rank, world, nbytes, dtype="bf16"):
+def check_rs_ag(dist, comm, rank, world, nbytes, dtype="bf16", algo=None):
     """Reduce-scatter of an `nbytes` bucket, then all-gather of the shards back
-    (the ZeRO bucket path of config 4): (rs_ok, ag_ok) on every rank."""
+    (the ZeRO bucket path of config 4) on the path `algo` (None = the
+    library's choice): (rs_ok, ag_ok) on every rank."""
+    comm.set_algo(algo)
+    try:
+        return _check_rs_ag(dist, comm, rank, world, nbytes, dtype)
+    finally:
+        comm.set_algo(None)
+
+
+def _check_rs_ag(dist, comm, rank, world, nbytes, dtype):
     tdt = _TDT[dtype]
     n = nbytes // torch.tensor([], dtype=tdt).element_size()
     rc = n // world
@@ -544,7 +574,6 @@ def _flatten_ok(checks):
 
 
 def bench_allreduce(args):
-    t_line = time.perf_counter()
     dist, rank, world, comm = _dist_setup()
     sp = torch.cuda.current_stream().cuda_stream
     xgmi = peer_copy_bench(dist, rank, world) if not args.no_peer else None
@@ -584,6 +613,12 @@ def bench_allreduce(args):
         for S in EXTRA_GROUP_SIZES:
             plan[f"group16_{S}"] = ("group", {"nbytes": S, "k": 16})
         plan[f"rs_ag_bf16_{args.rs_ag_bytes}"] = ("rs_ag", {"nbytes": args.rs_ag_bytes})
+        plan[f"rs_ag_bf16_direct_{args.rs_ag_bytes}"] = ("rs_ag", {"nbytes": args.rs_ag_bytes,
+                                                                   "algo": "direct"})
+        for S in EXTRA_RSAG_SIZES:
+            for algo in (None, "ring"):
+                plan[f"rs_ag_f32_{algo or 'default'}_{S}"] = ("rs_ag", {"nbytes": S, "dtype": "f32",
+                                                                        "algo": algo})
     checks = run_checks(dist, comm, rank, world, plan)
     err = comm.async_error()
     comm.destroy()
@@ -593,7 +628,7 @@ def bench_allreduce(args):
         initall = initall_check(torch.cuda.device_count()) if rank == 0 else None
         dist.barrier()
     t_chk = time.perf_counter() - t_chk
-    line_s = time.perf_counter() - t_line
+    line_s = time.perf_counter() - _T_START
     last = rows[-1]
     links = {2: 1, 4: 3, 8: 7}.get(world, 1)
     measured_link = (xgmi or {}).get("one_peer_GBs")
@@ -619,7 +654,8 @@ def bench_allreduce(args):
                         "spec_peak": round(links * XGMI_LINK_GBS, 2),
                         "measured_peer_copy": xgmi},
            "correct": {"all": correct_all, **checks, "initall_single_process": initall,
-                       "check_s": round(t_chk, 2), "line_s": round(line_s, 2),
+                       "check_s": round(t_chk, 2),
+                       "line_s": round(line_s, 2),  # bench.py start (imports included) -> here
                        "check_frac": round(t_chk / line_s, 3),
                        "inputs": "integer-valued pattern (exact in any fold order), per timed path"}}
     if extras is not None:
@@ -633,6 +669,7 @@ def bench_allreduce(args):
 EXTRA_F32_SIZES = (8, 1 << 10, 8 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20)
 EXTRA_F16_SIZES = (8, 1 << 10, 16 << 10, 128 << 10)
 EXTRA_GROUP_SIZES = (4 << 10, 32 << 10)
+EXTRA_RSAG_SIZES = (64 << 10, 1 << 20, 8 << 20)  # whole bucket (n blocks), f32
 
 
 def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
@@ -707,36 +744,55 @@ def bench_extras(dist, comm, rank, world, args):
         comm.set_algo(None)
     try:
         ex["rs_ag_bf16"] = _rs_ag(dist, comm, rank, world, args.rs_ag_bytes, min(args.steps, 10), 2)
+        comm.set_algo("direct")
+        ex["rs_ag_bf16_direct"] = _rs_ag(dist, comm, rank, world, args.rs_ag_bytes,
+                                         min(args.steps, 10), 2)
     except Exception as e:  # noqa: BLE001
         ex["rs_ag_error"] = repr(e)
+    finally:
+        comm.set_algo(None)
+    try:  # small / mid buckets: the one-hop LL / direct RS + AG vs the ring
+        ex["rs_ag_f32_sizes"] = []
+        for S in EXTRA_RSAG_SIZES:
+            for algo in (None, "ring"):
+                comm.set_algo(algo)
+                ex["rs_ag_f32_sizes"].append(_rs_ag(dist, comm, rank, world, S, 20, 3, dtype="f32"))
+    except Exception as e:  # noqa: BLE001
+        ex["rs_ag_sizes_error"] = repr(e)
+    finally:
+        comm.set_algo(None)
     ex["async_error"] = comm.async_error()
     return ex
 
 
-def _rs_ag(dist, comm, rank, world, S, steps, warmup):
+def _rs_ag(dist, comm, rank, world, S, steps, warmup, dtype="bf16"):
+    """Reduce-scatter of an S-byte bucket (n blocks) then all-gather of the
+    shards back: busbw = (S / t) (n-1)/n each, and us per call."""
     sp = torch.cuda.current_stream().cuda_stream
-    n = S // 2
+    tdt, code = _TDT[dtype], _CODE[dtype]
+    n = S // torch.tensor([], dtype=tdt).element_size()
     rc = n // world
     g = torch.Generator(device="cuda").manual_seed(2000 + rank)
-    x = (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
-    shard = torch.empty(rc, dtype=torch.bfloat16, device="cuda")
+    x = (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt)
+    shard = torch.empty(rc, dtype=tdt, device="cuda")
     y = torch.empty_like(x)
 
     def rs():
-        comm.reduce_scatter(x.data_ptr(), shard.data_ptr(), rc, nccl.ncclBfloat16, nccl.ncclSum, sp)
+        comm.reduce_scatter(x.data_ptr(), shard.data_ptr(), rc, code, nccl.ncclSum, sp)
 
     def ag():
-        comm.all_gather(shard.data_ptr(), y.data_ptr(), rc, nccl.ncclBfloat16, sp)
+        comm.all_gather(shard.data_ptr(), y.data_ptr(), rc, code, sp)
     t_rs = _time_coll(dist, rs, steps, warmup)
     t_ag = _time_coll(dist, ag, steps, warmup)
     frac = (world - 1) / world
     del x, y, shard
     torch.cuda.empty_cache()
-    return {"bytes": S, "steps": steps, "rs_busbw": round(S * steps / t_rs / 1e9 * frac, 2),
+    return {"bytes": S, "dtype": dtype, "steps": steps,
+            "rs_busbw": round(S * steps / t_rs / 1e9 * frac, 2),
             "ag_busbw": round(S * steps / t_ag / 1e9 * frac, 2),
+            "rs_us": round(t_rs / steps * 1e6, 2), "ag_us": round(t_ag / steps * 1e6, 2),
             "ms_per_rs_ag": round((t_rs + t_ag) / steps * 1e3, 3),
-            "algo_rs": comm.coll_algo(1, rc, nccl.ncclBfloat16),
-            "algo_ag": comm.coll_algo(2, rc, nccl.ncclBfloat16)}
+            "algo_rs": comm.coll_algo(1, rc, code), "algo_ag": comm.coll_algo(2, rc, code)}
 
 
 def bench_rs_ag(args):

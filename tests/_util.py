@@ -4,8 +4,9 @@
 * floats, same fold order: bit-exact, except NaN compares by NaN-ness and, for
   min/max only, +0 == -0 (CUDA fminf / v_min_f32 leave the zero sign open);
 * floats, different fold order (multi-rank collectives): the tolerance stated
-  in SURVEY.md §8c —  sum: |y - y_ref| <= (n-1)*u*sum|x_i| + ulp(y)/2,
-  prod: <= ((1+u)^(n-1) - 1)*|y_ref| + ulp(y)/2.
+  in SURVEY.md §8c against the exact value —  sum: |y - exact| <=
+  (n-1)*u*sum|x_i| + ulp(y)/2, prod: <= ((1+u)^(n-1) - 1)*|exact| + ulp(y)/2 —
+  and twice the fold term against another order's computed result (VCCL's).
 """
 import numpy as np
 
@@ -49,21 +50,40 @@ def assert_bitexact(t, got, exp, minmax=False, what=""):
     assert bad.size == 0, f"{what}: {bad.size} mismatches, first at {bad[:5]}: got {gf[bad[:5]]} exp {ef[bad[:5]]}"
 
 
-def assert_fold_tolerance(t, op, got, exp, inputs, what=""):
-    """Order-independent check for multi-rank fp sum/prod."""
+def exact_f64(t, op, inputs):
+    """The exactly rounded-once reference in f64 of a sum / prod of n inputs
+    (exact for sums of <= 8 values of <= 24-bit significands; products carry
+    a negligible ~n * 2^-53 relative error)."""
+    xs = np.stack([to_f64(t, x) for x in inputs])
+    return xs.prod(axis=0) if op == 1 else xs.sum(axis=0)
+
+
+def assert_fold_tolerance(t, op, got, exp, inputs, what="", exp_is_exact=False):
+    """Order-independent check for multi-rank fp sum/prod.
+
+    Against the exact value (exp_is_exact=True, exp in f64): any fold order of
+    n inputs lands within the forward-error bound
+        sum:  |y - exact| <= (n-1) u sum|x_i| + ulp(y)/2
+        prod: |y - exact| <= ((1+u)^(n-1) - 1) |exact| + ulp(y)/2.
+    Against another fold order's computed result (e.g. VCCL's schedule on the
+    same inputs; exp in the storage type): both sit within that bound of the
+    exact value, so the allowed difference is twice the fold term."""
     if t not in FLOAT_TYPES or op in (2, 3):
         assert_bitexact(t, got, exp, minmax=op in (2, 3), what=what)
         return
     n = len(inputs)
     u = UNIT_ROUNDOFF[t]
-    g, e = to_f64(t, got), to_f64(t, exp)
+    g = to_f64(t, got)
+    e = np.asarray(exp, dtype=np.float64) if exp_is_exact else to_f64(t, exp)
     xs = np.stack([to_f64(t, x) for x in inputs])
     finite = np.isfinite(e) & np.isfinite(g)
     if op == 1:
         bound = ((1 + u) ** (n - 1) - 1) * np.abs(e)
     else:
         bound = (n - 1) * u * np.abs(xs).sum(axis=0)
-    bound = bound + np.abs(e) * u + 1e-300
+    if not exp_is_exact:
+        bound = 2 * bound
+    bound = bound + np.maximum(np.abs(e), np.abs(g)) * u + 1e-300
     ok = ~finite | (np.abs(g - e) <= bound)
     ok &= ~(np.isnan(g) ^ np.isnan(e))
     bad = np.nonzero(~ok)[0]

@@ -48,7 +48,33 @@ CASES = [
     ("ar_u8_max_mis_direct", "ar_mis", 2, 1, 3_000_001),
     ("ar_f64_sum_mis_direct", "ar_mis", 0, 8, 300_001),
     ("ar_f16_sum_mis_ll", "ar_mis", 0, 6, 20_001),
+    # fp sum / prod per path, checked bit-exactly against the path's own fold
+    # and within the §8c tolerance of VCCL's (exact value; VCCL's ring
+    # schedule on a reference geometry) — the north-star fp parity claim
+    ("ar_f32_prod_ll", "ar", 1, 7, 200_003),
+    ("ar_f16_prod_direct", "ar", 1, 6, 1_000_001),
+    ("ar_bf16_prod_ring", "ar", 1, 9, 3_000_001),
+    ("ar_f16_sum_ring", "ar", 0, 6, 2_600_001),
+    ("ar_bf16_sum_direct", "ar", 0, 9, 1_500_001),
+    ("rs_f16_prod", "rs", 1, 6, 30_001),
+    ("rs_bf16_sum", "rs", 0, 9, 70_001),
+    # one-hop direct reduce-scatter / all-gather (a block above the test
+    # geometry's 1 MiB LL slot; several inbox chunks), odd counts = blocks
+    # off 16-byte alignment
+    ("rs_f32_sum_direct", "rs", 0, 7, 300_001),
+    ("rs_bf16_avg_direct_odd", "rs", 4, 9, 700_001),
+    ("rs_i8_min_direct_odd", "rs", 3, 0, 1_500_003),
+    ("rs_f16_prod_direct", "rs", 1, 6, 600_001),
+    ("ag_f32_direct", "ag", 0, 7, 300_001),
+    ("ag_u8_direct_odd", "ag", 0, 1, 1_500_007),
 ]
+
+# VCCL's ring schedule on the geometry its own tuner would pick on an 8-GPU
+# NVLink node (one ring order on every channel, 16 channels, NCCL_BUFFSIZE
+# 4 MiB): the "VCCL result" fp outputs are held to within tolerance.
+VCCL_REF_CHANNELS = 16
+VCCL_REF_SLOT = 512 << 10
+TOLERANCE_OPS = (0, 1)  # sum, prod
 
 
 def mis_offsets(dt):
@@ -81,6 +107,9 @@ def gen_input(case_idx, rank, n_ranks):
         if op == 1:  # keep products interesting
             return rng.integers(1, 4, total).astype(npdt)
         return rng.integers(0, 2**62, total, dtype=np.int64).astype(np.uint64).view(np.int64).astype(npdt)
+    if op == 1 and dt in (6, 7, 8, 9):  # products of n values stay normal
+        x = (rng.uniform(0.5, 2.0, total) * rng.choice([-1.0, 1.0], total)).astype(np.float32)
+        return O.f32_to_bf16_bits(x) if dt == 9 else x.astype(O.NP_DTYPE[dt])
     if dt == 9:
         return O.f32_to_bf16_bits(rng.uniform(-1, 1, total).astype(np.float32))
     if dt in (10, 11):  # fp8 codes of uniform values (every code of the range)
@@ -146,6 +175,25 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
         return _ring.expected_reducescatter(op, dt, ins, nch)
     full = np.concatenate(ins)
     return [full] * n_ranks
+
+
+def inputs(case_idx, n_ranks):
+    return [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
+
+
+def vccl_reference(case_idx, n_ranks):
+    """VCCL's own result for a float sum/prod case: its ring schedule (cbd
+    partition, chunking, runRing fold) on VCCL_REF_CHANNELS identity-ring
+    channels; None for cases outside the tolerance check."""
+    name, coll, op, dt, count = CASES[case_idx]
+    if dt not in (6, 7, 8, 9) or op not in TOLERANCE_OPS or coll == "ag":
+        return None
+    ins = inputs(case_idx, n_ranks)
+    ring = [list(range(n_ranks))]
+    if coll == "rs":
+        return _ring.expected_reducescatter(op, dt, ins, VCCL_REF_CHANNELS, VCCL_REF_SLOT, rings=ring)
+    e = _ring.expected_allreduce(op, dt, ins, VCCL_REF_CHANNELS, VCCL_REF_SLOT, rings=ring)
+    return [e] * n_ranks
 
 
 def out_count(case_idx, n_ranks):

@@ -21,7 +21,7 @@ import torch
 
 from tests import _ring
 from tests import ring_cases as RC
-from tests._util import assert_bitexact
+from tests._util import assert_bitexact, assert_fold_tolerance, exact_f64
 
 pytestmark = pytest.mark.gpu
 
@@ -45,10 +45,24 @@ DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in ch
 
 
 def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST):
+    """Bit-exact against the path's own fold order (the ring's IS VCCL's
+    schedule on our rings and channels); for fp sum / prod additionally
+    within the §8c tolerance of the exact value and of VCCL's result on its
+    reference geometry (RC.vccl_reference)."""
     name, coll, op, dt, count = RC.CASES[ci]
     exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
+    vref = RC.vccl_reference(ci, n)
+    if vref is not None:
+        ins = RC.inputs(ci, n)
+        cnt = outs[0].size
+        for r in range(n):
+            blk = [x[r * cnt:(r + 1) * cnt] for x in ins] if coll == "rs" else ins
+            assert_fold_tolerance(dt, op, outs[r], exact_f64(dt, op, blk), blk, exp_is_exact=True,
+                                  what=f"{name} n={n} rank {r} vs exact")
+            assert_fold_tolerance(dt, op, outs[r], vref[r], blk,
+                                  what=f"{name} n={n} rank {r} vs VCCL ring schedule")
 
 
 def test_duplicate_device_rejected():
@@ -59,16 +73,25 @@ def test_duplicate_device_rejected():
 
 
 def test_algorithm_choice(monkeypatch):
-    """Library defaults: LL up to 64 KiB (2 ranks), direct above; RS / AG on
-    the ring; NCCL_ALGO / NCCL_PROTO force one (vcclCommCollAlgo)."""
+    """Library defaults: AR LL up to 64 KiB (2 ranks), direct above; RS / AG
+    LL / direct / ring by bucket size; NCCL_ALGO / NCCL_PROTO force one
+    (vcclCommCollAlgo)."""
     monkeypatch.setenv("VCCL_ALLOW_SHARED_DEVICE", "1")
-    for k in ("NCCL_ALGO", "NCCL_PROTO", "VCCL_LL_THRESHOLD", "VCCL_DIRECT_THRESHOLD"):
+    for k in ("NCCL_ALGO", "NCCL_PROTO", "VCCL_LL_THRESHOLD", "VCCL_DIRECT_THRESHOLD",
+              "VCCL_LL_RSAG_THRESHOLD", "VCCL_DIRECT_RSAG_THRESHOLD"):
         monkeypatch.delenv(k, raising=False)
+    # RS / AG: one-hop LL while the bucket (n blocks) is <= n x the AR LL
+    # threshold, one-hop direct up to 64 MiB, the ring above.
     cases = {None: {(0, 16 << 10): "ll", (0, 17 << 10): "direct", (0, 1 << 28): "direct",
-                    (1, 1 << 10): "ring", (2, 1 << 10): "ring"},
-             "Ring": {(0, 1 << 10): "ring", (0, 1 << 20): "ring"},
-             "Tree": {(0, 1 << 10): "ll", (0, 1 << 20): "ring"},
-             "Direct": {(0, 1 << 10): "direct", (0, 1 << 28): "direct", (1, 1 << 10): "ring"}}
+                    (1, 1 << 10): "ll", (2, 1 << 10): "ll", (1, 16 << 10): "ll",
+                    (1, 17 << 10): "direct", (2, 1 << 20): "direct", (1, 1 << 23): "direct",
+                    (1, (1 << 23) + 4): "ring", (2, 1 << 26): "ring"},
+             "Ring": {(0, 1 << 10): "ring", (0, 1 << 20): "ring", (1, 1 << 10): "ring",
+                      (2, 1 << 20): "ring"},
+             "Tree": {(0, 1 << 10): "ll", (0, 1 << 20): "ring", (1, 1 << 10): "ll",
+                      (2, 1 << 26): "ring"},
+             "Direct": {(0, 1 << 10): "direct", (0, 1 << 28): "direct", (1, 1 << 10): "direct",
+                        (2, 1 << 10): "direct", (2, 1 << 26): "ring"}}
     for algo, expect in cases.items():
         if algo is None:
             monkeypatch.delenv("NCCL_ALGO", raising=False)

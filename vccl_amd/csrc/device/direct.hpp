@@ -34,6 +34,11 @@
 // raised only after reading every region (0, *) block b.  Region (1, o) is
 // rewritten by o only after o received the reader's phase-1 data of the next
 // chunk, which workgroup b of the reader sends only after its own phase 3.
+// The one-hop reduce-scatter / all-gather below write only (0, *) regions
+// and guard reuse with explicit acknowledgements; any of the three kernels
+// may follow any other on the same inbox (a peer one call ahead writes only
+// (0, *) regions, which the previous call has finished reading before that
+// peer could complete it).
 #pragma once
 #include "ll.hpp"
 #include "reduce_copy.hpp"
@@ -70,6 +75,11 @@ struct DirectWork {
   int64_t chunkElts;     // elements per chunk (last one shorter)
   int64_t blkElts;       // elements per block, the same for every chunk
   int64_t regionBytes;   // bytes per (phase, rank) inbox region
+  // Reduce-scatter: VCCL's cbd channel partition of the recvcount block
+  // (host/enqueue.cc cbd_schedule, the ring's own): channel c of
+  // [channelLo, channelHi] folds on ring c mod nRings (DevComm::rsOrder), so
+  // the direct path reproduces the ring's (= VCCL's) fold order exactly.
+  CbdLite cbd;
 };
 
 // Shard length of a chunk of `cc` elements: ceil(cc / n) in 16-byte units.
@@ -139,6 +149,15 @@ __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)
     if (nS == 1 && nD == 1) {
       reduce_copy<Fn, 1, 1, 2, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads);
       return;
+    }
+    if (nD == 1 && nS > 1) {  // reduce-scatter fold: n -> 1
+      switch (nS) {
+        case 2: reduce_copy<Fn, 2, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 3: reduce_copy<Fn, 3, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 4: reduce_copy<Fn, 4, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 8: reduce_copy<Fn, 8, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        default: break;
+      }
     }
     if (nS == nD) {
       switch (nS) {
@@ -361,6 +380,152 @@ __device__ void direct_allreduce(const DirectWork& w) {
       }
     }
     __syncthreads();  // the region reads of this chunk precede the next chunk's posts
+  }
+  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
+}
+
+// ------------------------------------------------------------ reduce-scatter
+// One-hop reduce-scatter over the full mesh (the mid-range slot of VCCL's
+// tuner, LL128 ring, prims_ll128.h:176-324 / enqueue.cc:2032): my block p of
+// the input goes straight to rank p.  Per chunk of the recvcount block:
+//   phase 1 (scatter): block b of my contribution to every peer p's block
+//            -> p's inbox region (0, me); raise flag (0, me, b) at p;
+//   phase 2 (fold):    wait for the n-1 flags (0, *, b); fold my block b from
+//            the n-1 regions and my own input, per channel part in the order
+//            of that part's ring (DirectPeers::rsOrder, the ring's fold), preOp
+//            on every input, postOp once, into my output; raise the
+//            acknowledgement (1, me, b) at every peer;
+//   phase 3 (ack):     wait for the n-1 acknowledgements (1, *, b): every peer
+//            has consumed what I wrote into it, so the next chunk (or call)
+//            may overwrite region (0, me) there.
+// count = recvcount; shards are the n blocks of the input (stride count).
+template <class Fn>
+__device__ void direct_reducescatter(const DirectWork& w) {
+  using T = typename Fn::EltType;
+  constexpr int64_t esz = (int64_t)sizeof(T);
+  __shared__ int shFail;
+  const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
+  uint32_t e = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const DirectPeers& P = *w.peers;
+  const int n = w.nRanks, me = w.rank, b = blockIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int64_t count = (int64_t)w.count;
+  char* myBuf = P.buf[me];
+  const char* myFlags = P.flags[me];
+  const char* in = (const char*)w.sendbuff;
+  char* out = (char*)w.recvbuff;
+  if (tid == 0) shFail = 0;
+  __syncthreads();
+  for (int c = 0; c < w.nChunks; c++) {
+    e = epoch_after(e);
+    if (shFail) continue;
+    const int64_t c0 = (int64_t)c * w.chunkElts;
+    const int64_t cc = count - c0 < w.chunkElts ? count - c0 : w.chunkElts;
+    const int64_t lo = c0 + (int64_t)b * w.blkElts;           // my block b, element range
+    const int64_t hi = lo + w.blkElts < c0 + cc ? lo + w.blkElts : c0 + cc;
+    const int64_t len = hi > lo ? hi - lo : 0;
+    const int64_t rOff = (int64_t)b * w.blkElts * esz;          // its offset in a region
+    // Phase 1: scatter (workgroup b starts at peer offset 1 + b mod (n-1)).
+    for (int i = 0; i < n - 1; i++) {
+      const int k = 1 + (b + i) % (n - 1);
+      const int p = me + k < n ? me + k : me + k - n;
+      const char* s[kDirectMaxRanks] = {in + ((int64_t)p * count + lo) * esz};
+      char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + rOff};
+      direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+    }
+    direct_post(w, P, 0, b, e);
+    // Phase 2: fold per channel part in its ring's order.
+    if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
+      for (int64_t cur = lo; cur < hi;) {
+        int64_t end;
+        const int ch = cbd_channel_of(w.cbd, cur, &end);
+        end = end < hi ? end : hi;
+        const int8_t* order = w.comm->rsOrder[ch % w.comm->nRings];
+        const int64_t ro = rOff + (cur - lo) * esz;
+        const char* s[kDirectMaxRanks];
+        char* d[kDirectMaxRanks] = {out + cur * esz};
+#pragma unroll
+        for (int j = 0; j < kDirectMaxRanks; j++) {
+          const int q = j < n ? order[j] : me;
+          s[j] = q == me ? in + ((int64_t)me * count + cur) * esz
+                         : myBuf + direct_region_off(0, q, n, w.regionBytes) + ro;
+        }
+        direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, 1,
+                                                           end - cur, tid, nt);
+        cur = end;
+      }
+    }
+    direct_post(w, P, 1, b, e);
+    // Phase 3: the peers' acknowledgements for this chunk.
+    (void)direct_wait(w, myFlags, 1, b, e, &shFail);
+  }
+  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
+}
+
+// ---------------------------------------------------------------- all-gather
+// One-hop all-gather (byte copies, as the reference runs AG as int8,
+// enqueue.cc:2398-2404): count = bytes per rank.  Per chunk:
+//   phase 1 (deliver): block b of my input -> every peer's region (0, me);
+//            raise (0, me, b) there;
+//   phase 2 (gather):  wait for (0, *, b); copy every rank's block b (mine
+//            from my input) into the output at rank * count; raise the
+//            acknowledgement (1, me, b) at every peer;
+//   phase 3 (ack):     wait for (1, *, b) before the next chunk (or call)
+//            overwrites region (0, me) at the peers.
+// Data goes through region (0, *) like the other collectives' first phase:
+// a peer that finished the previous call may start this one while I still
+// read (1, *) regions of a direct all-reduce's phase 3, never (0, *) ones
+// (its all-reduce could only finish after my phase-2 post, i.e. after my
+// last read of (0, *)).
+__device__ __forceinline__ void direct_allgather(const DirectWork& w) {
+  using Fn = FnCopy<uint8_t>;
+  const Fn fn(0);
+  __shared__ int shFail;
+  uint32_t e = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const DirectPeers& P = *w.peers;
+  const int n = w.nRanks, me = w.rank, b = blockIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int64_t count = (int64_t)w.count;
+  char* myBuf = P.buf[me];
+  const char* myFlags = P.flags[me];
+  const char* in = (const char*)w.sendbuff;
+  char* out = (char*)w.recvbuff;
+  if (tid == 0) shFail = 0;
+  __syncthreads();
+  for (int c = 0; c < w.nChunks; c++) {
+    e = epoch_after(e);
+    if (shFail) continue;
+    const int64_t c0 = (int64_t)c * w.chunkElts;
+    const int64_t cc = count - c0 < w.chunkElts ? count - c0 : w.chunkElts;
+    const int64_t lo = c0 + (int64_t)b * w.blkElts;
+    const int64_t hi = lo + w.blkElts < c0 + cc ? lo + w.blkElts : c0 + cc;
+    const int64_t len = hi > lo ? hi - lo : 0;
+    const int64_t rOff = (int64_t)b * w.blkElts;
+    // Phase 1: one read of my block, n-1 write-through stores (aligned regions).
+    {
+      const char* s[kDirectMaxRanks] = {in + lo};
+      char* d[kDirectMaxRanks];
+#pragma unroll
+      for (int j = 0; j < kDirectMaxRanks; j++) {
+        const int p = me + 1 + j < n ? me + 1 + j : me + 1 + j - n;
+        d[j] = j < n - 1 ? P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + rOff : nullptr;
+      }
+      direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, n - 1, len, tid, nt);
+    }
+    direct_post(w, P, 0, b, e);
+    // Phase 2: gather every rank's block b into the output.
+    if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
+      for (int k = 0; k < n; k++) {
+        const int o = me + k < n ? me + k : me + k - n;
+        const char* s[kDirectMaxRanks] = {o == me ? in + lo
+                                                  : myBuf + direct_region_off(0, o, n, w.regionBytes) + rOff};
+        char* d[kDirectMaxRanks] = {out + (int64_t)o * count + lo};
+        if (o == me && s[0] == d[0]) continue;  // in place: my block is already there
+        direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+      }
+    }
+    direct_post(w, P, 1, b, e);
+    (void)direct_wait(w, myFlags, 1, b, e, &shFail);
   }
   epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
 }

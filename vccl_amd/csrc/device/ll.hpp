@@ -51,6 +51,11 @@ struct LLWork {
   char* localBuf;          // my LL buffer: [2 parities][nRanks sources][linesPerSlot] lines
   char* peerBuf[kMaxRanks];  // every rank's LL buffer mapped here (peerBuf[rank] = local)
   LLPart parts[kLLMaxParts];
+  // Reduce-scatter / all-gather (one part): parts[0] = {input, output, bytes
+  // of ONE rank's block, 0}; nLines = lines of one block.  Reduce-scatter
+  // folds each line on the ring of its channel (VCCL's cbd partition of the
+  // block, DevComm::rsOrder).
+  CbdLite cbd;
 };
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -236,6 +241,115 @@ __device__ void ll_allreduce(const LLWork& w) {
     if (!ok) break;
     if (Fn::kPostOp) acc = ll_apply(fn, acc, 0, 2);
     ll_store8(part.recv, pl, part.nbytes, acc);
+  }
+  ll_epoch_retire(w.comm, e);
+}
+
+// ------------------------------------------------------------ reduce-scatter
+// One-hop LL reduce-scatter: line l of my contribution to rank p's block goes
+// to p's slot (parity, me); p folds its block line by line from the n-1 slots
+// and its own input, in the order of the line's ring (lines never straddle a
+// channel part: parts are 16-byte multiples of the block, lines 8 bytes).
+template <class Fn>
+__device__ void ll_reducescatter(const LLWork& w) {
+  using T = typename Fn::EltType;
+  const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
+  const uint32_t e = ll_epoch_of(w.comm);
+  const int parity = (int)(e & 1);
+  const int n = w.nRanks, me = w.rank;
+  const int64_t nLines = w.nLines, nb = w.parts[0].nbytes;
+  const char* in = w.parts[0].send;
+  char* out = w.parts[0].recv;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gthreads = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t l = gtid; l < nLines; l += gthreads) {
+    for (int k = 1; k < n; k++) {
+      const int p = me + k < n ? me + k : me + k - n;
+      const uint64_t v = ll_load8(in + (int64_t)p * nb, l, nb);
+      u32x4 line;
+      line.x = (uint32_t)v;
+      line.y = e;
+      line.z = (uint32_t)(v >> 32);
+      line.w = e;
+      const SysAddr d = sys_addr(w.peerBuf[p] + ll_slot_off(parity, me, n, w.linesPerSlot) + l * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(line, d.r, d.voff, 0, kSysAux);
+    }
+  }
+  bool ok = true;
+  for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
+    int64_t end;
+    const int ch = cbd_channel_of(w.cbd, l * 8 / (int64_t)sizeof(T), &end);
+    const int8_t* order = w.comm->rsOrder[ch % w.comm->nRings];
+    u32x4 v[kOrderMaxRanks];
+#pragma unroll
+    for (int j = 0; j < kOrderMaxRanks; j++) {  // every peer line of l in flight at once
+      const int q = j < n ? order[j] : me;
+      if (q != me) {
+        const SysAddr a = sys_addr(w.localBuf + ll_slot_off(parity, q, n, w.linesPerSlot) + l * 16);
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(a.r, a.voff, 0, kSysAux);
+      }
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < kOrderMaxRanks; j++) {
+      if (j >= n) break;
+      const int q = order[j];
+      uint64_t x;
+      if (q == me) {
+        x = ll_load8(in + (int64_t)me * nb, l, nb);
+      } else if (v[j].y == e && v[j].w == e) {
+        x = (uint64_t)v[j].x | ((uint64_t)v[j].z << 32);
+      } else {
+        ok = ll_read_line(w.localBuf + ll_slot_off(parity, q, n, w.linesPerSlot) + l * 16, e, w.comm,
+                          &x);
+        if (!ok) break;
+      }
+      if (Fn::kPreOp && w.preOp) x = ll_apply(fn, 0, x, 1);
+      acc = j == 0 ? x : ll_apply(fn, acc, x, 0);
+    }
+    if (!ok) break;
+    if (Fn::kPostOp) acc = ll_apply(fn, acc, 0, 2);
+    ll_store8(out, l, nb, acc);
+  }
+  ll_epoch_retire(w.comm, e);
+}
+
+// ---------------------------------------------------------------- all-gather
+// One-hop LL all-gather (bytes): my block's lines go to every peer's slot
+// (parity, me); every rank copies each rank's block out of its slots (its own
+// from its input) to output + rank * bytes.
+__device__ inline void ll_allgather(const LLWork& w) {
+  const uint32_t e = ll_epoch_of(w.comm);
+  const int parity = (int)(e & 1);
+  const int n = w.nRanks, me = w.rank;
+  const int64_t nLines = w.nLines, nb = w.parts[0].nbytes;
+  const char* in = w.parts[0].send;
+  char* out = w.parts[0].recv;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gthreads = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t l = gtid; l < nLines; l += gthreads) {
+    const uint64_t v = ll_load8(in, l, nb);
+    u32x4 line;
+    line.x = (uint32_t)v;
+    line.y = e;
+    line.z = (uint32_t)(v >> 32);
+    line.w = e;
+    for (int k = 1; k < n; k++) {
+      const int p = me + k < n ? me + k : me + k - n;
+      const SysAddr d = sys_addr(w.peerBuf[p] + ll_slot_off(parity, me, n, w.linesPerSlot) + l * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(line, d.r, d.voff, 0, kSysAux);
+    }
+    if (out + (int64_t)me * nb != in) ll_store8(out + (int64_t)me * nb, l, nb, v);
+  }
+  bool ok = true;
+  for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
+    for (int k = 1; k < n; k++) {
+      const int q = me + k < n ? me + k : me + k - n;
+      uint64_t x;
+      ok = ll_read_line(w.localBuf + ll_slot_off(parity, q, n, w.linesPerSlot) + l * 16, e, w.comm, &x);
+      if (!ok) break;
+      ll_store8(out + (int64_t)q * nb, l, nb, x);
+    }
   }
   ll_epoch_retire(w.comm, e);
 }

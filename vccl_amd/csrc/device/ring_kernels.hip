@@ -1,6 +1,8 @@
-// Collective kernels for ONE kernel element type (VCCL_KT): ring all-reduce
-// and reduce-scatter per reduction functor, plus (in the K_U8 unit) the
-// type-agnostic all-gather; the one-shot LL and two-shot direct all-reduce.  One workgroup per channel (enqueue.cc:1576-1666).
+// Collective kernels for ONE kernel element type (VCCL_KT): per reduction
+// functor the ring all-reduce / reduce-scatter (one workgroup per channel,
+// enqueue.cc:1576-1666), the one-shot LL and the direct (two-shot all-reduce,
+// one-hop reduce-scatter) kernels; in the K_U8 unit also the type-agnostic
+// all-gathers (ring, LL, direct).
 #include <hip/hip_runtime.h>
 
 #include "direct.hpp"
@@ -45,14 +47,30 @@ template <class Fn>
 __global__ __launch_bounds__(256) void k_ll_allreduce(LLWork w) {
   ll_allreduce<Fn>(w);
 }
+template <class Fn>
+__global__ __launch_bounds__(256) void k_ll_reducescatter(LLWork w) {
+  ll_reducescatter<Fn>(w);
+}
+template <int K>  // instantiated in the K_U8 unit only (byte copies)
+__global__ __launch_bounds__(256) void k_ll_allgather(LLWork w) { ll_allgather(w); }
 
 template <>
-hipError_t ll_launch<VCCL_KT>(int devOp, const LLWork& w, int grid, hipStream_t stream) {
+hipError_t ll_launch<VCCL_KT>(int coll, int devOp, const LLWork& w, int grid, hipStream_t stream) {
   using T = typename KTypeOf<VCCL_KT>::T;
+  if (coll == kCollAllGather) {
+    if constexpr (VCCL_KT == K_U8) {
+      hipLaunchKernelGGL(k_ll_allgather<K_U8>, dim3(grid), dim3(256), 0, stream, w);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   hipError_t err = hipErrorInvalidValue;
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
-      hipLaunchKernelGGL((k_ll_allreduce<Fn>), dim3(grid), dim3(256), 0, stream, w);
+      if (coll == kCollAllReduce)
+        hipLaunchKernelGGL((k_ll_allreduce<Fn>), dim3(grid), dim3(256), 0, stream, w);
+      else
+        hipLaunchKernelGGL((k_ll_reducescatter<Fn>), dim3(grid), dim3(256), 0, stream, w);
       err = hipGetLastError();
     }
   });
@@ -63,14 +81,33 @@ template <class Fn>
 __global__ __launch_bounds__(kDirectThreads) void k_direct_allreduce(DirectWork w) {
   direct_allreduce<Fn>(w);
 }
+template <class Fn>
+__global__ __launch_bounds__(kDirectThreads) void k_direct_reducescatter(DirectWork w) {
+  direct_reducescatter<Fn>(w);
+}
+template <int K>  // instantiated in the K_U8 unit only (byte copies)
+__global__ __launch_bounds__(kDirectThreads) void k_direct_allgather(DirectWork w) {
+  direct_allgather(w);
+}
 
 template <>
-hipError_t direct_launch<VCCL_KT>(int devOp, const DirectWork& w, hipStream_t stream) {
+hipError_t direct_launch<VCCL_KT>(int coll, int devOp, const DirectWork& w, hipStream_t stream) {
   using T = typename KTypeOf<VCCL_KT>::T;
+  if (coll == kCollAllGather) {
+    if constexpr (VCCL_KT == K_U8) {
+      hipLaunchKernelGGL(k_direct_allgather<K_U8>, dim3(w.nBlocks), dim3(kDirectThreads), 0, stream, w);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   hipError_t err = hipErrorInvalidValue;
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
-      hipLaunchKernelGGL((k_direct_allreduce<Fn>), dim3(w.nBlocks), dim3(kDirectThreads), 0, stream, w);
+      if (coll == kCollAllReduce)
+        hipLaunchKernelGGL((k_direct_allreduce<Fn>), dim3(w.nBlocks), dim3(kDirectThreads), 0, stream, w);
+      else
+        hipLaunchKernelGGL((k_direct_reducescatter<Fn>), dim3(w.nBlocks), dim3(kDirectThreads), 0,
+                           stream, w);
       err = hipGetLastError();
     }
   });

@@ -15,13 +15,15 @@ constexpr int kRingUnroll = 2;
 template <int K>
 hipError_t ring_launch(int coll, int devOp, const RingWork& w, int nthreads, hipStream_t stream);
 
-// One-shot LL all-reduce (ll.hpp): 256-thread workgroups, `grid` of them.
+// One-hop LL collectives (ll.hpp): 256-thread workgroups, `grid` of them.
+// All-gather only in the K_U8 unit (byte copies).
 template <int K>
-hipError_t ll_launch(int devOp, const LLWork& w, int grid, hipStream_t stream);
+hipError_t ll_launch(int coll, int devOp, const LLWork& w, int grid, hipStream_t stream);
 
-// Two-shot direct all-reduce (direct.hpp): w.nBlocks workgroups of
-// kDirectThreads threads.
+// Direct collectives over the full mesh (direct.hpp): two-shot all-reduce,
+// one-hop reduce-scatter / all-gather; w.nBlocks workgroups of
+// kDirectThreads threads.  All-gather only in the K_U8 unit.
 template <int K>
-hipError_t direct_launch(int devOp, const DirectWork& w, hipStream_t stream);
+hipError_t direct_launch(int coll, int devOp, const DirectWork& w, hipStream_t stream);
 
 }  // namespace vccl

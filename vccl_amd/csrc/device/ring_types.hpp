@@ -20,6 +20,8 @@ constexpr int kSteps = 8;            // NCCL_STEPS (device.h:24)
 constexpr int kMaxRanks = 64;
 constexpr int kMaxChannels = 64;     // MAXCHANNELS (device.h:62)
 constexpr int kFlagStride = 128;     // bytes between flags (one line each)
+constexpr int kOrderMaxRings = 8;    // ring sets of SURVEY.md Appendix D: 7 (n=8), 6 (n=4), 1
+constexpr int kOrderMaxRanks = 8;
 // Slot stride = slotBytes + kSlotPad: RS / AG place a chunk at byte offset
 // (logical offset mod 16) inside its slot, so the slot shares the user
 // block's misalignment and the copy stays on 16-byte packs (ring.hpp).
@@ -65,7 +67,44 @@ struct DevComm {
   // Same scheme for the two-shot direct all-reduce (direct.hpp).
   uint32_t dEpoch;
   uint32_t dDone;
+  // This rank's reduce-scatter fold order on each ring of the comm's ring
+  // set: rsOrder[k][j] = the rank at ring-k position (pos(me) + 1 + j) mod n,
+  // the order VCCL's ring reduce-scatter folds my block in on a channel of
+  // ring k (reduce_scatter.h:39-53: from my ring successor around to me).
+  // Channel c runs on ring c mod nRings.  The one-hop LL / direct
+  // reduce-scatters (n <= kOrderMaxRanks) fold in the same order.
+  int nRings;
+  int8_t rsOrder[kOrderMaxRings][kOrderMaxRanks];
 };
+
+// The part of VCCL's cbd partition a reduce-scatter needs to know which
+// channel (hence ring, hence fold order) an element of the block is on.
+struct CbdLite {
+  int channelLo, channelHi;
+  int64_t countLo, countMid, count;  // count = the whole block (recvcount)
+};
+
+// ncclCollCbdPart (device.h:297-323) inverted: the channel of element i and
+// the end of that channel's part.
+__host__ __device__ inline int cbd_channel_of(const CbdLite& p, int64_t i, int64_t* end) {
+  if (p.channelHi == p.channelLo) {
+    *end = p.count;
+    return p.channelLo;
+  }
+  if (i < p.countLo) {
+    *end = p.countLo;
+    return p.channelLo;
+  }
+  const int64_t nMid = p.channelHi - p.channelLo - 1;
+  const int64_t j = i - p.countLo;
+  if (p.countMid > 0 && j < nMid * p.countMid) {
+    const int64_t m = j / p.countMid;
+    *end = p.countLo + (m + 1) * p.countMid;
+    return p.channelLo + 1 + (int)m;
+  }
+  *end = p.count;
+  return p.channelHi;
+}
 
 // Per-launch work descriptor (kernel argument, by value).
 struct RingWork {

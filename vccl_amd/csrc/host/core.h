@@ -121,6 +121,8 @@ struct ncclComm {
   char* dBuf = nullptr;
   char* dFlags = nullptr;      // kDirectFlagBytes of epoch flags
   size_t directMaxBytes = 0;   // largest all-reduce carried by the direct path
+  size_t llRsAgMaxBytes = 0;   // largest RS / AG bucket (n blocks) on the one-hop LL path
+  size_t directRsAgMaxBytes = 0;  // ... and on the one-hop direct path
   int64_t dRegionBytes = 0;
   int directMaxBlocks = 0;
   vccl::DirectPeers* dPeers = nullptr;  // device-resident peer table

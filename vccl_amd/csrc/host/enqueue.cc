@@ -405,10 +405,40 @@ static ncclResult_t launch_ring(const Task& t) {
   return ncclSuccess;
 }
 
-// One-shot LL all-reduce for small buckets (ll.hpp); the chain-tree fold.
-// `ts` holds 1 .. kLLMaxParts all-reduces of one comm with the same type and
-// op (ll_fusable) whose lines fit one slot; they run as one launch on
-// ts[0].stream (the caller orders the other streams around it).
+// Dispatch a typed launcher over the kernel element type.
+template <class F>
+static hipError_t by_kernel_type(int kt, F&& f) {
+  switch (kt) {
+    case K_U8: return f.template operator()<K_U8>();
+    case K_U32: return f.template operator()<K_U32>();
+    case K_U64: return f.template operator()<K_U64>();
+    case K_F16: return f.template operator()<K_F16>();
+    case K_F32: return f.template operator()<K_F32>();
+    case K_F64: return f.template operator()<K_F64>();
+    case K_BF16: return f.template operator()<K_BF16>();
+    case K_F8E4M3: return f.template operator()<K_F8E4M3>();
+    case K_F8E5M2: return f.template operator()<K_F8E5M2>();
+  }
+  return hipErrorInvalidValue;
+}
+
+static int dev_coll(int coll) {
+  return coll == kAllReduce ? kCollAllReduce : coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
+}
+
+// The cbd partition of a reduce-scatter's block, for the one-hop LL / direct
+// reduce-scatters' per-channel fold order (the ring's own, cbd_schedule).
+static CbdLite rs_cbd(const ncclComm* comm, const Task& t) {
+  const CbdPlan p = cbd_schedule(kReduceScatter, (int64_t)t.count, type_size(t.datatype), comm->nRanks,
+                                 comm->nChannels, comm->slotBytes);
+  return CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)t.count};
+}
+
+// One-hop LL collectives.  All-reduce: `ts` holds 1 .. kLLMaxParts calls of
+// one comm with the same type and op (ll_fusable) whose lines fit one slot;
+// they run as one launch on ts[0].stream (the caller orders the other
+// streams around it).  Reduce-scatter / all-gather: one call; a slot holds
+// one rank's block.
 static int64_t ll_lines_of(const Task& t) {
   return ((int64_t)t.count * type_size(t.datatype) + 7) / 8;
 }
@@ -426,7 +456,8 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   w.linesPerSlot = comm->llLines;
   w.localBuf = comm->llBuf;
   for (int r = 0; r < comm->nRanks; r++) w.peerBuf[r] = comm->llPeer[r];
-  if (nTasks < 1 || nTasks > kLLMaxParts) return ncclInternalError;
+  if (nTasks < 1 || nTasks > kLLMaxParts || (t.coll != kAllReduce && nTasks != 1))
+    return ncclInternalError;
   int64_t lines = 0;
   for (int i = 0; i < nTasks; i++) {
     w.parts[i].send = (const char*)ts[i].sendbuff;
@@ -437,8 +468,9 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   }
   w.nParts = nTasks;
   w.nLines = lines;
+  if (t.coll == kReduceScatter) w.cbd = rs_cbd(comm, t);
   if (lines > comm->llLines) return ncclInternalError;
-  const int kt = kernel_type_of(t.devOp, (int)t.datatype);
+  const int kt = t.coll == kAllGather ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
   // A bounded grid (<= VCCL_LL_MAX_BLOCKS 256-thread workgroups, each thread
   // looping over lines): every rank's LL workgroups must be resident at once
@@ -447,18 +479,8 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   const int maxBlocks = (int)std::max<int64_t>(1, param_int("LL_MAX_BLOCKS", 256));
   int grid = (int)std::max<int64_t>(1, std::min<int64_t>((lines + 255) / 256, maxBlocks));
   grid = std::max(std::min(grid, comm->maxCTAs), comm->minCTAs);
-  hipError_t e = hipErrorInvalidValue;
-  switch (kt) {
-    case K_U8: e = ll_launch<K_U8>(t.devOp, w, grid, t.stream); break;
-    case K_U32: e = ll_launch<K_U32>(t.devOp, w, grid, t.stream); break;
-    case K_U64: e = ll_launch<K_U64>(t.devOp, w, grid, t.stream); break;
-    case K_F16: e = ll_launch<K_F16>(t.devOp, w, grid, t.stream); break;
-    case K_F32: e = ll_launch<K_F32>(t.devOp, w, grid, t.stream); break;
-    case K_F64: e = ll_launch<K_F64>(t.devOp, w, grid, t.stream); break;
-    case K_BF16: e = ll_launch<K_BF16>(t.devOp, w, grid, t.stream); break;
-    case K_F8E4M3: e = ll_launch<K_F8E4M3>(t.devOp, w, grid, t.stream); break;
-    case K_F8E5M2: e = ll_launch<K_F8E5M2>(t.devOp, w, grid, t.stream); break;
-  }
+  const int coll = dev_coll(t.coll), devOp = t.coll == kAllGather ? OP_COPY : t.devOp;
+  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return ll_launch<K>(coll, devOp, w, grid, t.stream); });
   if (e != hipSuccess) {
     VWARN("LL kernel launch failed: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
@@ -466,11 +488,14 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   return ncclSuccess;
 }
 
-// Two-shot direct all-reduce for mid-size buckets (direct.hpp).
+// Direct collectives over the full mesh (direct.hpp): two-shot all-reduce,
+// one-hop reduce-scatter / all-gather.
 static ncclResult_t launch_direct(const Task& t) {
   ncclComm* comm = t.comm;
   const int n = comm->nRanks;
-  const int64_t esz = type_size(t.datatype);
+  const bool ag = t.coll == kAllGather;
+  const int64_t esz = ag ? 1 : type_size(t.datatype);  // all-gather: bytes
+  const int64_t count = ag ? (int64_t)t.count * type_size(t.datatype) : (int64_t)t.count;
   const int64_t eltAlign = std::max<int64_t>(1, 16 / esz);
   auto align_up = [](int64_t x, int64_t a) { return (x + a - 1) / a * a; };
   DirectWork w{};
@@ -478,21 +503,30 @@ static ncclResult_t launch_direct(const Task& t) {
   w.peers = comm->dPeers;
   w.sendbuff = t.sendbuff;
   w.recvbuff = t.recvbuff;
-  w.count = t.count;
+  w.count = (uint64_t)count;
   w.redArg = t.arg;
   w.redArgPtr = t.argPtr;
-  w.redArgBytes = (int)esz;
+  w.redArgBytes = type_size(t.datatype);
   w.preOp = t.devOp == OP_PREMULSUM;
   w.nRanks = n;
   w.rank = comm->rank;
-  // Chunk: as many elements as fit one shard per inbox region, a multiple
-  // of n x 16 bytes; blocks of >= 16 KiB (one 512-thread x 2-pack hunk) per
-  // shard of the largest chunk, at most the cap.
   const int64_t regionElts = (comm->dRegionBytes - 16) / esz;
-  const int64_t chunkMax = regionElts * n / (n * eltAlign) * (n * eltAlign);
-  w.chunkElts = std::min<int64_t>((int64_t)t.count, chunkMax);
-  w.nChunks = (int)(((int64_t)t.count + w.chunkElts - 1) / w.chunkElts);
-  const int64_t shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
+  int64_t shard0;
+  if (t.coll == kAllReduce) {
+    // Chunk: as many elements as fit one shard per inbox region, a multiple
+    // of n x 16 bytes; the shard of the largest chunk is cut into blocks.
+    const int64_t chunkMax = regionElts * n / (n * eltAlign) * (n * eltAlign);
+    w.chunkElts = std::min<int64_t>(count, chunkMax);
+    shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
+  } else {
+    // Reduce-scatter / all-gather: a chunk is a range of ONE rank's block
+    // (count elements) that fits a region; it is cut into blocks directly.
+    w.chunkElts = std::min<int64_t>(count, regionElts / eltAlign * eltAlign);
+    shard0 = w.chunkElts;
+    if (t.coll == kReduceScatter) w.cbd = rs_cbd(comm, t);
+  }
+  w.nChunks = (int)((count + w.chunkElts - 1) / w.chunkElts);
+  // Blocks of >= 16 KiB (one 512-thread x 2-pack hunk), at most the cap.
   const int64_t minBlk = (16 << 10) / esz;
   int64_t nb = std::min<int64_t>((shard0 + minBlk - 1) / minBlk, comm->directMaxBlocks);
   nb = std::max<int64_t>(std::min<int64_t>(nb, comm->maxCTAs), comm->minCTAs);
@@ -500,21 +534,12 @@ static ncclResult_t launch_direct(const Task& t) {
   w.blkElts = align_up((shard0 + nb - 1) / nb, eltAlign);
   w.nBlocks = (int)((shard0 + w.blkElts - 1) / w.blkElts);
   w.regionBytes = comm->dRegionBytes;
-  if (shard0 * esz > w.regionBytes || w.nBlocks > kDirectMaxBlocks) return ncclInternalError;
-  const int kt = kernel_type_of(t.devOp, (int)t.datatype);
-  hipError_t e = hipErrorInvalidValue;
-  switch (kt) {
-    case K_U8: e = direct_launch<K_U8>(t.devOp, w, t.stream); break;
-    case K_U32: e = direct_launch<K_U32>(t.devOp, w, t.stream); break;
-    case K_U64: e = direct_launch<K_U64>(t.devOp, w, t.stream); break;
-    case K_F16: e = direct_launch<K_F16>(t.devOp, w, t.stream); break;
-    case K_F32: e = direct_launch<K_F32>(t.devOp, w, t.stream); break;
-    case K_F64: e = direct_launch<K_F64>(t.devOp, w, t.stream); break;
-    case K_BF16: e = direct_launch<K_BF16>(t.devOp, w, t.stream); break;
-    case K_F8E4M3: e = direct_launch<K_F8E4M3>(t.devOp, w, t.stream); break;
-    case K_F8E5M2: e = direct_launch<K_F8E5M2>(t.devOp, w, t.stream); break;
-    default: return ncclInvalidArgument;
-  }
+  if (shard0 * esz > w.regionBytes || w.nBlocks > kDirectMaxBlocks || w.nBlocks < 1)
+    return ncclInternalError;
+  const int kt = ag ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
+  if (kt < 0) return ncclInvalidArgument;
+  const int coll = dev_coll(t.coll), devOp = ag ? OP_COPY : t.devOp;
+  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return direct_launch<K>(coll, devOp, w, t.stream); });
   if (e != hipSuccess) {
     VWARN("direct kernel launch failed: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
@@ -523,18 +548,31 @@ static ncclResult_t launch_direct(const Task& t) {
 }
 
 // Algorithm choice (topoGetAlgoInfo, enqueue.cc:1805-1945, reduced to one
-// node over a full xGMI mesh): all-reduce buckets up to llMaxBytes take the
-// one-shot LL path, up to directMaxBytes the two-shot direct path (LL128's
-// mid-range slot), larger ones the SIMPLE ring.  NCCL_ALGO / NCCL_PROTO force
-// one: Ring/SIMPLE -> ring; Tree/LL -> LL where it fits; LL128/Direct ->
-// direct where it fits; anything that does not fit falls through to the ring.
+// node over a full xGMI mesh): buckets up to the LL threshold take the
+// one-hop LL path, up to the direct threshold the direct path (LL128's
+// mid-range slot; all-reduce two-shot, reduce-scatter / all-gather one-hop),
+// larger ones the SIMPLE ring.  NCCL_ALGO / NCCL_PROTO force one: Ring/SIMPLE
+// -> ring; Tree/LL -> LL where it fits; LL128/Direct -> direct where it
+// fits; anything that does not fit falls through to the ring.
 enum { kAlgoRing = 0, kAlgoLL = 1, kAlgoDirect = 2 };
 static int choose_algo(const Task& t) {
   const ncclComm* c = t.comm;
-  if (t.coll != kAllReduce || c->nRanks < 2 || c->algoForce == 1) return kAlgoRing;
-  const size_t bytes = t.count * (size_t)type_size(t.datatype);
-  const bool llFits = c->llBuf && bytes <= c->llMaxBytes;
-  const bool directFits = c->dBuf && bytes <= c->directMaxBytes;
+  if (c->nRanks < 2 || c->algoForce == 1) return kAlgoRing;
+  const size_t esz = (size_t)type_size(t.datatype);
+  bool llFits, directFits;
+  if (t.coll == kAllReduce) {
+    const size_t bytes = t.count * esz;
+    llFits = c->llBuf && bytes <= c->llMaxBytes;
+    directFits = c->dBuf && bytes <= c->directMaxBytes;
+  } else {
+    // Reduce-scatter / all-gather: one rank's block must fit an LL slot; the
+    // thresholds are on the whole bucket (n blocks), as the reference's tuner
+    // sizes RS / AG (enqueue.cc:1955, ncclFuncMaxSendRecvCount).
+    const size_t block = t.count * esz, bytes = block * (size_t)c->nRanks;
+    llFits = c->llBuf && c->nRanks <= kOrderMaxRanks && block <= (size_t)c->llLines * 8 &&
+             bytes <= c->llRsAgMaxBytes;
+    directFits = c->dBuf && bytes <= c->directRsAgMaxBytes;
+  }
   if (c->algoForce == 2) return llFits ? kAlgoLL : kAlgoRing;
   if (c->algoForce == 3) return directFits ? kAlgoDirect : kAlgoRing;
   if (llFits) return kAlgoLL;

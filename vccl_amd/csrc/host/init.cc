@@ -230,7 +230,17 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
         n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_THRESHOLD", (int64_t)1 << 62) : 0;
     c->directMaxBlocks = (int)std::max<int64_t>(
         1, std::min<int64_t>(param_int("DIRECT_MAX_BLOCKS", 64), kDirectMaxBlocks));
-    if (c->directMaxBytes > c->llMaxBytes) {
+    // Reduce-scatter / all-gather (the whole bucket, n blocks): one-hop LL
+    // while one rank's block fits a slot and the bucket is at most n x the
+    // all-reduce LL threshold (each rank sends 2(n-1)/n x the bucket as LL
+    // lines, vs 2(n-1) x for the LL all-reduce), the one-hop direct path up
+    // to VCCL_DIRECT_RSAG_THRESHOLD, the SIMPLE ring above.
+    c->llRsAgMaxBytes = n <= kOrderMaxRanks && c->llMaxBytes > 0
+                            ? (size_t)param_int("LL_RSAG_THRESHOLD", (int64_t)n * c->llMaxBytes)
+                            : 0;
+    c->directRsAgMaxBytes =
+        n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_RSAG_THRESHOLD", (int64_t)64 << 20) : 0;
+    if (c->directMaxBytes > c->llMaxBytes || c->directRsAgMaxBytes > c->llRsAgMaxBytes) {
       const int64_t chunk = std::max<int64_t>(param_int("DIRECT_CHUNK_BYTES", 16 << 20), 64 << 10);
       c->dRegionBytes = (chunk + n - 1) / n / 256 * 256 + 256;
       const size_t bytes = (size_t)2 * n * c->dRegionBytes;
@@ -242,7 +252,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       me.dBufPtr = c->dBuf;
       me.dFlagPtr = c->dFlags;
     } else {
-      c->directMaxBytes = 0;
+      c->directMaxBytes = c->directRsAgMaxBytes = 0;
     }
   }
   if (n > 1) NCCLCHECK(net_listen(c, &me));
@@ -266,8 +276,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // LL and the two-shot direct path need every peer's memory mapped
     // (full xGMI mesh): all-reduce takes the ring.  Net channels move
     // through the proxy, a few are enough (NCCL's net defaults use 2-4).
-    c->llMaxBytes = 0;
-    c->directMaxBytes = 0;
+    c->llMaxBytes = c->llRsAgMaxBytes = 0;
+    c->directMaxBytes = c->directRsAgMaxBytes = 0;
     c->nChannels = std::max(1, std::min(c->nChannels, (int)param_int("NET_NCHANNELS", 8)));
     VINFO("rank %d: inter-node ring through the net proxy, %d channels", c->rank, c->nChannels);
   }
@@ -326,6 +336,13 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   dc.useFences = (int)param_int("FENCES", 0);
   if (anyNet) dc.useFences = 1;  // slots and flags in host memory: full system-scope fences
   dc.pollMode = (int)param_int("POLL_MODE", 0);
+  // reduce-scatter fold order of this rank on each ring (ring_types.hpp)
+  dc.nRings = std::min(nRings, kOrderMaxRings);
+  for (int k = 0; k < dc.nRings && n <= kOrderMaxRanks; k++) {
+    const auto& ring = rings[k];
+    const int pos = (int)(std::find(ring.begin(), ring.end(), c->rank) - ring.begin());
+    for (int j = 0; j < n; j++) dc.rsOrder[k][j] = (int8_t)ring[(pos + 1 + j) % n];
+  }
   HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));
 
