@@ -90,9 +90,6 @@ def bench_reduce_copy(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # correctness guard on the measured buffers (bit-exact f32 add)
-    assert torch.equal(d.view(torch.int32), (a + b).view(torch.int32)), "reduce-copy mismatch"
-    torch.cuda.synchronize()
     e0, e1 = _evt(), _evt()
     t0 = time.perf_counter()
     e0.record(stream)
@@ -102,6 +99,9 @@ def bench_reduce_copy(args):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     gpu_s = e0.elapsed_time(e1) / 1e3
+    # correctness of the measured buffers (bit-exact f32 add), after the timed
+    # region so no idle gap separates warmup and timing
+    assert torch.equal(d.view(torch.int32), (a + b).view(torch.int32)), "reduce-copy mismatch"
     # per-launch kernel durations, separately (an event pair per launch
     # serialises the queue, so it stays out of the timed region)
     kern_ms = []
@@ -530,11 +530,12 @@ def run_checks(dist, comm, rank, world, plan):
     """Run every check of `plan` ({name: (kind, args)}) with the fences off
     (the default) and again with system-scope fences on (vcclCommSetFences,
     the VCCL_FENCES=1 path); returns {"fences_off": {...}, "fences_on": {...}}."""
-    res = {}
+    res = {"check_ms": {}}
     for mode, fences in (("fences_off", False), ("fences_on", True)):
         comm.set_fences(fences)
         r = {}
         for name, (kind, kw) in plan.items():
+            t0 = time.perf_counter()
             try:
                 if kind == "ar":
                     r[name] = check_ar(dist, comm, rank, world, **kw)
@@ -545,6 +546,7 @@ def run_checks(dist, comm, rank, world, plan):
                     r[name + "_rs"], r[name + "_ag"] = rs_ok, ag_ok
             except Exception as e:  # noqa: BLE001 - a failed check is a verdict, not a crash
                 r[name] = f"error: {e!r}"
+            res["check_ms"][f"{mode}:{name}"] = round((time.perf_counter() - t0) * 1e3, 1)
         res[mode] = r
     comm.set_fences(False)
     return res
@@ -569,7 +571,7 @@ def initall_check(world_devices, timeout=240):
 
 
 def _flatten_ok(checks):
-    vals = [v for m in checks.values() for v in m.values()]
+    vals = [v for k, m in checks.items() if k != "check_ms" for v in m.values()]
     return all(v is True for v in vals)
 
 

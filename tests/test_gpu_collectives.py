@@ -91,7 +91,7 @@ def test_algorithm_choice(monkeypatch):
              "Tree": {(0, 1 << 10): "ll", (0, 1 << 20): "ring", (1, 1 << 10): "ll",
                       (2, 1 << 26): "ring"},
              "Direct": {(0, 1 << 10): "direct", (0, 1 << 28): "direct", (1, 1 << 10): "direct",
-                        (2, 1 << 10): "direct", (2, 1 << 26): "ring"}}
+                        (2, 1 << 10): "direct", (2, 1 << 26): "direct"}}
     for algo, expect in cases.items():
         if algo is None:
             monkeypatch.delenv("NCCL_ALGO", raising=False)

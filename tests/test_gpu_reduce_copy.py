@@ -226,3 +226,42 @@ def test_fp8_all_code_pairs(t):
         got = _run(dev_op, t, arg, [a, b], pre=pre, post=post)[0]
         exp = O.reduce_copy(dev_op, t, arg, [a, b], pre_op_args=[arg] * pre, post_op=post)[0]
         assert_bitexact(t, got, exp, minmax=op in (2, 3), what=f"fp8 t{t} op{op}")
+
+
+# Destinations at DIFFERENT misalignments (the reference falls back to element
+# packs, common_kernel.h:237-241): the body is aligned on destination 0 and
+# every other destination is realigned by wavefront shuffle + funnel shift,
+# with <= 4 partial stores at each wave's two ends.  Sizes straddle the wave
+# (64 packs), hunk and grid boundaries; bytes around each destination must
+# stay untouched.
+DST_OFFSETS = {1: [(0, 1), (3, 0), (5, 13), (0, 15, 7)], 2: [(0, 2), (6, 0), (2, 14), (0, 8, 4)],
+               4: [(0, 4), (12, 0), (4, 8), (0, 12, 4)], 8: [(0, 8), (8, 0), (8, 8, 0)]}
+
+
+@pytest.mark.parametrize("t", [1, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("op", [0, 2])
+def test_destination_realignment(t, op):
+    rng = np.random.default_rng(2000 + 10 * t + op)
+    sz = np.dtype(O.NP_DTYPE[t]).itemsize
+    for doffs in DST_OFFSETS[sz]:
+        for soffs in ([0, 0], [sz, 0], [(3 * sz) % 16, (5 * sz) % 16]):
+            for n in (1, 5, 63, 64 * 16 // sz + 3, 4097, 100_003, (1 << 20) + 9):
+                srcs = [_rand(rng, t, n) for _ in range(2)]
+                dev_op, arg, pre, post = _dev_args(op, t, 2)
+                exp = O.reduce_copy(dev_op, t, arg, srcs, pre_op_args=[arg] * pre, post_op=post)[0]
+                keep, sp = [], []
+                for i, x in enumerate(srcs):
+                    tt, ptr = to_dev(x, offset=soffs[i])
+                    keep.append(tt)
+                    sp.append(ptr)
+                outs = [empty_dev(n * sz, offset=o) for o in doffs]
+                nccl.reduce_copy(dev_op, t, arg, sp, [ptr for _, ptr in outs], n, stream_ptr(),
+                                 pre_op_srcs=pre, post_op=post)
+                torch.cuda.synchronize()
+                for (tt, _), o in zip(outs, doffs):
+                    got = from_dev(tt, O.NP_DTYPE[t], n, o)
+                    assert_bitexact(t, got, exp, minmax=op == 2,
+                                    what=f"t{t} op{op} n{n} srcs{soffs} dsts{doffs}")
+                    raw = tt.cpu().numpy()
+                    assert (raw[:o] == 0xA5).all() and (raw[o + n * sz:] == 0xA5).all(), \
+                        f"guard bytes written t{t} n{n} dsts{doffs}"

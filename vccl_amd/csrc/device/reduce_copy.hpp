@@ -414,6 +414,80 @@ __device__ __forceinline__ u32x4 realign(u32x4 cur, u32x4 ext, int k) {
   return funnel16(cur, nxt, k);
 }
 
+// ------------------------------------------------- misaligned destinations
+// Destination d whose address is k_d bytes past a 16-byte boundary where
+// destination 0 is aligned (the body's reference): its aligned pack holding
+// body bytes [16p + 16 - k, 16p + 32 - k) is bytes [16 - k, 32 - k) of this
+// lane's result and the next lane's (wavefront shuffle + funnel shift, the
+// source realignment run backwards).  A wave's two ends have no neighbour in
+// the wave: lane 0 stores the first 16 - k bytes of its result and the last
+// valid lane the last k bytes, each as <= 4 naturally aligned 8/4/2/1-byte
+// stores; the neighbouring wave's ends fill the rest of those packs (disjoint
+// bytes).  Every body byte is written exactly once.
+
+// Bytes [from, from + 8) of the 16-byte value (lo | hi << 64), zero past 16.
+__device__ __forceinline__ uint64_t bytes_at(uint64_t lo, uint64_t hi, int from) {
+  if (from == 0) return lo;
+  if (from < 8) return (lo >> (8 * from)) | (hi << (64 - 8 * from));
+  if (from == 8) return hi;
+  return hi >> (8 * (from - 8));
+}
+// Store bytes [from, to) of v to addr + from .. addr + to - 1.
+template <int P>
+__device__ __forceinline__ void st_partial(char* addr, u32x4 v, int from, int to) {
+  const uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  const uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  while (from < to) {
+    const uintptr_t a = (uintptr_t)(addr + from);
+    const uint64_t x = bytes_at(lo, hi, from);
+    if ((a & 7) == 0 && to - from >= 8) {
+      stT<P, uint64_t>(addr + from, 0, x);
+      from += 8;
+    } else if ((a & 3) == 0 && to - from >= 4) {
+      stT<P, uint32_t>(addr + from, 0, (uint32_t)x);
+      from += 4;
+    } else if ((a & 1) == 0 && to - from >= 2) {
+      stT<P, uint16_t>(addr + from, 0, (uint16_t)x);
+      from += 2;
+    } else {
+      stT<P, uint8_t>(addr + from, 0, (uint8_t)x);
+      from += 1;
+    }
+  }
+}
+// Store body pack p (value v) to destination `dst` (the body start of that
+// destination, k bytes past alignment).  Every lane of the wave must call it
+// (the shuffle); `valid` = p < nPacks, `nextValid` = this lane's successor
+// pack is in the body and held by the next lane.
+template <int P>
+__device__ __forceinline__ void st16_realigned(char* dst, int k, int64_t p, u32x4 v, bool valid,
+                                               bool nextValid) {
+  if (k == 0) {
+    if (valid) st16<P>(dst, p * 16, v);
+    return;
+  }
+  u32x4 nxt;
+  nxt.x = __shfl_down(v.x, 1);
+  nxt.y = __shfl_down(v.y, 1);
+  nxt.z = __shfl_down(v.z, 1);
+  nxt.w = __shfl_down(v.w, 1);
+  if (!valid) return;
+  char* at = dst + p * 16;
+  if (__lane_id() == 0) st_partial<P>(at, v, 0, 16 - k);
+  if (nextValid && __lane_id() != 63) st16<P>(dst - k, (p + 1) * 16, funnel16(v, nxt, 16 - k));
+  else st_partial<P>(at, v, 16 - k, 16);
+}
+template <int POLS>
+__device__ __forceinline__ void st16_dst_realigned(const RCArgs& a, int d, int k, int64_t p, u32x4 v,
+                                                   bool valid, bool nextValid) {
+  switch (d) {
+    case 0: st16_realigned<dst_pol(POLS, 0)>(a.dsts[0], k, p, v, valid, nextValid); return;
+    case 1: st16_realigned<dst_pol(POLS, 1)>(a.dsts[1], k, p, v, valid, nextValid); return;
+    case 2: st16_realigned<dst_pol(POLS, 2)>(a.dsts[2], k, p, v, valid, nextValid); return;
+    default: st16_realigned<dst_pol(POLS, 3)>(dst_ptr(a, d), k, p, v, valid, nextValid); return;
+  }
+}
+
 // Body packs [0, nPacks) when every destination is 16-byte aligned and source
 // s starts k_s bytes past a 16-byte boundary (some k_s != 0).  Whole waves
 // run (the shuffle needs every lane); a lane past the end loads clamped packs
@@ -428,9 +502,11 @@ __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, 
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t nHunks = (nPacks + hunkPacks - 1) / hunkPacks;
   const bool last = __lane_id() == 63;
-  int k[NS];
+  int k[NS], kd[ND];
 #pragma unroll
   for (int s = 0; s < NS; s++) k[s] = (int)((uintptr_t)src_ptr(a, s) & 15);
+#pragma unroll
+  for (int d = 0; d < ND; d++) kd[d] = (int)((uintptr_t)dst_ptr(a, d) & 15);
   for (int64_t h = worker; h < nHunks; h += nWorkers) {
     const int64_t p0 = h * hunkPacks + tid;
     if (p0 - __lane_id() >= nPacks) continue;  // the whole wave is past the end
@@ -461,10 +537,9 @@ __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, 
         acc = pack_reduce(fn, acc, v);
       }
       if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
-      if (p < nPacks) {
 #pragma unroll
-        for (int d = 0; d < ND; d++) st16_dst<POLS>(a, d, p * 16, acc);
-      }
+      for (int d = 0; d < ND; d++)
+        st16_dst_realigned<POLS>(a, d, kd[d], p, acc, p < nPacks, p + 1 < nPacks);
     }
   }
 }
@@ -495,8 +570,9 @@ __device__ __forceinline__ void rc_hunks_shifted_rt(const Fn& fn, const RCArgs& 
       acc = pack_reduce(fn, acc, v);
     }
     if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
-    if (p < nPacks)
-      for (int d = 0; d < a.nDsts; d++) st16_dst<POLS>(a, d, p * 16, acc);
+    for (int d = 0; d < a.nDsts; d++)
+      st16_dst_realigned<POLS>(a, d, (int)((uintptr_t)dst_ptr(a, d) & 15), p, acc, p < nPacks,
+                               p + 1 < nPacks);
   }
 }
 
@@ -556,10 +632,11 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
                                                                nthreads);
     return;
   }
-  // Misaligned (see above): destinations must share one misalignment m.
+  // Misaligned (see above): the body is aligned on destination 0; sources
+  // and the other destinations at other offsets are realigned in registers.
   const int m = (int)((uintptr_t)a.dsts[0] & 15);
   bool ok = m % esz == 0;
-  for (int d = 1; d < a.nDsts; d++) ok = ok && (int)((uintptr_t)dst_ptr(a, d) & 15) == m;
+  for (int d = 1; d < a.nDsts; d++) ok = ok && ((uintptr_t)dst_ptr(a, d) & (esz - 1)) == 0;
   for (int s = 0; s < a.nSrcs; s++) ok = ok && ((uintptr_t)src_ptr(a, s) & (esz - 1)) == 0;
   if (!ok) {
     rc_elems<Fn, POLS>(fn, a, 0, nElts, gtid, gthreads);

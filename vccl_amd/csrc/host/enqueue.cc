@@ -574,7 +574,9 @@ static int choose_algo(const Task& t) {
     directFits = c->dBuf && bytes <= c->directRsAgMaxBytes;
   }
   if (c->algoForce == 2) return llFits ? kAlgoLL : kAlgoRing;
-  if (c->algoForce == 3) return directFits ? kAlgoDirect : kAlgoRing;
+  // Forced direct: any bucket the inbox can stream (the size threshold only
+  // steers the automatic choice)
+  if (c->algoForce == 3) return c->dBuf && c->nRanks <= kDirectMaxRanks ? kAlgoDirect : kAlgoRing;
   if (llFits) return kAlgoLL;
   if (directFits) return kAlgoDirect;
   return kAlgoRing;
