@@ -175,9 +175,9 @@ def test_multi_process_ranks(n, geom):
         if geom == "ring_only":  # NCCL_ALGO forces the ring for every size
             env["NCCL_ALGO"] = "Ring"
             ll_max = direct_max = 0
-        if geom == "direct_only":  # every all-reduce that fits takes the direct path
+        if geom == "direct_only":  # every collective takes the direct path, any size
             env["NCCL_ALGO"] = "Direct"
-            ll_max = 0
+            ll_max, direct_max = 0, 1 << 62
     elif geom == "net":
         # every ring connection through the net proxy (host-pinned staging +
         # TCP, proxy.cc), as between nodes; LL / direct need the xGMI mesh,

@@ -156,6 +156,8 @@ hipError_t rc_launch<VCCL_KT>(int devOp, const RCArgs& a, int64_t nElts, uint64_
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if (a.nSrcs == 2 && a.nDsts == 1) err = launch_nsnd<Fn, 2, 1>(a, nElts, redArg, lg, stream);
     else if (a.nSrcs == 1 && a.nDsts == 1) err = launch_nsnd<Fn, 1, 1>(a, nElts, redArg, lg, stream);
+    // reduce + copy to two places (the ring all-reduce's final step shape)
+    else if (a.nSrcs == 2 && a.nDsts == 2) err = launch_nsnd<Fn, 2, 2>(a, nElts, redArg, lg, stream);
     else err = launch_nsnd<Fn, 0, 0>(a, nElts, redArg, lg, stream);
   });
   return err;

@@ -17,8 +17,13 @@
 
 namespace vccl {
 
+// 512 threads per channel: the ring primitive (pipelined aligned copy +
+// realigning misaligned path, inlined per (recv, send, src, dst) shape) needs
+// ~137 VGPRs, above the 128 a 1024-thread workgroup allows (that spilled in
+// the hot loop).  Channel count, not threads per channel, sets ring
+// bandwidth.
 template <int COLL, class Fn, int UNROLL>
-__global__ __launch_bounds__(1024) void k_ring(RingWork w) {
+__global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingWork w) {
   __shared__ int shAbort;
   if (threadIdx.x == 0) shAbort = 0;
   __syncthreads();

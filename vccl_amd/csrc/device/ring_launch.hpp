@@ -11,6 +11,7 @@ namespace vccl {
 
 enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2 };
 constexpr int kRingUnroll = 2;
+constexpr int kRingMaxThreads = 512;  // k_ring launch bound (ring_kernels.hip)
 
 template <int K>
 hipError_t ring_launch(int coll, int devOp, const RingWork& w, int nthreads, hipStream_t stream);

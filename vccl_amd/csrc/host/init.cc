@@ -16,6 +16,7 @@
 
 #include "../../../include/vccl_ext.h"
 #include "../device/direct.hpp"
+#include "../device/ring_launch.hpp"
 #include "core.h"
 
 namespace vccl {
@@ -166,8 +167,14 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     if (has(proto, "LL128") || has(algo, "direct")) c->algoForce = 3;
     if (has(proto, "simple") || (has(algo, "ring") && !has(algo, "tree"))) c->algoForce = 1;
   }
-  c->nThreads = (int)param_int("NTHREADS", 1024);
-  if (c->nThreads != 256 && c->nThreads != 512 && c->nThreads != 1024) c->nThreads = 1024;
+  // Threads per ring channel (NCCL_NTHREADS, tuning.cc:198-200): 256 or 512
+  // (the ring kernel's launch bound, ring_launch.hpp kRingMaxThreads).
+  c->nThreads = (int)param_int("NTHREADS", kRingMaxThreads);
+  if (c->nThreads != 256 && c->nThreads != 512) {
+    if (c->nThreads != kRingMaxThreads)
+      VINFO("NCCL_NTHREADS=%d not supported by the ring kernel, using %d", c->nThreads, kRingMaxThreads);
+    c->nThreads = kRingMaxThreads;
+  }
 
   HIPCHECK(hipHostMalloc((void**)&c->abortFlag, sizeof(int), hipHostMallocMapped));
   HIPCHECK(hipHostMalloc((void**)&c->errorFlag, sizeof(int), hipHostMallocMapped));
