@@ -403,19 +403,30 @@ def _hash32(lo, hi, device="cuda"):
 
 
 _DIGEST = {}
+_DIGEST_CHUNK = 1 << 24
 
 
 def _digest(lo, hi):
-    """_hash32 over [lo, hi), served from a per-device uint8 cache of the
-    prefix [0, 2^k) (computed once, the checks then cost one gather each)."""
+    """5-bit digest of every index in [lo, hi): a per-device uint8 cache grown
+    in fixed 2^24-index chunks, chunk j drawn by torch's counter-based
+    (Philox) generator seeded with 4242 + j — identical on every rank and
+    every device whatever the cache size, with no period a misplaced block
+    could hide in (_hash32 below is the equivalent closed form, kept for
+    reference and CPU use)."""
     dev = torch.cuda.current_device()
     g = _DIGEST.get(dev)
     if g is None or g.numel() < hi:
-        size = 1 << max(20, (hi - 1).bit_length())
-        g = torch.empty(size, dtype=torch.uint8, device="cuda")
-        for a in range(0, size, _SLICE):
-            g[a:a + _SLICE] = _hash32(a, min(size, a + _SLICE)).to(torch.uint8)
-        _DIGEST[dev] = g
+        nchunks = -(-hi // _DIGEST_CHUNK)
+        have = 0 if g is None else g.numel() // _DIGEST_CHUNK
+        new = torch.empty(nchunks * _DIGEST_CHUNK, dtype=torch.uint8, device="cuda")
+        if g is not None:
+            new[:g.numel()] = g
+        gen = torch.Generator(device="cuda")
+        for j in range(have, nchunks):
+            gen.manual_seed(4242 + j)
+            new[j * _DIGEST_CHUNK:(j + 1) * _DIGEST_CHUNK] = torch.randint(
+                0, 32, (_DIGEST_CHUNK,), dtype=torch.uint8, device="cuda", generator=gen)
+        _DIGEST[dev] = g = new
     return g[lo:hi]
 
 
@@ -433,7 +444,7 @@ def pattern_fill(buf, r, world, base=0):
     n = buf.numel()
     for lo in range(0, n, _SLICE):
         hi = min(n, lo + _SLICE)
-        buf[lo:hi] = lut[_digest(base + lo, base + hi).long()]
+        buf[lo:hi] = lut[_digest(base + lo, base + hi).int()]
 
 
 def pattern_ok(buf, world, base=0):
@@ -443,7 +454,7 @@ def pattern_ok(buf, world, base=0):
     n = buf.numel()
     for lo in range(0, n, _SLICE):
         hi = min(n, lo + _SLICE)
-        if not torch.equal(buf[lo:hi], lut[_digest(base + lo, base + hi).long()]):
+        if not torch.equal(buf[lo:hi], lut[_digest(base + lo, base + hi).int()]):
             return False
     return True
 
@@ -504,7 +515,6 @@ def _check_rs_ag(dist, comm, rank, world, nbytes, dtype):
     torch.cuda.synchronize()
     ag_ok = pattern_ok(x, world) and comm.async_error() == 0
     del x, shard
-    torch.cuda.empty_cache()
     return _all_ok(dist, rs_ok), _all_ok(dist, ag_ok)
 
 

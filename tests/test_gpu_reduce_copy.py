@@ -265,3 +265,21 @@ def test_destination_realignment(t, op):
                     raw = tt.cpu().numpy()
                     assert (raw[:o] == 0xA5).all() and (raw[o + n * sz:] == 0xA5).all(), \
                         f"guard bytes written t{t} n{n} dsts{doffs}"
+
+
+def test_lds_staged_variant():
+    """The north-star's LDS double-buffered staging (k_reduce_copy_lds,
+    rc_kernels.hip: global_load_lds_dwordx4 two tiles deep, ds_read back) —
+    a benchmark variant selected by launch config order 2 — must be
+    bit-exact like the register path it lost to.  Sizes are
+    whole 8 KiB tiles (the launcher falls back to the register path
+    otherwise, which the ragged size checks)."""
+    rng = np.random.default_rng(31)
+    for n, grid, st in ((1 << 22, 256, 1), (1 << 22, 1024, 2), ((1 << 20) + 2048, 97, 1),
+                        (1 << 20, 4096, 2), ((1 << 20) + 5, 256, 1)):
+        a = rng.standard_normal(n).astype(np.float32)
+        b = rng.standard_normal(n).astype(np.float32)
+        cfg = {"blockSize": 256, "unroll": 2, "gridBlocks": grid, "ntLoads": 1, "ntStores": st,
+               "order": 2}
+        got = _run(0, 7, 0, [a, b], config=cfg)[0]
+        assert np.array_equal(got.view(np.uint32), (a + b).view(np.uint32)), (n, grid, st)

@@ -147,28 +147,28 @@ __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)
     // (every load of a hunk issued before the shuffles): the scatter / gather
     // copies (1 -> 1) and the phase-2 fold (n -> n).
     if (nS == 1 && nD == 1) {
-      reduce_copy<Fn, 1, 1, 2, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads);
+      reduce_copy<Fn, 1, 1, 2, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads);
       return;
     }
     if (nD == 1 && nS > 1) {  // reduce-scatter fold: n -> 1
       switch (nS) {
-        case 2: reduce_copy<Fn, 2, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
-        case 3: reduce_copy<Fn, 3, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
-        case 4: reduce_copy<Fn, 4, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
-        case 8: reduce_copy<Fn, 8, 1, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 2: reduce_copy<Fn, 2, 1, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 3: reduce_copy<Fn, 3, 1, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 4: reduce_copy<Fn, 4, 1, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 8: reduce_copy<Fn, 8, 1, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
         default: break;
       }
     }
     if (nS == nD) {
       switch (nS) {
-        case 2: reduce_copy<Fn, 2, 2, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
-        case 3: reduce_copy<Fn, 3, 3, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
-        case 4: reduce_copy<Fn, 4, 4, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
-        case 8: reduce_copy<Fn, 8, 8, 1, P, 0, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 2: reduce_copy<Fn, 2, 2, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 3: reduce_copy<Fn, 3, 3, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 4: reduce_copy<Fn, 4, 4, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
+        case 8: reduce_copy<Fn, 8, 8, 1, P, 0, false, false>(fn, a, nElts, 0, 1, tid, nthreads); return;
         default: break;
       }
     }
-    reduce_copy<Fn, 0, 0, 1, P, 0, true>(fn, a, nElts, 0, 1, tid, nthreads);
+    reduce_copy<Fn, 0, 0, 1, P, 0, true, false>(fn, a, nElts, 0, 1, tid, nthreads);
     return;
   }
   const int64_t nPacks = elemOnly ? 0 : nElts * (int64_t)sizeof(T) / 16;

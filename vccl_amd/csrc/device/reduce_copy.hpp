@@ -459,7 +459,11 @@ __device__ __forceinline__ void st_partial(char* addr, u32x4 v, int from, int to
 // destination, k bytes past alignment).  Every lane of the wave must call it
 // (the shuffle); `valid` = p < nPacks, `nextValid` = this lane's successor
 // pack is in the body and held by the next lane.
-template <int P>
+// PP: policy of the partial stores.  The grid kernels store them plainly
+// (write-back): the two halves of a wave-boundary pack then merge in L2
+// instead of reaching HBM as two byte-masked write-throughs.  Ring FIFO slots
+// keep the slot's system-coherent policy (the peer reads them).
+template <int P, int PP = P>
 __device__ __forceinline__ void st16_realigned(char* dst, int k, int64_t p, u32x4 v, bool valid,
                                                bool nextValid) {
   if (k == 0) {
@@ -473,19 +477,23 @@ __device__ __forceinline__ void st16_realigned(char* dst, int k, int64_t p, u32x
   nxt.w = __shfl_down(v.w, 1);
   if (!valid) return;
   char* at = dst + p * 16;
-  if (__lane_id() == 0) st_partial<P>(at, v, 0, 16 - k);
+  if (__lane_id() == 0) st_partial<PP>(at, v, 0, 16 - k);
   if (nextValid && __lane_id() != 63) st16<P>(dst - k, (p + 1) * 16, funnel16(v, nxt, 16 - k));
-  else st_partial<P>(at, v, 16 - k, 16);
+  else st_partial<PP>(at, v, 16 - k, 16);
 }
-template <int POLS>
+template <int POLS, bool PLAIN_PARTIALS = false>
 __device__ __forceinline__ void st16_dst_realigned(const RCArgs& a, int d, int k, int64_t p, u32x4 v,
                                                    bool valid, bool nextValid) {
+#define VCCL_RA(D, PTR)                                                                        \
+  st16_realigned<dst_pol(POLS, D), PLAIN_PARTIALS ? kPlain : dst_pol(POLS, D)>(PTR, k, p, v, valid, \
+                                                                             nextValid)
   switch (d) {
-    case 0: st16_realigned<dst_pol(POLS, 0)>(a.dsts[0], k, p, v, valid, nextValid); return;
-    case 1: st16_realigned<dst_pol(POLS, 1)>(a.dsts[1], k, p, v, valid, nextValid); return;
-    case 2: st16_realigned<dst_pol(POLS, 2)>(a.dsts[2], k, p, v, valid, nextValid); return;
-    default: st16_realigned<dst_pol(POLS, 3)>(dst_ptr(a, d), k, p, v, valid, nextValid); return;
+    case 0: VCCL_RA(0, a.dsts[0]); return;
+    case 1: VCCL_RA(1, a.dsts[1]); return;
+    case 2: VCCL_RA(2, a.dsts[2]); return;
+    default: VCCL_RA(3, dst_ptr(a, d)); return;
   }
+#undef VCCL_RA
 }
 
 // Body packs [0, nPacks) when every destination is 16-byte aligned and source
@@ -494,7 +502,7 @@ __device__ __forceinline__ void st16_dst_realigned(const RCArgs& a, int d, int k
 // and stores nothing.  NS / ND compile-time (NS > 0): every load of a hunk —
 // the aligned packs and lane 63's successor packs — is issued before the
 // first shuffle, so their latencies overlap.
-template <class Fn, int NS, int ND, int UNROLL, int POLS>
+template <class Fn, int NS, int ND, int UNROLL, int POLS, bool DSTR>
 __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, int64_t nPacks,
                                                  int64_t worker, int64_t nWorkers, int tid,
                                                  int nthreads) {
@@ -506,7 +514,7 @@ __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, 
 #pragma unroll
   for (int s = 0; s < NS; s++) k[s] = (int)((uintptr_t)src_ptr(a, s) & 15);
 #pragma unroll
-  for (int d = 0; d < ND; d++) kd[d] = (int)((uintptr_t)dst_ptr(a, d) & 15);
+  for (int d = 0; d < ND; d++) kd[d] = DSTR ? (int)((uintptr_t)dst_ptr(a, d) & 15) : 0;
   for (int64_t h = worker; h < nHunks; h += nWorkers) {
     const int64_t p0 = h * hunkPacks + tid;
     if (p0 - __lane_id() >= nPacks) continue;  // the whole wave is past the end
@@ -538,15 +546,18 @@ __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, 
       }
       if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
 #pragma unroll
-      for (int d = 0; d < ND; d++)
-        st16_dst_realigned<POLS>(a, d, kd[d], p, acc, p < nPacks, p + 1 < nPacks);
+      for (int d = 0; d < ND; d++) {
+        if constexpr (DSTR)
+          st16_dst_realigned<POLS, true>(a, d, kd[d], p, acc, p < nPacks, p + 1 < nPacks);
+        else if (p < nPacks) st16_dst<POLS>(a, d, p * 16, acc);
+      }
     }
   }
 }
 
 // Runtime operand counts (any nSrcs / nDsts up to the maxima), one pack per
 // thread per step.
-template <class Fn, int POLS>
+template <class Fn, int POLS, bool DSTR>
 __device__ __forceinline__ void rc_hunks_shifted_rt(const Fn& fn, const RCArgs& a, int64_t nPacks,
                                                     int64_t worker, int64_t nWorkers, int tid,
                                                     int nthreads) {
@@ -570,9 +581,13 @@ __device__ __forceinline__ void rc_hunks_shifted_rt(const Fn& fn, const RCArgs& 
       acc = pack_reduce(fn, acc, v);
     }
     if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
-    for (int d = 0; d < a.nDsts; d++)
-      st16_dst_realigned<POLS>(a, d, (int)((uintptr_t)dst_ptr(a, d) & 15), p, acc, p < nPacks,
-                               p + 1 < nPacks);
+    for (int d = 0; d < a.nDsts; d++) {
+      if constexpr (DSTR)
+        st16_dst_realigned<POLS>(a, d, (int)((uintptr_t)dst_ptr(a, d) & 15), p, acc, p < nPacks,
+                                 p + 1 < nPacks);
+      else if (p < nPacks)
+        st16_dst<POLS>(a, d, p * 16, acc);
+    }
   }
 }
 
@@ -619,7 +634,13 @@ __device__ __forceinline__ void reduce_copy_aligned(const Fn& fn, const RCArgs& 
 // `nthreads` threads (this workgroup = `worker`).  Pointers in `a` are the
 // element-0 addresses.  Wave-uniform control flow throughout (every branch
 // below depends on pointers and counts only).
-template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false>
+//
+// DSTR (destination realignment): destinations at different misalignments
+// are realigned in registers (true), or — for callers that never pass them
+// and need the registers (the direct kernels stage a misaligned output
+// through their aligned inbox) — sent to the element path (false).
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false,
+          bool DSTR = true>
 __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
                                             int64_t worker, int64_t nWorkers, int tid,
                                             int nthreads) {
@@ -636,7 +657,8 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
   // and the other destinations at other offsets are realigned in registers.
   const int m = (int)((uintptr_t)a.dsts[0] & 15);
   bool ok = m % esz == 0;
-  for (int d = 1; d < a.nDsts; d++) ok = ok && ((uintptr_t)dst_ptr(a, d) & (esz - 1)) == 0;
+  for (int d = 1; d < a.nDsts; d++)
+    ok = ok && ((uintptr_t)dst_ptr(a, d) & (DSTR ? esz - 1 : 15)) == (DSTR ? 0u : (uintptr_t)m);
   for (int s = 0; s < a.nSrcs; s++) ok = ok && ((uintptr_t)src_ptr(a, s) & (esz - 1)) == 0;
   if (!ok) {
     rc_elems<Fn, POLS>(fn, a, 0, nElts, gtid, gthreads);
@@ -661,10 +683,10 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
     // batched loads for the grid kernels; the in-ring copy (PIPE, a 1024-thread
     // workgroup with a 128-VGPR budget) keeps the lean one-pack loop
     if constexpr (NS >= 1 && ND >= 1 && !PIPE)
-      rc_hunks_shifted<Fn, NS, ND, (UNROLL < 2 ? UNROLL : 2), POLS>(fn, b, nPacks, worker, nWorkers,
-                                                                    tid, nthreads);
+      rc_hunks_shifted<Fn, NS, ND, (UNROLL < 2 ? UNROLL : 2), POLS, DSTR>(fn, b, nPacks, worker,
+                                                                          nWorkers, tid, nthreads);
     else
-      rc_hunks_shifted_rt<Fn, POLS>(fn, b, nPacks, worker, nWorkers, tid, nthreads);
+      rc_hunks_shifted_rt<Fn, POLS, DSTR>(fn, b, nPacks, worker, nWorkers, tid, nthreads);
   }
   const int64_t eDone = he + nPacks * 16 / esz;
   if (eDone < nElts) rc_elems<Fn, POLS>(fn, a, eDone, nElts, gtid, gthreads);
