@@ -536,15 +536,44 @@ def check_group(dist, comm, rank, world, nbytes, k):
     return _all_ok(dist, ok and comm.async_error() == 0)
 
 
+def _fences_plan(plan, algo_of):
+    """One check per path family (kind, dtype, algorithm actually run) for the
+    fences-on pass, at the family's smallest planned size (RS + AG at <= 64
+    MiB): every path runs once with fences, the biggest buckets only without.
+    algo_of(kind, kw) -> the algorithm the library runs for that check."""
+    fam = {}
+    for name, (kind, kw) in plan.items():
+        key = (kind, kw.get("dtype"), algo_of(kind, kw), kw.get("k"))
+        if key not in fam or kw.get("nbytes", 0) < fam[key][1][1].get("nbytes", 0):
+            fam[key] = (name, (kind, kw))
+    out = {}
+    for name, (kind, kw) in fam.values():
+        if kind == "rs_ag" and kw["nbytes"] > (64 << 20):
+            kw = {**kw, "nbytes": 64 << 20}
+            name = name.rsplit("_", 1)[0] + f"_{64 << 20}"
+        out[name] = (kind, kw)
+    return out
+
+
 def run_checks(dist, comm, rank, world, plan):
     """Run every check of `plan` ({name: (kind, args)}) with the fences off
-    (the default) and again with system-scope fences on (vcclCommSetFences,
-    the VCCL_FENCES=1 path); returns {"fences_off": {...}, "fences_on": {...}}."""
+    (the default), then each path family once more with system-scope fences
+    on (vcclCommSetFences, the VCCL_FENCES=1 path); returns
+    {"fences_off": {...}, "fences_on": {...}, "check_ms": {...}}."""
+    def algo_of(kind, kw):
+        if kw.get("algo"):
+            return kw["algo"]
+        esz = torch.tensor([], dtype=_TDT[kw.get("dtype", "f32" if kind != "rs_ag" else "bf16")]).element_size()
+        n = max(1, kw["nbytes"] // esz)
+        code = _CODE[kw.get("dtype", "f32" if kind != "rs_ag" else "bf16")]
+        return comm.coll_algo(1, n // world, code) if kind == "rs_ag" else comm.coll_algo(0, n, code)
+
     res = {"check_ms": {}}
-    for mode, fences in (("fences_off", False), ("fences_on", True)):
+    for mode, fences, pl in (("fences_off", False, plan),
+                             ("fences_on", True, _fences_plan(plan, algo_of))):
         comm.set_fences(fences)
         r = {}
-        for name, (kind, kw) in plan.items():
+        for name, (kind, kw) in pl.items():
             t0 = time.perf_counter()
             try:
                 if kind == "ar":

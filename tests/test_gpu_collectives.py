@@ -73,16 +73,17 @@ def test_duplicate_device_rejected():
 
 
 def test_algorithm_choice(monkeypatch):
-    """Library defaults: AR LL up to 64 KiB (2 ranks), direct above; RS / AG
-    LL / direct / ring by bucket size; NCCL_ALGO / NCCL_PROTO force one
-    (vcclCommCollAlgo)."""
+    """Library defaults: AR LL up to 64 KiB (2 ranks), direct up to 64 MiB,
+    the ring above; RS / AG LL / direct / ring by bucket size; NCCL_ALGO /
+    NCCL_PROTO force one (vcclCommCollAlgo)."""
     monkeypatch.setenv("VCCL_ALLOW_SHARED_DEVICE", "1")
     for k in ("NCCL_ALGO", "NCCL_PROTO", "VCCL_LL_THRESHOLD", "VCCL_DIRECT_THRESHOLD",
               "VCCL_LL_RSAG_THRESHOLD", "VCCL_DIRECT_RSAG_THRESHOLD"):
         monkeypatch.delenv(k, raising=False)
     # RS / AG: one-hop LL while the bucket (n blocks) is <= n x the AR LL
     # threshold, one-hop direct up to 64 MiB, the ring above.
-    cases = {None: {(0, 16 << 10): "ll", (0, 17 << 10): "direct", (0, 1 << 28): "direct",
+    cases = {None: {(0, 16 << 10): "ll", (0, 17 << 10): "direct", (0, 1 << 24): "direct",
+                    (0, (1 << 24) + 4): "ring", (0, 1 << 28): "ring",
                     (1, 1 << 10): "ll", (2, 1 << 10): "ll", (1, 16 << 10): "ll",
                     (1, 17 << 10): "direct", (2, 1 << 20): "direct", (1, 1 << 23): "direct",
                     (1, (1 << 23) + 4): "ring", (2, 1 << 26): "ring"},
@@ -193,14 +194,14 @@ def test_multi_process_ranks(n, geom):
         env.update(VCCL_ALLOW_SHARED_DEVICE="1", VCCL_LL_MAX_BLOCKS="32",
                    VCCL_DIRECT_MAX_BLOCKS="16", VCCL_NTHREADS="256", VCCL_CHANNELS_PER_RING="2")
         nch, slot = _ring.n_channels(n, per_ring=2), 512 << 10
-        ll_max, direct_max, chunk = 128 << 10, 1 << 62, 16 << 20
+        ll_max, direct_max, chunk = 128 << 10, 64 << 20, 16 << 20
     else:  # library defaults (2 ranks x 32 channels x 1024 threads fit on one GPU)
         for k in TEST_GEOM:
             env.pop(k, None)
         env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         nch, slot = _ring.n_channels(n), 512 << 10
         ll_max = (64 << 10) if n <= 2 else (128 << 10)
-        direct_max, chunk = 1 << 62, 16 << 20
+        direct_max, chunk = 64 << 20, 16 << 20
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
                                    str(r), str(n), "0", hexid, d], env=env,

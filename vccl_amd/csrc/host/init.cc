@@ -142,8 +142,10 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   // Defaults from tools/sweep_ring.py (profiles/r01_sweep_ring*.log): a
   // channel is one workgroup whose throughput is bounded by the per-slot
   // credit round trip, so bandwidth scales with channels: 8 per ring for the
-  // 8- and 4-GPU ring sets (56 / 48 workgroups), 32 for 2 GPUs.
-  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : 32);
+  // 8- and 4-GPU ring sets (56 / 48 workgroups), 48 for 2 GPUs
+  // (profiles/r02g/sweep_ring_1g.log: 16 / 32 / 48 channels -> 199 / 299 /
+  // 436 GB/s busbw at 1 GiB, 2 ranks on one GPU).
+  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : 48);
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
   // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490)
   nch = std::max(c->minCTAs, std::min(nch, c->maxCTAs));
@@ -225,16 +227,16 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       HIPCHECK(hipIpcGetMemHandle(&me.llHandle, c->llBuf));
       me.llPtr = c->llBuf;
     }
-    // Inbox of the two-shot direct all-reduce (direct.hpp) for buckets in
-    // (LL threshold, VCCL_DIRECT_THRESHOLD]: 2 phases x n regions of one
-    // shard of a VCCL_DIRECT_CHUNK_BYTES chunk each, plus the epoch flags.
-    // Larger buckets stream through the inbox chunk by chunk.  Default: every
-    // all-reduce above the LL threshold (n <= 8) — it beat the SIMPLE ring at
-    // every size in the rehearsals (same wire bytes, 2 hops instead of
-    // 2(n-1)); the ring stays for reduce-scatter / all-gather, n > 8 and
-    // NCCL_ALGO=Ring.
+    // Inbox of the direct collectives (direct.hpp): 2 phases x n regions of
+    // one shard of a VCCL_DIRECT_CHUNK_BYTES chunk each, plus the epoch
+    // flags.  Larger buckets stream through the inbox chunk by chunk.
+    // Two-shot direct all-reduce up to VCCL_DIRECT_THRESHOLD (64 MiB), the
+    // SIMPLE ring above: the ring, with VCCL's own partition, is the
+    // north-star path and keeps VCCL's fold order for large buckets; the
+    // direct path's two hops (vs 2(n-1)) matter where the per-hop latency
+    // does, i.e. small and mid buckets.
     c->directMaxBytes =
-        n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_THRESHOLD", (int64_t)1 << 62) : 0;
+        n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_THRESHOLD", (int64_t)64 << 20) : 0;
     c->directMaxBlocks = (int)std::max<int64_t>(
         1, std::min<int64_t>(param_int("DIRECT_MAX_BLOCKS", 64), kDirectMaxBlocks));
     // Reduce-scatter / all-gather (the whole bucket, n blocks): one-hop LL
