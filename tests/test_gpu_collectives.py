@@ -38,7 +38,8 @@ os.environ.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
 TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": str(256 << 10),
              "VCCL_ALLOW_SHARED_DEVICE": "1", "VCCL_LL_THRESHOLD": str(1 << 20),
              "VCCL_LL_MAX_BLOCKS": "32", "VCCL_DIRECT_THRESHOLD": str(4 << 20),
-             "VCCL_DIRECT_MAX_BLOCKS": "16", "VCCL_DIRECT_CHUNK_BYTES": str(1 << 20)}
+             "VCCL_DIRECT_MAX_BLOCKS": "16", "VCCL_DIRECT_CHUNK_BYTES": str(1 << 20),
+             "VCCL_DIRECT_RSAG_THRESHOLD": str(64 << 20)}
 LL_DEFAULT = 1 << 20
 DIRECT_TEST = 4 << 20
 DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in chunks
@@ -80,13 +81,13 @@ def test_algorithm_choice(monkeypatch):
     for k in ("NCCL_ALGO", "NCCL_PROTO", "VCCL_LL_THRESHOLD", "VCCL_DIRECT_THRESHOLD",
               "VCCL_LL_RSAG_THRESHOLD", "VCCL_DIRECT_RSAG_THRESHOLD"):
         monkeypatch.delenv(k, raising=False)
-    # RS / AG: one-hop LL while the bucket (n blocks) is <= n x the AR LL
-    # threshold, one-hop direct up to 64 MiB, the ring above.
+    # RS / AG at 2 ranks: one-hop LL while the bucket (n blocks) is <= n x
+    # the AR LL threshold, the ring above (the one-hop direct path needs
+    # n >= 4 by default: it saves n-2 hops).
     cases = {None: {(0, 16 << 10): "ll", (0, 17 << 10): "direct", (0, 1 << 24): "direct",
                     (0, (1 << 24) + 4): "ring", (0, 1 << 28): "ring",
                     (1, 1 << 10): "ll", (2, 1 << 10): "ll", (1, 16 << 10): "ll",
-                    (1, 17 << 10): "direct", (2, 1 << 20): "direct", (1, 1 << 23): "direct",
-                    (1, (1 << 23) + 4): "ring", (2, 1 << 26): "ring"},
+                    (1, 17 << 10): "ring", (2, 1 << 20): "ring", (2, 1 << 26): "ring"},
              "Ring": {(0, 1 << 10): "ring", (0, 1 << 20): "ring", (1, 1 << 10): "ring",
                       (2, 1 << 20): "ring"},
              "Tree": {(0, 1 << 10): "ll", (0, 1 << 20): "ring", (1, 1 << 10): "ll",

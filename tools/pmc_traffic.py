@@ -27,7 +27,7 @@ def run_pass(counter):
     d = os.path.join(OUT, f"pmc_{counter.lower()}")
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2", "--no-cpu"]
-    subprocess.run(cmd, check=True, timeout=600, cwd=ROOT)
+    subprocess.run(cmd, check=True, timeout=180, cwd=ROOT)
     return d
 
 

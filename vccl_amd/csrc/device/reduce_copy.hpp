@@ -423,7 +423,12 @@ __device__ __forceinline__ u32x4 realign(u32x4 cur, u32x4 ext, int k) {
 // the wave: lane 0 stores the first 16 - k bytes of its result and the last
 // valid lane the last k bytes, each as <= 4 naturally aligned 8/4/2/1-byte
 // stores; the neighbouring wave's ends fill the rest of those packs (disjoint
-// bytes).  Every body byte is written exactly once.
+// bytes).  Every body byte is written exactly once.  Measured (2 x 256 MiB
+// f32 -> destinations at +0 / +4 B, profiles/r02f, r02g, r02h): 5.55 TB/s
+// with the partial stores write-through like the rest (element path before:
+// 3.6); plain partial stores 2.7 (two partial writes of one line meet in L2
+// and reach HBM as read-modify-writes); completing wave-boundary packs
+// through LDS after a workgroup barrier 5.0.
 
 // Bytes [from, from + 8) of the 16-byte value (lo | hi << 64), zero past 16.
 __device__ __forceinline__ uint64_t bytes_at(uint64_t lo, uint64_t hi, int from) {
@@ -459,11 +464,7 @@ __device__ __forceinline__ void st_partial(char* addr, u32x4 v, int from, int to
 // destination, k bytes past alignment).  Every lane of the wave must call it
 // (the shuffle); `valid` = p < nPacks, `nextValid` = this lane's successor
 // pack is in the body and held by the next lane.
-// PP: policy of the partial stores.  The grid kernels store them plainly
-// (write-back): the two halves of a wave-boundary pack then merge in L2
-// instead of reaching HBM as two byte-masked write-throughs.  Ring FIFO slots
-// keep the slot's system-coherent policy (the peer reads them).
-template <int P, int PP = P>
+template <int P>
 __device__ __forceinline__ void st16_realigned(char* dst, int k, int64_t p, u32x4 v, bool valid,
                                                bool nextValid) {
   if (k == 0) {
@@ -477,23 +478,19 @@ __device__ __forceinline__ void st16_realigned(char* dst, int k, int64_t p, u32x
   nxt.w = __shfl_down(v.w, 1);
   if (!valid) return;
   char* at = dst + p * 16;
-  if (__lane_id() == 0) st_partial<PP>(at, v, 0, 16 - k);
+  if (__lane_id() == 0) st_partial<P>(at, v, 0, 16 - k);
   if (nextValid && __lane_id() != 63) st16<P>(dst - k, (p + 1) * 16, funnel16(v, nxt, 16 - k));
-  else st_partial<PP>(at, v, 16 - k, 16);
+  else st_partial<P>(at, v, 16 - k, 16);
 }
-template <int POLS, bool PLAIN_PARTIALS = false>
+template <int POLS>
 __device__ __forceinline__ void st16_dst_realigned(const RCArgs& a, int d, int k, int64_t p, u32x4 v,
                                                    bool valid, bool nextValid) {
-#define VCCL_RA(D, PTR)                                                                        \
-  st16_realigned<dst_pol(POLS, D), PLAIN_PARTIALS ? kPlain : dst_pol(POLS, D)>(PTR, k, p, v, valid, \
-                                                                             nextValid)
   switch (d) {
-    case 0: VCCL_RA(0, a.dsts[0]); return;
-    case 1: VCCL_RA(1, a.dsts[1]); return;
-    case 2: VCCL_RA(2, a.dsts[2]); return;
-    default: VCCL_RA(3, dst_ptr(a, d)); return;
+    case 0: st16_realigned<dst_pol(POLS, 0)>(a.dsts[0], k, p, v, valid, nextValid); return;
+    case 1: st16_realigned<dst_pol(POLS, 1)>(a.dsts[1], k, p, v, valid, nextValid); return;
+    case 2: st16_realigned<dst_pol(POLS, 2)>(a.dsts[2], k, p, v, valid, nextValid); return;
+    default: st16_realigned<dst_pol(POLS, 3)>(dst_ptr(a, d), k, p, v, valid, nextValid); return;
   }
-#undef VCCL_RA
 }
 
 // Body packs [0, nPacks) when every destination is 16-byte aligned and source
@@ -549,120 +546,6 @@ __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, 
       for (int d = 0; d < ND; d++) {
         if constexpr (DSTR) st16_dst_realigned<POLS>(a, d, kd[d], p, acc, p < nPacks, p + 1 < nPacks);
         else if (p < nPacks) st16_dst<POLS>(a, d, p * 16, acc);
-      }
-    }
-  }
-}
-
-template <int POLS>
-__device__ __forceinline__ void st_partial_dst(const RCArgs&, int d, char* at, u32x4 v, int from,
-                                               int to) {
-  switch (d) {
-    case 0: st_partial<dst_pol(POLS, 0)>(at, v, from, to); return;
-    case 1: st_partial<dst_pol(POLS, 1)>(at, v, from, to); return;
-    case 2: st_partial<dst_pol(POLS, 2)>(at, v, from, to); return;
-    default: st_partial<dst_pol(POLS, 3)>(at, v, from, to); return;
-  }
-}
-
-// Grid-kernel variant for destinations at other misalignments than
-// destination 0: the wave-boundary packs are completed through LDS instead
-// of partial stores.  Each wave's lane 0 publishes its results; after one
-// barrier lane 63 funnels its result with the next wave's (or, at the wave
-// boundary between unroll steps, wave 0's of the next step) and stores a full
-// aligned pack, so partial stores remain only at the hunk's two ends (2 per
-// 2 x nthreads packs instead of 2 per 64 packs: partial writes reach HBM as
-// read-modify-writes).  Whole-workgroup control flow: every thread runs every
-// hunk iteration (the barrier), inactive waves only skip the work.
-template <class Fn, int NS, int ND, int UNROLL, int POLS>
-__device__ __forceinline__ void rc_hunks_shifted_xdst(const Fn& fn, const RCArgs& a, int64_t nPacks,
-                                                      int64_t worker, int64_t nWorkers, int tid,
-                                                      int nthreads) {
-  static_assert(NS >= 1 && NS <= kMaxSrcs && ND >= 1, "compile-time operand counts");
-  __shared__ u32x4 edge[2][UNROLL][16];  // lane-0 results per wave, double-buffered by hunk
-  const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
-  const int64_t nHunks = (nPacks + hunkPacks - 1) / hunkPacks;
-  const int lane = __lane_id(), wave = tid >> 6, nWaves = nthreads >> 6;
-  const bool last = lane == 63;
-  int k[NS], kd[ND];
-#pragma unroll
-  for (int s = 0; s < NS; s++) k[s] = (int)((uintptr_t)src_ptr(a, s) & 15);
-#pragma unroll
-  for (int d = 0; d < ND; d++) kd[d] = (int)((uintptr_t)dst_ptr(a, d) & 15);
-  int par = 0;
-  for (int64_t h = worker; h < nHunks; h += nWorkers, par ^= 1) {
-    const int64_t p0 = h * hunkPacks + tid;
-    const bool active = p0 - lane < nPacks;  // wave-uniform
-    u32x4 acc[UNROLL];
-    if (active) {
-      u32x4 cur[NS][UNROLL], ext[NS][UNROLL];
-#pragma unroll
-      for (int s = 0; s < NS; s++)
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++)
-          cur[s][u] = ld16_body_src<POLS>(a, s, k[s], p0 + (int64_t)u * nthreads, nPacks);
-#pragma unroll
-      for (int s = 0; s < NS; s++)
-#pragma unroll
-        for (int u = 0; u < UNROLL; u++) {
-          ext[s][u] = cur[s][u];
-          const int64_t pn = p0 + (int64_t)u * nthreads + 1;
-          if (k[s] != 0 && last)
-            ext[s][u] = ld16_succ_src<POLS>(a, s, k[s], (pn < nPacks ? pn : nPacks) * 16);
-        }
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++) {
-        u32x4 r = k[0] ? realign(cur[0][u], ext[0][u], k[0]) : cur[0][u];
-        if (Fn::kPreOp && a.preOpSrcs > 0) r = pack_preop(fn, r);
-#pragma unroll
-        for (int s = 1; s < NS; s++) {
-          u32x4 v = k[s] ? realign(cur[s][u], ext[s][u], k[s]) : cur[s][u];
-          if (Fn::kPreOp && s < a.preOpSrcs) v = pack_preop(fn, v);
-          r = pack_reduce(fn, r, v);
-        }
-        if (Fn::kPostOp && a.postOp) r = pack_postop(fn, r);
-        acc[u] = r;
-        if (lane == 0) edge[par][u][wave] = r;
-      }
-    }
-    __syncthreads();
-    if (!active) continue;
-#pragma unroll
-    for (int u = 0; u < UNROLL; u++) {
-      const int64_t p = p0 + (int64_t)u * nthreads;
-      const bool valid = p < nPacks, nextValid = p + 1 < nPacks;
-      u32x4 nxt;
-      nxt.x = __shfl_down(acc[u].x, 1);
-      nxt.y = __shfl_down(acc[u].y, 1);
-      nxt.z = __shfl_down(acc[u].z, 1);
-      nxt.w = __shfl_down(acc[u].w, 1);
-      // lane 63: the successor pack is lane 0 of the next wave (same unroll
-      // step) or of wave 0 at the next step; none at the hunk's end
-      bool haveNext = !last;
-      if (last) {
-        if (wave + 1 < nWaves) {
-          nxt = edge[par][u][wave + 1];
-          haveNext = true;
-        } else if (u + 1 < UNROLL) {
-          nxt = edge[par][u + 1 < UNROLL ? u + 1 : 0][0];
-          haveNext = true;
-        }
-      }
-      const bool first = lane == 0 && wave == 0 && u == 0;  // the hunk's first pack
-#pragma unroll
-      for (int d = 0; d < ND; d++) {
-        char* dp = dst_ptr(a, d);
-        const int kk = kd[d];
-        if (kk == 0) {
-          if (valid) st16_dst<POLS>(a, d, p * 16, acc[u]);
-          continue;
-        }
-        if (!valid) continue;
-        if (first) st_partial_dst<POLS>(a, d, dp + p * 16, acc[u], 0, 16 - kk);
-        if (nextValid && haveNext)
-          st16_dst<POLS>(a, d, (p + 1) * 16 - kk, funnel16(acc[u], nxt, 16 - kk));
-        else
-          st_partial_dst<POLS>(a, d, dp + p * 16, acc[u], 16 - kk, 16);
       }
     }
   }
@@ -795,16 +678,7 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
   if (nPacks > 0) {
     // batched loads for the grid kernels; the in-ring copy (PIPE, a 1024-thread
     // workgroup with a 128-VGPR budget) keeps the lean one-pack loop
-    bool dstsShared = true;  // every destination aligned past the head
-    for (int d = 1; d < b.nDsts; d++) dstsShared = dstsShared && ((uintptr_t)dst_ptr(b, d) & 15) == 0;
-    if constexpr (NS >= 1 && ND >= 2 && !PIPE && DSTR) {
-      if (!dstsShared)
-        rc_hunks_shifted_xdst<Fn, NS, ND, (UNROLL < 2 ? UNROLL : 2), POLS>(fn, b, nPacks, worker,
-                                                                            nWorkers, tid, nthreads);
-      else
-        rc_hunks_shifted<Fn, NS, ND, (UNROLL < 2 ? UNROLL : 2), POLS, DSTR>(fn, b, nPacks, worker,
-                                                                            nWorkers, tid, nthreads);
-    } else if constexpr (NS >= 1 && ND >= 1 && !PIPE)
+    if constexpr (NS >= 1 && ND >= 1 && !PIPE)
       rc_hunks_shifted<Fn, NS, ND, (UNROLL < 2 ? UNROLL : 2), POLS, DSTR>(fn, b, nPacks, worker,
                                                                           nWorkers, tid, nthreads);
     else

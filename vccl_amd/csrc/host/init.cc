@@ -247,8 +247,12 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     c->llRsAgMaxBytes = n <= kOrderMaxRanks && c->llMaxBytes > 0
                             ? (size_t)param_int("LL_RSAG_THRESHOLD", (int64_t)n * c->llMaxBytes)
                             : 0;
+    // (The one-hop path saves n-2 hops over the ring: nothing at n = 2, and
+    // the 2-rank rehearsal has the ring ahead at 1-8 MiB, profiles/r02h; at
+    // n = 8 the one-hop paths lead at <= 1 MiB, profiles/r02e/lat_n8.log.)
     c->directRsAgMaxBytes =
-        n <= kDirectMaxRanks ? (size_t)param_int("DIRECT_RSAG_THRESHOLD", (int64_t)64 << 20) : 0;
+        n <= kDirectMaxRanks
+            ? (size_t)param_int("DIRECT_RSAG_THRESHOLD", n >= 4 ? (int64_t)64 << 20 : 0) : 0;
     if (c->directMaxBytes > c->llMaxBytes || c->directRsAgMaxBytes > c->llRsAgMaxBytes) {
       const int64_t chunk = std::max<int64_t>(param_int("DIRECT_CHUNK_BYTES", 16 << 20), 64 << 10);
       c->dRegionBytes = (chunk + n - 1) / n / 256 * 256 + 256;
