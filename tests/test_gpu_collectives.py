@@ -74,9 +74,10 @@ def test_duplicate_device_rejected():
 
 
 def test_algorithm_choice(monkeypatch):
-    """Library defaults: AR LL up to 64 KiB (2 ranks), direct up to 64 MiB,
-    the ring above; RS / AG LL / direct / ring by bucket size; NCCL_ALGO /
-    NCCL_PROTO force one (vcclCommCollAlgo)."""
+    """Library defaults at 2 ranks: AR LL up to 64 KiB, the ring above (the
+    direct path defaults up to 64 MiB from 4 ranks); RS / AG LL / ring by
+    bucket size; NCCL_ALGO / NCCL_PROTO force one (vcclCommCollAlgo), Direct
+    for any size."""
     monkeypatch.setenv("VCCL_ALLOW_SHARED_DEVICE", "1")
     for k in ("NCCL_ALGO", "NCCL_PROTO", "VCCL_LL_THRESHOLD", "VCCL_DIRECT_THRESHOLD",
               "VCCL_LL_RSAG_THRESHOLD", "VCCL_DIRECT_RSAG_THRESHOLD"):
@@ -84,7 +85,7 @@ def test_algorithm_choice(monkeypatch):
     # RS / AG at 2 ranks: one-hop LL while the bucket (n blocks) is <= n x
     # the AR LL threshold, the ring above (the one-hop direct path needs
     # n >= 4 by default: it saves n-2 hops).
-    cases = {None: {(0, 16 << 10): "ll", (0, 17 << 10): "direct", (0, 1 << 24): "direct",
+    cases = {None: {(0, 16 << 10): "ll", (0, 17 << 10): "ring", (0, 1 << 24): "ring",
                     (0, (1 << 24) + 4): "ring", (0, 1 << 28): "ring",
                     (1, 1 << 10): "ll", (2, 1 << 10): "ll", (1, 16 << 10): "ll",
                     (1, 17 << 10): "ring", (2, 1 << 20): "ring", (2, 1 << 26): "ring"},
@@ -202,7 +203,7 @@ def test_multi_process_ranks(n, geom):
         env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         nch, slot = _ring.n_channels(n), 512 << 10
         ll_max = (64 << 10) if n <= 2 else (128 << 10)
-        direct_max, chunk = 64 << 20, 16 << 20
+        direct_max, chunk = (64 << 20) if n >= 4 else 0, 16 << 20
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
                                    str(r), str(n), "0", hexid, d], env=env,

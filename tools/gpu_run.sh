@@ -8,6 +8,9 @@
 #        n2        bench.py N>1 rehearsal: 2 ranks sharing the one GPU
 #        smoke     __graft_entry__.smoke()
 #        py:<file> python <file> (a tool script)
+#        sweep:<mode>  tools/sweep_rc.py with SWEEP_MODE=<mode> (6 rounds)
+#        pmc       tools/pmc_traffic.py (separate FETCH_SIZE / WRITE_SIZE passes)
+#        lat:<n>   tools/coll_latency.py on n ranks sharing the GPU (LAT_* env)
 # Outputs go to gpurun_out/<label>/.  Every GPU step has its own time limit
 # and the chain stops at the first failure (no retries).
 set -e
@@ -26,6 +29,9 @@ for s in "$@"; do
     n2) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 > $O/bench_n2.json 2> $O/bench_n2.err ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
     py:*) timeout -k 10 600 python -u ${s#py:} > $O/$(basename ${s#py:} .py).log 2>&1 ;;
+    sweep:*) SWEEP_MODE=${s#sweep:} SWEEP_ROUNDS=${SWEEP_ROUNDS:-6} timeout -k 10 300 python -u tools/sweep_rc.py > $O/sweep_${s#sweep:}.log 2>&1 ;;
+    pmc) timeout -k 10 400 python -u tools/pmc_traffic.py > $O/pmc_traffic.log 2>&1 && cp gpurun_out/pmc_traffic.json $O/ ;;
+    lat:*) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#lat:} --master-addr 127.0.0.1 --master-port 29534 tools/coll_latency.py > $O/lat_n${s#lat:}.log 2> $O/lat_n${s#lat:}.err ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

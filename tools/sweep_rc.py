@@ -91,17 +91,17 @@ def main():
 
 def misaligned(n, rounds, reps):
     """2-src f32 sum at the config-2 size with byte offsets (src0, src1, dst):
-    aligned; a shifted source (wavefront-shuffle realignment); a common
-    misalignment (head/tail elements + aligned body); destinations that
-    differ from the sources AND each other are not in this set (element path,
-    measured as 'elements' by misaligning dst against a 2-dst pair)."""
+    aligned; a shifted source (lane-shift realignment); a common
+    misalignment (head/tail elements + aligned body); two destinations, aligned
+    and at different misalignments (destination realignment)."""
     base = [torch.empty(n * 4 + 64, dtype=torch.uint8, device="cuda") for _ in range(4)]
     for b in base[:2]:
         b.view(torch.float32)[:n] = torch.rand(n, device="cuda")
     s = torch.cuda.current_stream()
     variants = {"aligned": ((0, 0), (0,)), "shifted_src1_+4": ((0, 4), (0,)),
                 "shifted_both_+4_+8": ((4, 8), (0,)), "common_+4": ((4, 4), (4,)),
-                "elements_dsts_0_4": ((0, 0), (0, 4))}
+                "aligned_2dst": ((0, 0), (0, 0)), "dsts_0_4": ((0, 0), (0, 4)),
+                "dsts_0_12": ((0, 0), (0, 12)), "dsts_8_4": ((0, 0), (8, 4))}
     times = {k: [] for k in variants}
     for r in range(rounds):
         for name, (so, do) in variants.items():

@@ -510,7 +510,10 @@ __device__ __forceinline__ uint32_t e5m2x4_add_cvt(uint32_t a, uint32_t b) {
 }
 // Off by default: measured level with the per-element lowering for E5M2
 // (6.62-6.75 TB/s either way, interleaved, profiles/r01z/ab_fp8.log; bit-exact
-// in that run's tests under VCCL_LIB).  -DVCCL_F8_E5M2_CVT selects it.
+// in that run's tests under VCCL_LIB), and slower in round 2 (0.873 vs 0.889
+// of peak, profiles/r02/dtypes_*.log) although it cuts SQ_INSTS_VALU per
+// launch from 64.9 M to 26.3 M (profiles/r02/pmc_valu_e5m2_ab.csv): the
+// 1-byte kernels are not VALU-bound.  -DVCCL_F8_E5M2_CVT selects it.
 #ifdef VCCL_F8_E5M2_CVT
 __device__ __forceinline__ u32x4 pack_reduce(const FnSum<f8e5m2_t>&, u32x4 a, u32x4 b) {
   return u32x4{e5m2x4_add_cvt(a.x, b.x), e5m2x4_add_cvt(a.y, b.y), e5m2x4_add_cvt(a.z, b.z),

@@ -402,33 +402,81 @@ __device__ __forceinline__ u32x4 ld16_succ_src(const RCArgs& a, int s, int k, in
     default: return ld16<src_pol(POLS, 3)>(src_ptr(a, s) - k, off);
   }
 }
-// This lane's pack funnel-shifted with the next lane's (wavefront shuffle);
-// lane 63 supplies `ext`, its own load of the successor pack.
+// The next lane's value (lane l gets lane l+1's), lane 63 gets `fill`: one
+// DPP `wave_shl:1` move per dword (a VALU op; lanes whose source lies past
+// the wave keep the old value), no LDS round trip as ds_bpermute would take.
+// Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130 /* wave_shl:1 */, 0xf, 0xf,
+                                               false);
+}
+__device__ __forceinline__ u32x4 from_next_lane(u32x4 v, u32x4 fill) {
+  u32x4 o;
+  o.x = from_next_lane(v.x, fill.x);
+  o.y = from_next_lane(v.y, fill.y);
+  o.z = from_next_lane(v.z, fill.z);
+  o.w = from_next_lane(v.w, fill.w);
+  return o;
+}
+// The previous lane's value (lane l gets lane l-1's), lane 0 gets `fill`
+// (DPP `wave_shr:1`).
+__device__ __forceinline__ u32x4 from_prev_lane(u32x4 v, u32x4 fill) {
+  u32x4 o;
+  o.x = (uint32_t)__builtin_amdgcn_update_dpp((int)fill.x, (int)v.x, 0x138, 0xf, 0xf, false);
+  o.y = (uint32_t)__builtin_amdgcn_update_dpp((int)fill.y, (int)v.y, 0x138, 0xf, 0xf, false);
+  o.z = (uint32_t)__builtin_amdgcn_update_dpp((int)fill.z, (int)v.z, 0x138, 0xf, 0xf, false);
+  o.w = (uint32_t)__builtin_amdgcn_update_dpp((int)fill.w, (int)v.w, 0x138, 0xf, 0xf, false);
+  return o;
+}
+// Lane 63's value in every lane.
+__device__ __forceinline__ u32x4 lane63_of(u32x4 v) {
+  u32x4 o;
+  o.x = __builtin_amdgcn_readlane(v.x, 63);
+  o.y = __builtin_amdgcn_readlane(v.y, 63);
+  o.z = __builtin_amdgcn_readlane(v.z, 63);
+  o.w = __builtin_amdgcn_readlane(v.w, 63);
+  return o;
+}
+// Lane 0's value in every lane (v_readlane into scalar registers).
+__device__ __forceinline__ u32x4 lane0_of(u32x4 v) {
+  u32x4 o;
+  o.x = __builtin_amdgcn_readlane(v.x, 0);
+  o.y = __builtin_amdgcn_readlane(v.y, 0);
+  o.z = __builtin_amdgcn_readlane(v.z, 0);
+  o.w = __builtin_amdgcn_readlane(v.w, 0);
+  return o;
+}
+// This lane's pack funnel-shifted with the next lane's; lane 63 supplies
+// `ext`, the successor pack (its own load, or lane 0 of the wave's next pack
+// row).
 __device__ __forceinline__ u32x4 realign(u32x4 cur, u32x4 ext, int k) {
-  u32x4 nxt;
-  nxt.x = __shfl_down(cur.x, 1);
-  nxt.y = __shfl_down(cur.y, 1);
-  nxt.z = __shfl_down(cur.z, 1);
-  nxt.w = __shfl_down(cur.w, 1);
-  if (__lane_id() == 63) nxt = ext;
-  return funnel16(cur, nxt, k);
+  return funnel16(cur, from_next_lane(cur, ext), k);
 }
 
 // ------------------------------------------------- misaligned destinations
-// Destination d whose address is k_d bytes past a 16-byte boundary where
-// destination 0 is aligned (the body's reference): its aligned pack holding
-// body bytes [16p + 16 - k, 16p + 32 - k) is bytes [16 - k, 32 - k) of this
-// lane's result and the next lane's (wavefront shuffle + funnel shift, the
-// source realignment run backwards).  A wave's two ends have no neighbour in
-// the wave: lane 0 stores the first 16 - k bytes of its result and the last
-// valid lane the last k bytes, each as <= 4 naturally aligned 8/4/2/1-byte
-// stores; the neighbouring wave's ends fill the rest of those packs (disjoint
-// bytes).  Every body byte is written exactly once.  Measured (2 x 256 MiB
-// f32 -> destinations at +0 / +4 B, profiles/r02f, r02g, r02h): 5.55 TB/s
-// with the partial stores write-through like the rest (element path before:
-// 3.6); plain partial stores 2.7 (two partial writes of one line meet in L2
-// and reach HBM as read-modify-writes); completing wave-boundary packs
-// through LDS after a workgroup barrier 5.0.
+// Destination d whose body starts k bytes past a 16-byte boundary A (where
+// destination 0, the body's reference, is aligned): its aligned pack q
+// (address A + 16q) holds body bytes [16q - k, 16q + 16 - k), i.e. the last
+// k bytes of body pack q - 1 and the first 16 - k of pack q.  The lane
+// holding pack p stores aligned pack q = p, funnelling the previous lane's
+// result with its own (DPP lane shift + v_alignbyte, the source realignment
+// run backwards), so a wave row of 64 packs stores 64 aligned packs — whole
+// 64 B lines when A is line-aligned, as for a buffer offset by k.  Lane 0's
+// previous pack is lane 63's of the wave's previous row (v_readlane); only a
+// wave span's two ends store partial packs: its first lane the first
+// 16 - k bytes of its result, its last valid lane the last k bytes, each as
+// <= 4 naturally aligned 8/4/2/1-byte stores (the neighbouring span's ends
+// fill the rest of those packs).  Every body byte is written exactly once.
+// Measured (2 x 256 MiB f32 -> 2 x 256 MiB, profiles/r02l): destinations at
+// +0 / +4 B 5.85 TB/s, +0 / +12 B 5.85, against 6.25 for the same operands
+// all aligned (two destinations: half the traffic is writes) — 0.94 of the
+// aligned rate.  Before: the element path 3.6 (round 1); pack q = p + 1 per
+// lane (rows ending mid-line) with partial stores at every row's ends
+// 5.0-5.55 (profiles/r02e, r02f); plain (write-back) partial stores 2.7 (two
+// partial writes of one line meet in L2 and reach HBM as read-modify-writes,
+// profiles/r02g); wave-boundary packs completed through LDS after a
+// workgroup barrier 5.0 (profiles/r02h); 4-row spans 5.0 (fewer partials,
+// half the waves in flight, profiles/r02l_r4).
 
 // Bytes [from, from + 8) of the 16-byte value (lo | hi << 64), zero past 16.
 __device__ __forceinline__ uint64_t bytes_at(uint64_t lo, uint64_t hi, int from) {
@@ -462,43 +510,53 @@ __device__ __forceinline__ void st_partial(char* addr, u32x4 v, int from, int to
 }
 // Store body pack p (value v) to destination `dst` (the body start of that
 // destination, k bytes past alignment).  Every lane of the wave must call it
-// (the shuffle); `valid` = p < nPacks, `nextValid` = this lane's successor
-// pack is in the body and held by the next lane.
+// (the lane shift); `valid` = p < nPacks, `nextValid` = p + 1 < nPacks.
+// `prevOk`: `prev` is pack p - 1 (lane 63 of the wave's previous row), so
+// lane 0 stores a whole pack instead of its first 16 - k bytes; `lastRow`:
+// lane 63's last k bytes are not stored by a next row's lane 0.
 template <int P>
-__device__ __forceinline__ void st16_realigned(char* dst, int k, int64_t p, u32x4 v, bool valid,
+__device__ __forceinline__ void st16_realigned(char* dst, int k, int64_t p, u32x4 v, u32x4 prev,
+                                               bool prevOk, bool lastRow, bool valid,
                                                bool nextValid) {
   if (k == 0) {
     if (valid) st16<P>(dst, p * 16, v);
     return;
   }
-  u32x4 nxt;
-  nxt.x = __shfl_down(v.x, 1);
-  nxt.y = __shfl_down(v.y, 1);
-  nxt.z = __shfl_down(v.z, 1);
-  nxt.w = __shfl_down(v.w, 1);
+  const u32x4 pv = from_prev_lane(v, prev);
   if (!valid) return;
   char* at = dst + p * 16;
-  if (__lane_id() == 0) st_partial<P>(at, v, 0, 16 - k);
-  if (nextValid && __lane_id() != 63) st16<P>(dst - k, (p + 1) * 16, funnel16(v, nxt, 16 - k));
-  else st_partial<P>(at, v, 16 - k, 16);
+  if (prevOk || __lane_id() != 0) st16<P>(dst - k, p * 16, funnel16(pv, v, 16 - k));
+  else st_partial<P>(at, v, 0, 16 - k);
+  if (!nextValid || (lastRow && __lane_id() == 63)) st_partial<P>(at, v, 16 - k, 16);
 }
 template <int POLS>
 __device__ __forceinline__ void st16_dst_realigned(const RCArgs& a, int d, int k, int64_t p, u32x4 v,
+                                                   u32x4 prev, bool prevOk, bool lastRow,
                                                    bool valid, bool nextValid) {
   switch (d) {
-    case 0: st16_realigned<dst_pol(POLS, 0)>(a.dsts[0], k, p, v, valid, nextValid); return;
-    case 1: st16_realigned<dst_pol(POLS, 1)>(a.dsts[1], k, p, v, valid, nextValid); return;
-    case 2: st16_realigned<dst_pol(POLS, 2)>(a.dsts[2], k, p, v, valid, nextValid); return;
-    default: st16_realigned<dst_pol(POLS, 3)>(dst_ptr(a, d), k, p, v, valid, nextValid); return;
+#define VCCL_ST_CASE(D, PTR)                                                                     \
+  case D:                                                                                        \
+    st16_realigned<dst_pol(POLS, D)>(PTR, k, p, v, prev, prevOk, lastRow, valid, nextValid);     \
+    return;
+    VCCL_ST_CASE(0, a.dsts[0])
+    VCCL_ST_CASE(1, a.dsts[1])
+    VCCL_ST_CASE(2, a.dsts[2])
+    default:
+    VCCL_ST_CASE(3, dst_ptr(a, d))
+#undef VCCL_ST_CASE
   }
 }
 
-// Body packs [0, nPacks) when every destination is 16-byte aligned and source
-// s starts k_s bytes past a 16-byte boundary (some k_s != 0).  Whole waves
-// run (the shuffle needs every lane); a lane past the end loads clamped packs
-// and stores nothing.  NS / ND compile-time (NS > 0): every load of a hunk —
-// the aligned packs and lane 63's successor packs — is issued before the
-// first shuffle, so their latencies overlap.
+// Body packs [0, nPacks) when some operand is not 16-byte aligned on the
+// body (source s k_s bytes past a boundary, destination d k_d bytes).  A hunk
+// gives every wave UNROLL consecutive rows of 64 packs (row u = packs
+// [64u, 64u + 64) of the wave's span), so lane 63's successor pack in row u
+// is lane 0's pack of row u + 1 (a v_readlane): only the span's last row
+// loads lane 63's successor itself, and only the span's two ends store
+// partial destination packs.  Whole waves run (the lane shift needs every
+// lane); a lane past the end loads clamped packs and stores nothing.  NS / ND
+// compile-time (NS > 0): every load of a hunk is issued before the first
+// lane shift, so their latencies overlap.  nthreads is a multiple of 64.
 template <class Fn, int NS, int ND, int UNROLL, int POLS, bool DSTR>
 __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, int64_t nPacks,
                                                  int64_t worker, int64_t nWorkers, int tid,
@@ -506,46 +564,58 @@ __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, 
   static_assert(NS >= 1 && NS <= kMaxSrcs, "compile-time source count");
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t nHunks = (nPacks + hunkPacks - 1) / hunkPacks;
-  const bool last = __lane_id() == 63;
+  const int lane = __lane_id();
+  const bool last = lane == 63;
   int k[NS], kd[ND];
 #pragma unroll
   for (int s = 0; s < NS; s++) k[s] = (int)((uintptr_t)src_ptr(a, s) & 15);
 #pragma unroll
   for (int d = 0; d < ND; d++) kd[d] = DSTR ? (int)((uintptr_t)dst_ptr(a, d) & 15) : 0;
   for (int64_t h = worker; h < nHunks; h += nWorkers) {
-    const int64_t p0 = h * hunkPacks + tid;
-    if (p0 - __lane_id() >= nPacks) continue;  // the whole wave is past the end
-    u32x4 cur[NS][UNROLL], ext[NS][UNROLL];
+    // this wave's span: UNROLL rows of 64 consecutive packs
+    const int64_t p0 = h * hunkPacks + (int64_t)(tid - lane) * UNROLL + lane;
+    if (p0 - lane >= nPacks) continue;  // the whole wave is past the end
+    u32x4 cur[NS][UNROLL];
 #pragma unroll
     for (int s = 0; s < NS; s++)
 #pragma unroll
       for (int u = 0; u < UNROLL; u++)
-        cur[s][u] = ld16_body_src<POLS>(a, s, k[s], p0 + (int64_t)u * nthreads, nPacks);
+        cur[s][u] = ld16_body_src<POLS>(a, s, k[s], p0 + 64 * u, nPacks);
+    u32x4 extLast[NS];  // lane 63's successor of the span's last row
 #pragma unroll
-    for (int s = 0; s < NS; s++)
-#pragma unroll
-      for (int u = 0; u < UNROLL; u++) {
-        ext[s][u] = cur[s][u];
-        const int64_t pn = p0 + (int64_t)u * nthreads + 1;
-        if (k[s] != 0 && last)
-          ext[s][u] = ld16_succ_src<POLS>(a, s, k[s], (pn < nPacks ? pn : nPacks) * 16);
-      }
+    for (int s = 0; s < NS; s++) {
+      extLast[s] = cur[s][UNROLL - 1];
+      const int64_t pn = p0 + 64 * (UNROLL - 1) + 1;
+      if (k[s] != 0 && last)
+        extLast[s] = ld16_succ_src<POLS>(a, s, k[s], (pn < nPacks ? pn : nPacks) * 16);
+    }
+    u32x4 acc[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
-      const int64_t p = p0 + (int64_t)u * nthreads;
-      u32x4 acc = k[0] ? realign(cur[0][u], ext[0][u], k[0]) : cur[0][u];
-      if (Fn::kPreOp && a.preOpSrcs > 0) acc = pack_preop(fn, acc);
+      auto src = [&](int s) __attribute__((always_inline)) -> u32x4 {
+        if (!k[s]) return cur[s][u];
+        return realign(cur[s][u], u + 1 < UNROLL ? lane0_of(cur[s][u + 1]) : extLast[s], k[s]);
+      };
+      acc[u] = src(0);
+      if (Fn::kPreOp && a.preOpSrcs > 0) acc[u] = pack_preop(fn, acc[u]);
 #pragma unroll
       for (int s = 1; s < NS; s++) {
-        u32x4 v = k[s] ? realign(cur[s][u], ext[s][u], k[s]) : cur[s][u];
+        u32x4 v = src(s);
         if (Fn::kPreOp && s < a.preOpSrcs) v = pack_preop(fn, v);
-        acc = pack_reduce(fn, acc, v);
+        acc[u] = pack_reduce(fn, acc[u], v);
       }
-      if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
+      if (Fn::kPostOp && a.postOp) acc[u] = pack_postop(fn, acc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; u++) {
+      const int64_t p = p0 + 64 * u;
 #pragma unroll
       for (int d = 0; d < ND; d++) {
-        if constexpr (DSTR) st16_dst_realigned<POLS>(a, d, kd[d], p, acc, p < nPacks, p + 1 < nPacks);
-        else if (p < nPacks) st16_dst<POLS>(a, d, p * 16, acc);
+        if constexpr (DSTR)
+          st16_dst_realigned<POLS>(a, d, kd[d], p, acc[u], u > 0 ? lane63_of(acc[u > 0 ? u - 1 : 0]) : acc[u],
+                                   u > 0, u + 1 == UNROLL, p < nPacks, p + 1 < nPacks);
+        else if (p < nPacks)
+          st16_dst<POLS>(a, d, p * 16, acc[u]);
       }
     }
   }
@@ -579,8 +649,8 @@ __device__ __forceinline__ void rc_hunks_shifted_rt(const Fn& fn, const RCArgs& 
     if (Fn::kPostOp && a.postOp) acc = pack_postop(fn, acc);
     for (int d = 0; d < a.nDsts; d++) {
       if constexpr (DSTR)
-        st16_dst_realigned<POLS>(a, d, (int)((uintptr_t)dst_ptr(a, d) & 15), p, acc, p < nPacks,
-                                 p + 1 < nPacks);
+        st16_dst_realigned<POLS>(a, d, (int)((uintptr_t)dst_ptr(a, d) & 15), p, acc, acc, false,
+                                 true, p < nPacks, p + 1 < nPacks);
       else if (p < nPacks)
         st16_dst<POLS>(a, d, p * 16, acc);
     }
@@ -635,6 +705,12 @@ __device__ __forceinline__ void reduce_copy_aligned(const Fn& fn, const RCArgs& 
 // are realigned in registers (true), or — for callers that never pass them
 // and need the registers (the direct kernels stage a misaligned output
 // through their aligned inbox) — sent to the element path (false).
+#ifndef VCCL_SHIFT_ROWS
+#define VCCL_SHIFT_ROWS 2
+#endif
+// Rows of 64 packs per wave span on the grid kernels' misaligned path (2:
+// 4 measured slower, see above).
+constexpr int kShiftRows = VCCL_SHIFT_ROWS;
 template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false,
           bool DSTR = true>
 __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
@@ -679,8 +755,8 @@ __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64
     // batched loads for the grid kernels; the in-ring copy (PIPE, a 1024-thread
     // workgroup with a 128-VGPR budget) keeps the lean one-pack loop
     if constexpr (NS >= 1 && ND >= 1 && !PIPE)
-      rc_hunks_shifted<Fn, NS, ND, (UNROLL < 2 ? UNROLL : 2), POLS, DSTR>(fn, b, nPacks, worker,
-                                                                          nWorkers, tid, nthreads);
+      rc_hunks_shifted<Fn, NS, ND, (DSTR ? kShiftRows : (UNROLL < 2 ? UNROLL : 2)), POLS, DSTR>(
+          fn, b, nPacks, worker, nWorkers, tid, nthreads);
     else
       rc_hunks_shifted_rt<Fn, POLS, DSTR>(fn, b, nPacks, worker, nWorkers, tid, nthreads);
   }

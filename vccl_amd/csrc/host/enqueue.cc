@@ -563,7 +563,7 @@ static int choose_algo(const Task& t) {
   if (t.coll == kAllReduce) {
     const size_t bytes = t.count * esz;
     llFits = c->llBuf && bytes <= c->llMaxBytes;
-    directFits = c->dBuf && bytes <= c->directMaxBytes;
+    directFits = c->dPeers && bytes <= c->directMaxBytes;
   } else {
     // Reduce-scatter / all-gather: one rank's block must fit an LL slot; the
     // thresholds are on the whole bucket (n blocks), as the reference's tuner
@@ -571,12 +571,13 @@ static int choose_algo(const Task& t) {
     const size_t block = t.count * esz, bytes = block * (size_t)c->nRanks;
     llFits = c->llBuf && c->nRanks <= kOrderMaxRanks && block <= (size_t)c->llLines * 8 &&
              bytes <= c->llRsAgMaxBytes;
-    directFits = c->dBuf && bytes <= c->directRsAgMaxBytes;
+    directFits = c->dPeers && bytes <= c->directRsAgMaxBytes;
   }
   if (c->algoForce == 2) return llFits ? kAlgoLL : kAlgoRing;
   // Forced direct: any bucket the inbox can stream (the size threshold only
-  // steers the automatic choice)
-  if (c->algoForce == 3) return c->dBuf && c->nRanks <= kDirectMaxRanks ? kAlgoDirect : kAlgoRing;
+  // steers the automatic choice); needs every peer's inbox mapped (no net
+  // peers)
+  if (c->algoForce == 3) return c->dPeers && c->nRanks <= kDirectMaxRanks ? kAlgoDirect : kAlgoRing;
   if (llFits) return kAlgoLL;
   if (directFits) return kAlgoDirect;
   return kAlgoRing;
