@@ -43,6 +43,11 @@
  *                     = channelLo, channelHi, countLo, countMid, countHi,
  *                     chunkLo, chunkMid, chunkHi (elements; bytes for
  *                     all-gather, which the reference runs as int8).
+ *   vcclRingChunkOf    for element i of an all-reduce on that partition:
+ *                     out[0] = its channel, out[1] = the ring chunk c of its
+ *                     loop (the chunk that finishes at ring position c,
+ *                     src/device/all_reduce.h:32-64), out[2] = the end of that
+ *                     chunk — the lookup the direct all-reduce folds by.
  */
 #ifndef VCCL_EXT_H_
 #define VCCL_EXT_H_
@@ -74,6 +79,8 @@ ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences);
 ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoch, uint32_t directEpoch);
 ncclResult_t vcclRingPartition(int coll, size_t count, ncclDataType_t datatype, int nRanks,
                                int nChannels, size_t slotBytes, int64_t* out);
+ncclResult_t vcclRingChunkOf(size_t count, ncclDataType_t datatype, int nRanks, int nChannels,
+                             size_t slotBytes, size_t i, int64_t* out);
 
 #ifdef __cplusplus
 }

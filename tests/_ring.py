@@ -6,9 +6,10 @@ follows it, host/enqueue.cc cbd_schedule; the tests take it from the oracle's
 independent restatement, oracle/vccl_sched.py); the ring set per channel and
 the channel count mirror vccl_amd/csrc/host/init.cc.  The oracle's ring_fold
 then reproduces the fold order element by element, so ring results are
-checked bit-exactly against VCCL's schedule on the same rings and channels,
-and the one-shot LL / two-shot direct paths (own fold orders) bit-exactly
-against their own order and within the §8c tolerance of VCCL's.
+checked bit-exactly against VCCL's schedule on the same rings and channels —
+the two-shot direct all-reduce folds in that same order — and the one-shot
+LL all-reduce (VCCL's chain-tree order) bit-exactly against its own order
+and within the §8c tolerance of VCCL's ring result.
 """
 import numpy as np
 
@@ -104,24 +105,3 @@ def direct_chunk_elts(count, n, elt_size, chunk_bytes=16 << 20):
     region = (chunk_bytes + n - 1) // n // 256 * 256 + 256
     unit = n * max(1, 16 // elt_size)
     return min(count, (region - 16) // elt_size * n // unit * unit)
-
-
-def direct_owner(count, n, elt_size, chunk_bytes=16 << 20):
-    """Owner rank of every element: per chunk, shard o belongs to rank o."""
-    chunk = direct_chunk_elts(count, n, elt_size, chunk_bytes)
-    idx = np.arange(count)
-    c0 = idx // chunk * chunk
-    cc = np.minimum(chunk, count - c0)
-    shard = _align_up(_div_up(cc, n), max(1, 16 // elt_size))
-    return ((idx - c0) // shard).astype(np.int32)
-
-
-def expected_direct(op, dtype, inputs, chunk_bytes=16 << 20):
-    """Direct all-reduce: shard o of each chunk (owned by rank o) is folded in
-    the ring order of the identity ring, x_{o+1} (+) ... (+) x_o — the ring
-    all-reduce fold with chunk o finishing at ring index o (all_reduce.h:42-64)."""
-    n = len(inputs)
-    dev_op, arg = O.host_to_dev_redop(op, dtype, n)
-    pre = dev_op == O.DEV_PREMULSUM
-    owner = direct_owner(inputs[0].size, n, inputs[0].dtype.itemsize, chunk_bytes)
-    return O.ring_fold(dev_op, dtype, arg, pre, list(inputs), owner)

@@ -149,23 +149,24 @@ def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
 
 
 def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk):
-    """All-reduce result: LL chain fold up to ll_max bytes, the direct path's
-    fold up to direct_max, the ring's owner-map fold above."""
+    """All-reduce result: LL chain fold up to ll_max bytes, the ring's
+    owner-map fold (VCCL's ring schedule on these channels) above — for the
+    two-shot direct path too, which folds every element in the ring's order
+    (direct.hpp phase 2), so neither direct_max nor the inbox chunk
+    (direct_chunk) changes the expected bits."""
+    del direct_max, direct_chunk
     count = len(ins[0])
     if count * ins[0].dtype.itemsize <= ll_max:
         dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
         return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
-    if count * ins[0].dtype.itemsize <= direct_max:
-        return _ring.expected_direct(op, dt, ins, direct_chunk)
     return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
 
 
 def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20):
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
-    (oracle ref_chain_fold); up to `direct_max` the two-shot direct path
-    (identity-ring fold per shard of each `direct_chunk`-byte chunk); larger
-    ones the ring (owner-map ring fold)."""
+    (oracle ref_chain_fold); larger ones the two-shot direct path (up to
+    `direct_max`) or the ring, both in the ring's owner-map fold."""
     name, coll, op, dt, count = CASES[case_idx]
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace", "ar_mis"):

@@ -4,14 +4,16 @@
 Replays phases 1-3 with numpy over the same shard / block partition and inbox
 region layout the kernel uses, and checks that (a) every write stays inside
 its inbox region, (b) every output element is produced exactly once per rank,
-and (c) the result equals the oracle fold the GPU parity tests expect
-(tests/_ring.py expected_direct), for ragged counts, every element size and
-n = 2..8.  No GPU needed.
+and (c) the result equals the ring all-reduce's (VCCL's ring schedule on the same
+channels and rings, tests/_ring.py expected_allreduce): phase 2 folds every
+element in the order of its ring chunk (direct.hpp, ar_chunk_of), for ragged
+counts, every element size and n = 2..8.  No GPU needed.
 """
 import numpy as np
 import pytest
 
 from oracle import oracle as O
+from oracle import vccl_sched as S
 from tests import _ring
 
 MIN_BLK_BYTES = 16 << 10
@@ -31,13 +33,18 @@ def _geometry(count, n, esz, max_blocks, chunk_bytes):
     return chunk, blk, n_blocks, region
 
 
-def _simulate(op, dtype, inputs, max_blocks=64, chunk_bytes=16 << 20):
+def _simulate(op, dtype, inputs, nch, slot, max_blocks=64, chunk_bytes=16 << 20):
     n = len(inputs)
     dev_op, arg = O.host_to_dev_redop(op, dtype, n)
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size
     esz = inputs[0].dtype.itemsize
     chunk, blk, n_blocks, region = _geometry(count, n, esz, max_blocks, chunk_bytes)
+    # the ring's partition of the bucket: channel and finishing ring position
+    # of every element (what ar_chunk_of looks up on the device)
+    work = S.cbd_schedule("ar", count, esz, n, nch, buff_size=slot * S.NCCL_STEPS)
+    chan, fin = S.allreduce_owner(work, count, n)
+    rings = _ring.ring_orders(n)
     assert n_blocks <= 128
     n_chunks = -(-count // chunk)
     outs = [np.zeros_like(inputs[0]) for _ in range(n)]
@@ -62,14 +69,17 @@ def _simulate(op, dtype, inputs, max_blocks=64, chunk_bytes=16 << 20):
                     off, ln = block_of(p, b)
                     assert in_off + ln * esz <= region, "inbox region overflow"
                     inbox[p, 0, me, b] = inputs[me][off:off + ln].copy()
-            for me in range(n):  # phase 2: srcs x_{me+1}, ..., x_{me-1}, own
+            for me in range(n):  # phase 2: every element in its ring chunk's order
                 off, ln = block_of(me, b)
-                ins = [inbox[me, 0, (me + j) % n, b] for j in range(1, n)] + [inputs[me][off:off + ln]]
-                if ln:
-                    # ring_fold over [x_{me+1}, ..., x_me], finishing at the last position
-                    res = O.ring_fold(dev_op, dtype, arg, pre, ins, np.full(ln, n - 1, np.int32))
-                else:
-                    res = inputs[me][off:off]
+                res = inputs[me][off:off + ln].copy()
+                src = {q: inbox[me, 0, q, b] for q in range(n) if q != me}
+                src[me] = inputs[me][off:off + ln]
+                ch = chan[off:off + ln]
+                for c in np.unique(ch):
+                    sel = np.nonzero(ch == c)[0]
+                    ring = rings[c % len(rings)]
+                    res[sel] = O.ring_fold(dev_op, dtype, arg, pre, [src[q][sel] for q in ring],
+                                           fin[off + sel])
                 outs[me][off:off + ln] = res
                 written[me][off:off + ln] += 1
                 for j in range(1, n):
@@ -99,8 +109,9 @@ def test_direct_simulation_matches_expected(n, dtype, count, chunk_bytes):
     else:
         ins = [rng.uniform(-1, 1, count).astype(O.NP_DTYPE[dtype]) for _ in range(n)]
         op = 4 if dtype == 6 else 0  # f16 avg exercises preOp on every input
-    outs = _simulate(op, dtype, ins, chunk_bytes=chunk_bytes)
-    exp = _ring.expected_direct(op, dtype, ins, chunk_bytes)
+    nch, slot = _ring.n_channels(n), 512 << 10
+    outs = _simulate(op, dtype, ins, nch, slot, chunk_bytes=chunk_bytes)
+    exp = _ring.expected_allreduce(op, dtype, ins, nch, slot)
     for r in range(n):
         assert np.array_equal(outs[r].view(np.uint8), exp.view(np.uint8)), f"rank {r}"
 

@@ -100,3 +100,26 @@ def test_hand_derived_cases():
     # the per-call channel tuning: 1 MiB all-reduce < nc * 512 thr * 64 B for
     # nc > 32, so at most 32 channels carry it (enqueue.cc:1921-1924)
     assert S.ring_n_max_channels("ar", 1 << 18, 4, 8, 56) == 32
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_library_chunk_lookup_equals_oracle(n):
+    """vcclRingChunkOf (ring_types.hpp ar_chunk_of, the lookup the direct
+    all-reduce folds by) vs the oracle's owner map of VCCL's ring all-reduce
+    (channel and finishing ring position of every element): at every chunk
+    boundary (both sides) and at random elements."""
+    rng = np.random.default_rng(n)
+    for nch in (1, 7, 14, 56):
+        for dt in (7, 9, 0, 8):
+            for count in (3, 1000, 65_536 + 8, (1 << 20) + 17, 3_000_001):
+                w = S.cbd_schedule("ar", count, ESZ[dt], n, nch, buff_size=(256 << 10) * S.NCCL_STEPS)
+                chan, owner = S.allreduce_owner(w, count, n)
+                key = chan.astype(np.int64) * 64 + owner
+                starts = np.concatenate([[0], np.nonzero(np.diff(key))[0] + 1])
+                ends = np.concatenate([starts[1:], [count]])
+                pick = set(starts[:200].tolist()) | set((ends[:200] - 1).tolist())
+                pick |= set(rng.integers(0, count, 100).tolist())
+                for i in sorted(pick):
+                    ch, k, end = nccl.ring_chunk_of(count, dt, n, nch, 256 << 10, i)
+                    j = np.searchsorted(starts, i, side="right") - 1
+                    assert (ch, k, end) == (chan[i], owner[i], ends[j]), (n, nch, dt, count, i)

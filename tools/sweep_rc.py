@@ -31,6 +31,8 @@ def main():
     mode = os.environ.get("SWEEP_MODE", "policies")
     if mode == "misaligned":
         return misaligned(n, rounds, reps)
+    if mode.startswith("dtype"):  # dtype<code>: geometry sweep of one element type's sum kernel
+        return dtype_geometry(int(mode[5:]), n * 4, rounds, reps)
     if mode == "policies":
         # load/store policy: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1 nt; order 1 = XCD-contiguous hunks
         for block, unroll, ld, st, order in itertools.product(
@@ -121,6 +123,55 @@ def misaligned(n, rounds, reps):
         print(json.dumps({"cfg": name, "offsets": [so, do],
                           "median_gbs": round(float(np.median(nbytes / (t / 1e3) / 1e9)), 1),
                           "median_us": round(float(np.median(t)) * 1e3, 2)}))
+
+
+def dtype_geometry(dt, nbytes, rounds, reps):
+    """Config 2's byte shape (2 x nbytes -> nbytes) for element type `dt`:
+    block size x unroll x hunks per workgroup, default policies (nt loads,
+    sc0 sc1 stores), interleaved with the library default."""
+    esz = {0: 1, 1: 1, 6: 2, 9: 2, 10: 1, 11: 1, 4: 8, 5: 8, 8: 8}.get(dt, 4)
+    n = nbytes // esz
+    a = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
+    b = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
+    if dt in (10, 11):  # finite fp8 codes
+        a &= 0x77
+        b &= 0x77
+    d = torch.empty_like(a)
+    s = torch.cuda.current_stream()
+    variants = [None]
+    for block, unroll, per in itertools.product((256, 512, 1024), (1, 2, 4, 8), (1, 2)):
+        hunk = block * unroll * 16
+        grid = max(1, (nbytes + hunk - 1) // hunk // per)
+        variants.append({"blockSize": block, "unroll": unroll, "gridBlocks": grid,
+                         "ntLoads": 1, "ntStores": 2, "order": 0})
+    times = {i: [] for i in range(len(variants))}
+    ref = None
+    for r in range(rounds):
+        order = list(range(len(variants)))
+        np.random.default_rng(r).shuffle(order)
+        for i in order:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(reps)]
+            for e0, e1 in ev:
+                e0.record(s)
+                nccl.reduce_copy(0, dt, 0, [a.data_ptr(), b.data_ptr()], [d.data_ptr()], n, s.cuda_stream,
+                                 config=variants[i])
+                e1.record(s)
+            torch.cuda.synchronize()
+            times[i] += [e0.elapsed_time(e1) for e0, e1 in ev]
+            if ref is None:
+                ref = d.clone()
+            elif r == 0:
+                assert torch.equal(d, ref), variants[i]
+    rows = []
+    for i, cfg in enumerate(variants):
+        t = np.array(times[i][reps:])
+        gbs = 3 * nbytes / (t / 1e3) / 1e9
+        rows.append({"dtype": dt, "cfg": cfg or "default", "median_gbs": round(float(np.median(gbs)), 1),
+                     "median_us": round(float(np.median(t)) * 1e3, 2)})
+    rows.sort(key=lambda x: -x["median_gbs"])
+    for row in rows:
+        print(json.dumps(row))
 
 
 if __name__ == "__main__":

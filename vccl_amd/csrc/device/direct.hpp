@@ -12,12 +12,16 @@
 //   on every rank (so a workgroup only ever waits for its namesakes).
 //   phase 1 (scatter): rank r writes block b of every foreign shard p into
 //            p's inbox region (0, r), then raises flag (0, r, b) at p;
-//   phase 2 (reduce):  rank o waits for the n-1 flags (0, *, b), folds its
-//            block in the reference ring order on the identity ring —
-//            x_{o+1} (+) x_{o+2} (+) ... (+) x_o, preOp on every input,
-//            postOp once (all_reduce.h:42-64 with chunk o finishing at ring
-//            index o) — and writes the result to its own output and to every
-//            peer's inbox region (1, o), then raises flag (1, o, b) there;
+//   phase 2 (reduce):  rank o waits for the n-1 flags (0, *, b) and folds
+//            its block exactly as VCCL's ring all-reduce folds those elements:
+//            every element belongs to a ring chunk c of one loop of its
+//            channel's ncclCollCbdPart (ar_chunk_of, the ring's own partition
+//            on the comm's channels and ring set), which the ring folds from
+//            position c+1 around to c, x_{R[c+1]} (+) ... (+) x_{R[c]}, preOp
+//            on every input, postOp once (all_reduce.h:42-64); each wave of
+//            the workgroup walks its span of the block chunk by chunk in that
+//            order — then writes the result to its own output and to every
+//            peer's inbox region (1, o), and raises flag (1, o, b) there;
 //   phase 3 (gather):  every rank waits for the n-1 flags (1, *, b) and copies
 //            the owners' blocks from its inbox into its output.
 // Buckets larger than the inbox move through it in chunks (the three phases
@@ -75,13 +79,18 @@ struct DirectWork {
   int64_t chunkElts;     // elements per chunk (last one shorter)
   int64_t blkElts;       // elements per block, the same for every chunk
   int64_t regionBytes;   // bytes per (phase, rank) inbox region
-  // Reduce-scatter: VCCL's cbd channel partition of the recvcount block
-  // (host/enqueue.cc cbd_schedule, the ring's own): channel c of
-  // [channelLo, channelHi] folds on ring c mod nRings (DevComm::rsOrder), so
+  // VCCL's cbd channel partition (host/enqueue.cc cbd_schedule, the ring's
+  // own) of the recvcount block (reduce-scatter) or of the whole bucket
+  // (all-reduce, with the ring chunk arChunk): channel c of [channelLo,
+  // channelHi] folds on ring c mod nRings (DevComm::rsOrder / ringAt), so
   // the direct path reproduces the ring's (= VCCL's) fold order exactly.
   CbdLite cbd;
+  int64_t arChunk;
 };
 
+// (Bit-exact with the ring all-reduce on the same channels: an all-reduce's
+// result does not depend on whether the ring or the direct path ran it.)
+//
 // Shard length of a chunk of `cc` elements: ceil(cc / n) in 16-byte units.
 // The block length stays that of the first (largest) chunk, so block b sits
 // at the same inbox offset in every chunk (a shorter last chunk only leaves
@@ -237,6 +246,42 @@ __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)
   }
 }
 
+// Copy nBytes from a 16-byte-aligned source to nD 16-byte-aligned
+// destinations (write-through): the direct all-reduce's broadcast of a
+// folded chunk (both ends are the output / inbox, aligned by construction),
+// kept apart from the engine so no misaligned variant is instantiated.  The
+// source was just stored by the same wave (plain stores, drained): plain
+// loads read it back through the CU's own cache path.
+template <int U>
+__device__ __forceinline__ void direct_bcast(const char* src, char* const (&dst)[kDirectMaxRanks], int nD,
+                                             int64_t nBytes, int tid, int nthreads) {
+  const int64_t nPacks = nBytes / 16;
+  for (int64_t base = 0; base < nPacks; base += (int64_t)nthreads * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t p = base + u * nthreads + tid;
+      if (p < nPacks) v[u] = ld16<kPlain>(src, p * 16);
+    }
+#pragma unroll
+    for (int d = 0; d < kDirectMaxRanks; d++) {
+      if (d < nD) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int64_t p = base + u * nthreads + tid;
+          if (p < nPacks) st16<kSys>(dst[d], p * 16, v[u]);
+        }
+      }
+    }
+  }
+  for (int64_t i = nPacks * 16 + tid; i < nBytes; i += nthreads) {
+    const uint8_t x = ldT<kPlain, uint8_t>(src, i);
+#pragma unroll
+    for (int d = 0; d < kDirectMaxRanks; d++)
+      if (d < nD) stT<kSys, uint8_t>(dst[d], i, x);
+  }
+}
+
 // Wait until every peer's flag (phase, peer, b) in MY flag array equals e.
 // Lane p of wave 0 polls peer p; bounded like RingCtx::spin_ge.
 __device__ __forceinline__ bool direct_wait(const DirectWork& w, const char* myFlags, int phase,
@@ -295,7 +340,6 @@ __device__ void direct_allreduce(const DirectWork& w) {
   const int n = w.nRanks, me = w.rank, b = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
-  (void)eltAlign;
   char* myBuf = P.buf[me];
   const char* myFlags = P.flags[me];
   if (tid == 0) shFail = 0;
@@ -341,30 +385,64 @@ __device__ void direct_allreduce(const DirectWork& w) {
     }
     direct_post(w, P, 0, b, e);
 
-    // Phase 2: fold my shard's block b, x_{me+1} (+) ... (+) x_{me}; send it out.
+    // Phase 2: fold my shard's block b in the ring's order; send it out.
     if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
       int64_t off, len;
       block_of(me, &off, &len);
-      // Operand j < n-1: peer (me + j + 1) mod n; operand n-1: my own input /
-      // output (staged in my own aligned region (1, me) when the output is
-      // off 16-byte alignment, copied out in phase 3 with the other blocks).
-      // Filled with compile-time indices only (no scratch array).
-      const char* s[kDirectMaxRanks];
-      char* d[kDirectMaxRanks];
+      // Each wave takes a contiguous span of the block (whole 16-byte packs)
+      // and walks it ring chunk by ring chunk: a chunk boundary splits one
+      // wave's pass, not the workgroup's.
+      constexpr int64_t esz = (int64_t)sizeof(T);
+      // wave index made provably wave-uniform: everything derived from it
+      // (span, chunk lookup, operand pointers) stays in SGPRs
+      const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
+      const int64_t span = ((len + eltAlign - 1) / eltAlign + nw - 1) / nw * eltAlign;
+      int64_t cur = (int64_t)wv * span < len ? (int64_t)wv * span : len;
+      const int64_t wend = cur + span < len ? cur + span : len;
+      while (cur < wend) {
+        int k;
+        int64_t segEnd;
+        const int ch = ar_chunk_of(w.cbd, w.arChunk, n, eltAlign, c0 + off + cur, &k, &segEnd);
+        segEnd -= c0 + off;
+        const int64_t end = segEnd < wend ? segEnd : wend;
+        const int8_t* R = w.comm->ringAt[ch % w.comm->nRings];
+        // (a) fold: sources in ring order, positions k+1, ..., k (my own
+        // input where the position is mine, else my inbox region of that
+        // rank) -> my output (staged in my own aligned region (1, me) when
+        // the output is off 16-byte alignment, copied out in phase 3).
+        char* res = outMis ? myBuf + direct_region_off(1, me, n, w.regionBytes) + inOff + cur * esz
+                           : out + (off + cur) * esz;
+        {
+          const char* s[kDirectMaxRanks];
+          char* d[kDirectMaxRanks] = {res};
 #pragma unroll
-      for (int j = 0; j < kDirectMaxRanks; j++) {
-        const int src = me + j + 1 < n ? me + j + 1 : me + j + 1 - n;
-        if (j < n - 1) {
-          s[j] = myBuf + direct_region_off(0, src, n, w.regionBytes) + inOff;
-          d[j] = P.buf[src] + direct_region_off(1, me, n, w.regionBytes) + inOff;
-        } else {
-          s[j] = in + off * (int64_t)sizeof(T);
-          d[j] = outMis ? myBuf + direct_region_off(1, me, n, w.regionBytes) + inOff
-                        : out + off * (int64_t)sizeof(T);
+          for (int j = 0; j < kDirectMaxRanks; j++) {
+            int pos = k + 1 + j;
+            pos = pos >= n ? pos - n : pos;
+            pos = pos >= n ? pos - n : pos;
+            const int q = j < n ? __builtin_amdgcn_readfirstlane(R[pos]) : me;
+            s[j] = q == me ? in + (off + cur) * esz
+                           : myBuf + direct_region_off(0, q, n, w.regionBytes) + inOff + cur * esz;
+          }
+          direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, 1,
+                                                             end - cur, lane, 64);
         }
+        // (b) broadcast: this wave reads back what it just stored (same
+        // wave, drained) and writes it into every peer's region (1, me).
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        {
+          const char* s[kDirectMaxRanks] = {res};
+          char* d[kDirectMaxRanks];
+#pragma unroll
+          for (int j = 0; j < kDirectMaxRanks; j++) {
+            const int dst = me + j + 1 < n ? me + j + 1 : me + j + 1 - n;
+            d[j] = j < n - 1 ? P.buf[dst] + direct_region_off(1, me, n, w.regionBytes) + inOff + cur * esz
+                             : nullptr;
+          }
+          direct_bcast<kDirectUnroll>(s[0], d, n - 1, (end - cur) * esz, lane, 64);
+        }
+        cur = end;
       }
-      direct_rc<Fn, kDirectUnroll, kSys, kSys, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, n, len,
-                                                       tid, nt);
     }
     direct_post(w, P, 1, b, e);
 

@@ -1,21 +1,27 @@
-// Collective kernels for ONE kernel element type (VCCL_KT): per reduction
-// functor the ring all-reduce / reduce-scatter (one workgroup per channel,
-// enqueue.cc:1576-1666), the one-shot LL and the direct (two-shot all-reduce,
-// one-hop reduce-scatter) kernels; in the K_U8 unit also the type-agnostic
-// all-gathers (ring, LL, direct).
+// Collective kernels for ONE kernel element type (VCCL_KT) and ONE family
+// (VCCL_PART: 0 ring, 1 LL, 2 direct — separate objects, built in parallel):
+// per reduction functor the ring all-reduce / reduce-scatter (one workgroup
+// per channel, enqueue.cc:1576-1666), the one-shot LL and the direct
+// (two-shot all-reduce, one-hop reduce-scatter) kernels; in the K_U8 unit
+// also the type-agnostic all-gathers (ring, LL, direct).
 #include <hip/hip_runtime.h>
 
-#include "direct.hpp"
 #include "dispatch.hpp"
-#include "ll.hpp"
-#include "ring.hpp"
 #include "ring_launch.hpp"
+#if VCCL_PART == 0
+#include "ring.hpp"
+#endif
 
 #ifndef VCCL_KT
 #error "compile with -DVCCL_KT=<kernel element type>"
 #endif
+#ifndef VCCL_PART
+#error "compile with -DVCCL_PART=<0 ring | 1 LL | 2 direct>"
+#endif
 
 namespace vccl {
+
+#if VCCL_PART == 0
 
 // 512 threads per channel: the ring primitive (pipelined aligned copy +
 // realigning misaligned path, inlined per (recv, send, src, dst) shape) needs
@@ -48,6 +54,35 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingWork w) {
   }
 }
 
+template <>
+hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingWork& w, int nthreads,
+                                hipStream_t stream) {
+  using T = typename KTypeOf<VCCL_KT>::T;
+  hipError_t err = hipErrorInvalidValue;
+  dim3 grid(w.nChannels), block(nthreads);
+  if (coll == kCollAllGather) {
+    if constexpr (VCCL_KT == K_U8) {
+      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, kRingUnroll>), grid, block, 0,
+                         stream, w);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  dispatch_op<T>(devOp, [&]<class Fn>() {
+    if constexpr (std::is_same<Fn, FnCopy<T>>::value) {
+      err = hipErrorInvalidValue;
+    } else if (coll == kCollAllReduce) {
+      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, kRingUnroll>), grid, block, 0, stream, w);
+      err = hipGetLastError();
+    } else if (coll == kCollReduceScatter) {
+      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, kRingUnroll>), grid, block, 0, stream, w);
+      err = hipGetLastError();
+    }
+  });
+  return err;
+}
+
+#elif VCCL_PART == 1
 template <class Fn>
 __global__ __launch_bounds__(256) void k_ll_allreduce(LLWork w) {
   ll_allreduce<Fn>(w);
@@ -82,6 +117,7 @@ hipError_t ll_launch<VCCL_KT>(int coll, int devOp, const LLWork& w, int grid, hi
   return err;
 }
 
+#elif VCCL_PART == 2
 template <class Fn>
 __global__ __launch_bounds__(kDirectThreads) void k_direct_allreduce(DirectWork w) {
   direct_allreduce<Fn>(w);
@@ -119,32 +155,6 @@ hipError_t direct_launch<VCCL_KT>(int coll, int devOp, const DirectWork& w, hipS
   return err;
 }
 
-template <>
-hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingWork& w, int nthreads,
-                                hipStream_t stream) {
-  using T = typename KTypeOf<VCCL_KT>::T;
-  hipError_t err = hipErrorInvalidValue;
-  dim3 grid(w.nChannels), block(nthreads);
-  if (coll == kCollAllGather) {
-    if constexpr (VCCL_KT == K_U8) {
-      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, kRingUnroll>), grid, block, 0,
-                         stream, w);
-      return hipGetLastError();
-    }
-    return hipErrorInvalidValue;
-  }
-  dispatch_op<T>(devOp, [&]<class Fn>() {
-    if constexpr (std::is_same<Fn, FnCopy<T>>::value) {
-      err = hipErrorInvalidValue;
-    } else if (coll == kCollAllReduce) {
-      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, kRingUnroll>), grid, block, 0, stream, w);
-      err = hipGetLastError();
-    } else if (coll == kCollReduceScatter) {
-      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, kRingUnroll>), grid, block, 0, stream, w);
-      err = hipGetLastError();
-    }
-  });
-  return err;
-}
+#endif
 
 }  // namespace vccl

@@ -75,6 +75,11 @@ struct DevComm {
   // reduce-scatters (n <= kOrderMaxRanks) fold in the same order.
   int nRings;
   int8_t rsOrder[kOrderMaxRings][kOrderMaxRanks];
+  // ringAt[k][p] = the rank at position p of ring k (the ring's own order,
+  // ring->index space): VCCL's ring all-reduce folds chunk c of a loop from
+  // position c+1 around to c (all_reduce.h:42-64), whichever rank computes
+  // it — the direct all-reduce folds in that order too.
+  int8_t ringAt[kOrderMaxRings][kOrderMaxRanks];
 };
 
 // The part of VCCL's cbd partition a reduce-scatter needs to know which
@@ -104,6 +109,29 @@ __host__ __device__ inline int cbd_channel_of(const CbdLite& p, int64_t i, int64
   }
   *end = p.count;
   return p.channelHi;
+}
+
+// The ring all-reduce's chunk of element i (all_reduce.h:32-47 inside the
+// ncclCollCbdPart of its channel): channel, chunk index c within its loop
+// (the chunk that finishes at ring position c) and the end of that chunk.
+// `chunk` is the SIMPLE chunk of every part (cbd_schedule: one value),
+// eltAlign = 16 / sizeof(T); the last loop's chunk is
+// alignUp(divUp(rem, n), eltAlign), exactly as ring_allreduce steps it.
+__host__ __device__ inline int ar_chunk_of(const CbdLite& p, int64_t chunk, int n, int64_t eltAlign,
+                                           int64_t i, int* c, int64_t* end) {
+  int64_t partEnd;
+  const int ch = cbd_channel_of(p, i, &partEnd);
+  const int64_t nMid = p.channelHi - p.channelLo - 1;
+  const int64_t partStart = ch == p.channelLo ? 0
+                            : ch == p.channelHi ? p.countLo + nMid * p.countMid
+                                                : p.countLo + (int64_t)(ch - p.channelLo - 1) * p.countMid;
+  const int64_t rel = i - partStart, loopCount = (int64_t)n * chunk;
+  const int64_t eo = rel / loopCount * loopCount, rem = partEnd - partStart - eo;
+  const int64_t ck = rem < loopCount ? ((rem + n - 1) / n + eltAlign - 1) / eltAlign * eltAlign : chunk;
+  *c = (int)((rel - eo) / ck);
+  const int64_t e = partStart + eo + (int64_t)(*c + 1) * ck;
+  *end = e < partEnd ? e : partEnd;
+  return ch;
 }
 
 // Per-launch work descriptor (kernel argument, by value).

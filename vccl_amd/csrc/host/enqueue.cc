@@ -518,6 +518,11 @@ static ncclResult_t launch_direct(const Task& t) {
     const int64_t chunkMax = regionElts * n / (n * eltAlign) * (n * eltAlign);
     w.chunkElts = std::min<int64_t>(count, chunkMax);
     shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
+    // the ring's partition of this bucket: phase 2 folds every element in the
+    // order VCCL's ring all-reduce gives it on these channels (ar_chunk_of)
+    const CbdPlan p = cbd_schedule(kAllReduce, count, esz, n, comm->nChannels, comm->slotBytes);
+    w.cbd = CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, count};
+    w.arChunk = p.chunkLo;
   } else {
     // Reduce-scatter / all-gather: a chunk is a range of ONE rank's block
     // (count elements) that fits a region; it is cut into blocks directly.
@@ -932,6 +937,23 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition
   const int64_t v[8] = {p.channelLo, p.channelHi, p.countLo, p.countMid,
                         p.countHi,   p.chunkLo,   p.chunkMid, p.chunkHi};
   memcpy(out, v, sizeof(v));
+  return ncclSuccess;
+}
+
+extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingChunkOf(
+    size_t count, ncclDataType_t datatype, int nRanks, int nChannels, size_t slotBytes, size_t i,
+    int64_t* out) {
+  if (!out || type_size(datatype) < 1 || nRanks < 1 || nChannels < 1 || nChannels > kMaxChannels ||
+      count == 0 || i >= count || slotBytes < 4096)
+    return ncclInvalidArgument;
+  const int64_t esz = type_size(datatype);
+  const CbdPlan p = cbd_schedule(kAllReduce, (int64_t)count, esz, nRanks, nChannels, (int64_t)slotBytes);
+  const CbdLite cbd{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)count};
+  int k;
+  int64_t end;
+  out[0] = ar_chunk_of(cbd, p.chunkLo, nRanks, std::max<int64_t>(1, 16 / esz), (int64_t)i, &k, &end);
+  out[1] = k;
+  out[2] = end;
   return ncclSuccess;
 }
 

@@ -360,6 +360,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     const auto& ring = rings[k];
     const int pos = (int)(std::find(ring.begin(), ring.end(), c->rank) - ring.begin());
     for (int j = 0; j < n; j++) dc.rsOrder[k][j] = (int8_t)ring[(pos + 1 + j) % n];
+    for (int j = 0; j < n; j++) dc.ringAt[k][j] = (int8_t)ring[j];
   }
   HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));

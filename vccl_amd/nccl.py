@@ -40,7 +40,7 @@ EXPORTED = [
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
-    "vcclRingPartition",
+    "vcclRingPartition", "vcclRingChunkOf",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
 ]
@@ -107,6 +107,7 @@ def lib() -> ctypes.CDLL:
         "vcclRingPartition": [c_int, c_size, c_int, c_int, c_int, c_size,
                               ctypes.POINTER(ctypes.c_int64)],
         "vcclCommDebugSetEpochs": [vp, ctypes.c_uint32, ctypes.c_uint32],
+        "vcclRingChunkOf": [c_size, c_int, c_int, c_int, c_size, c_size, ctypes.POINTER(ctypes.c_int64)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -176,6 +177,15 @@ def ring_partition(coll: int, count: int, dtype: int, nranks: int, nchannels: in
     out = (ctypes.c_int64 * 8)()
     check(lib().vcclRingPartition(coll, count, dtype, nranks, nchannels, slot_bytes, out),
           "vcclRingPartition")
+    return tuple(out)
+
+
+def ring_chunk_of(count: int, dtype: int, nranks: int, nchannels: int, slot_bytes: int,
+                  i: int) -> tuple[int, int, int]:
+    """vcclRingChunkOf: (channel, ring chunk c, chunk end) of all-reduce
+    element i on the ring's partition (the direct all-reduce's fold lookup)."""
+    out = (ctypes.c_int64 * 3)()
+    check(lib().vcclRingChunkOf(count, dtype, nranks, nchannels, slot_bytes, i, out), "vcclRingChunkOf")
     return tuple(out)
 
 
