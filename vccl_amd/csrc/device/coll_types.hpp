@@ -1,0 +1,106 @@
+// Work descriptors and buffer layouts of the one-hop LL (ll.hpp) and direct
+// (direct.hpp) collectives, shared by the host planner and the kernels.  Kept
+// apart from the kernel code so host objects and the other kernel families do
+// not recompile when a kernel body changes.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ring_types.hpp"
+
+namespace vccl {
+
+// ------------------------------------------------------------------- LL
+constexpr int kLLMaxParts = 16;
+
+struct LLPart {
+  const char* send;
+  char* recv;
+  int64_t nbytes;          // count * sizeof(T)
+  int64_t line0;           // first line of this part in the slot
+};
+
+struct LLWork {
+  DevComm* comm;
+  uint64_t redArg;
+  const void* redArgPtr;
+  int redArgBytes;
+  int preOp;
+  int nRanks, rank;
+  int linesPerSlot;        // capacity of one (parity, source) slot
+  int nParts;              // 1 .. kLLMaxParts all-reduces in this launch
+  int64_t nLines;          // lines of all parts (<= linesPerSlot)
+  char* localBuf;          // my LL buffer: [2 parities][nRanks sources][linesPerSlot] lines
+  char* peerBuf[kMaxRanks];  // every rank's LL buffer mapped here (peerBuf[rank] = local)
+  LLPart parts[kLLMaxParts];
+  // Reduce-scatter / all-gather (one part): parts[0] = {input, output, bytes
+  // of ONE rank's block, 0}; nLines = lines of one block.  Reduce-scatter
+  // folds each line on the ring of its channel (VCCL's cbd partition of the
+  // block, DevComm::rsOrder).
+  CbdLite cbd;
+};
+
+// Byte offset of the (parity, source rank) slot inside an LL buffer.
+__host__ __device__ __forceinline__ size_t ll_slot_off(int parity, int src, int nRanks,
+                                                       int linesPerSlot) {
+  return ((size_t)parity * nRanks + src) * (size_t)linesPerSlot * 16;
+}
+
+// --------------------------------------------------------------- direct
+constexpr int kDirectMaxRanks = 8;     // phase 2 folds all n inputs in registers
+constexpr int kDirectMaxBlocks = 128;
+constexpr int kDirectFlagStride = 64;  // bytes between flags
+constexpr int kDirectThreads = 512;
+constexpr int kDirectUnroll = 2;
+
+// Every rank's inbox and flag array, mapped into this process (device memory,
+// so runtime peer indices never index a by-value kernel argument).
+struct DirectPeers {
+  char* buf[kDirectMaxRanks];
+  char* flags[kDirectMaxRanks];
+};
+
+struct DirectWork {
+  DevComm* comm;
+  const DirectPeers* peers;
+  const void* sendbuff;
+  void* recvbuff;
+  uint64_t count;        // elements
+  uint64_t redArg;
+  const void* redArgPtr;
+  int redArgBytes;
+  int preOp;
+  int nRanks, rank;
+  int nBlocks;           // workgroups (block b of every shard -> workgroup b)
+  int nChunks;           // the bucket moves through the inbox in chunks
+  int64_t chunkElts;     // elements per chunk (last one shorter)
+  int64_t blkElts;       // elements per block, the same for every chunk
+  int64_t regionBytes;   // bytes per (phase, rank) inbox region
+  // VCCL's cbd channel partition (host/enqueue.cc cbd_schedule, the ring's
+  // own) of the recvcount block (reduce-scatter) or of the whole bucket
+  // (all-reduce, with the ring chunk arChunk): channel c of [channelLo,
+  // channelHi] folds on ring c mod nRings (DevComm::rsOrder / ringAt), so
+  // the direct path reproduces the ring's (= VCCL's) fold order exactly.
+  CbdLite cbd;
+  int64_t arChunk;
+};
+
+// Shard length of a chunk of `cc` elements: ceil(cc / n) in 16-byte units.
+// The block length stays that of the first (largest) chunk, so block b sits
+// at the same inbox offset in every chunk (a shorter last chunk only leaves
+// high blocks empty) — the buffer-reuse argument (direct.hpp header) needs
+// fixed offsets.
+__host__ __device__ __forceinline__ int64_t direct_shard_elts(int64_t cc, int n, int64_t eltAlign) {
+  return ((cc + n - 1) / n + eltAlign - 1) / eltAlign * eltAlign;
+}
+
+__host__ __device__ __forceinline__ size_t direct_region_off(int phase, int src, int nRanks,
+                                                             int64_t regionBytes) {
+  return ((size_t)phase * nRanks + src) * (size_t)regionBytes;
+}
+__host__ __device__ __forceinline__ size_t direct_flag_off(int phase, int src, int b) {
+  return (((size_t)phase * kDirectMaxRanks + src) * kDirectMaxBlocks + b) * kDirectFlagStride;
+}
+constexpr size_t kDirectFlagBytes = (size_t)2 * kDirectMaxRanks * kDirectMaxBlocks * kDirectFlagStride;
+
+}  // namespace vccl

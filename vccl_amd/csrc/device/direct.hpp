@@ -44,69 +44,12 @@
 // (0, *) regions, which the previous call has finished reading before that
 // peer could complete it).
 #pragma once
+#include "coll_types.hpp"
 #include "ll.hpp"
 #include "reduce_copy.hpp"
 #include "ring_types.hpp"
 
 namespace vccl {
-
-constexpr int kDirectMaxRanks = 8;     // phase 2 folds all n inputs in registers
-constexpr int kDirectMaxBlocks = 128;
-constexpr int kDirectFlagStride = 64;  // bytes between flags
-constexpr int kDirectThreads = 512;
-constexpr int kDirectUnroll = 2;
-
-// Every rank's inbox and flag array, mapped into this process (device memory,
-// so runtime peer indices never index a by-value kernel argument).
-struct DirectPeers {
-  char* buf[kDirectMaxRanks];
-  char* flags[kDirectMaxRanks];
-};
-
-struct DirectWork {
-  DevComm* comm;
-  const DirectPeers* peers;
-  const void* sendbuff;
-  void* recvbuff;
-  uint64_t count;        // elements
-  uint64_t redArg;
-  const void* redArgPtr;
-  int redArgBytes;
-  int preOp;
-  int nRanks, rank;
-  int nBlocks;           // workgroups (block b of every shard -> workgroup b)
-  int nChunks;           // the bucket moves through the inbox in chunks
-  int64_t chunkElts;     // elements per chunk (last one shorter)
-  int64_t blkElts;       // elements per block, the same for every chunk
-  int64_t regionBytes;   // bytes per (phase, rank) inbox region
-  // VCCL's cbd channel partition (host/enqueue.cc cbd_schedule, the ring's
-  // own) of the recvcount block (reduce-scatter) or of the whole bucket
-  // (all-reduce, with the ring chunk arChunk): channel c of [channelLo,
-  // channelHi] folds on ring c mod nRings (DevComm::rsOrder / ringAt), so
-  // the direct path reproduces the ring's (= VCCL's) fold order exactly.
-  CbdLite cbd;
-  int64_t arChunk;
-};
-
-// (Bit-exact with the ring all-reduce on the same channels: an all-reduce's
-// result does not depend on whether the ring or the direct path ran it.)
-//
-// Shard length of a chunk of `cc` elements: ceil(cc / n) in 16-byte units.
-// The block length stays that of the first (largest) chunk, so block b sits
-// at the same inbox offset in every chunk (a shorter last chunk only leaves
-// high blocks empty) — the reuse argument above needs fixed offsets.
-__host__ __device__ __forceinline__ int64_t direct_shard_elts(int64_t cc, int n, int64_t eltAlign) {
-  return ((cc + n - 1) / n + eltAlign - 1) / eltAlign * eltAlign;
-}
-
-__host__ __device__ __forceinline__ size_t direct_region_off(int phase, int src, int nRanks,
-                                                             int64_t regionBytes) {
-  return ((size_t)phase * nRanks + src) * (size_t)regionBytes;
-}
-__host__ __device__ __forceinline__ size_t direct_flag_off(int phase, int src, int b) {
-  return (((size_t)phase * kDirectMaxRanks + src) * kDirectMaxBlocks + b) * kDirectFlagStride;
-}
-constexpr size_t kDirectFlagBytes = (size_t)2 * kDirectMaxRanks * kDirectMaxBlocks * kDirectFlagStride;
 
 // Fold up to kDirectMaxRanks sources into up to kDirectMaxRanks destinations:
 // dst_d[i] = postOp(pre?(src_0[i]) (+) pre?(src_1[i]) (+) ...), preOp on

@@ -24,47 +24,13 @@
 // i occupies lines [line0_i, line0_i + ceil(bytes_i / 8)) of the slot, so the
 // whole batch costs one hop and one epoch.
 #pragma once
+#include "coll_types.hpp"
 #include "reduce_copy.hpp"
 #include "ring_types.hpp"
 
 namespace vccl {
 
-constexpr int kLLMaxParts = 16;
-
-struct LLPart {
-  const char* send;
-  char* recv;
-  int64_t nbytes;          // count * sizeof(T)
-  int64_t line0;           // first line of this part in the slot
-};
-
-struct LLWork {
-  DevComm* comm;
-  uint64_t redArg;
-  const void* redArgPtr;
-  int redArgBytes;
-  int preOp;
-  int nRanks, rank;
-  int linesPerSlot;        // capacity of one (parity, source) slot
-  int nParts;              // 1 .. kLLMaxParts all-reduces in this launch
-  int64_t nLines;          // lines of all parts (<= linesPerSlot)
-  char* localBuf;          // my LL buffer: [2 parities][nRanks sources][linesPerSlot] lines
-  char* peerBuf[kMaxRanks];  // every rank's LL buffer mapped here (peerBuf[rank] = local)
-  LLPart parts[kLLMaxParts];
-  // Reduce-scatter / all-gather (one part): parts[0] = {input, output, bytes
-  // of ONE rank's block, 0}; nLines = lines of one block.  Reduce-scatter
-  // folds each line on the ring of its channel (VCCL's cbd partition of the
-  // block, DevComm::rsOrder).
-  CbdLite cbd;
-};
-
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-// Byte offset of the (parity, source rank) slot inside an LL buffer.
-__host__ __device__ __forceinline__ size_t ll_slot_off(int parity, int src, int nRanks,
-                                                       int linesPerSlot) {
-  return ((size_t)parity * nRanks + src) * (size_t)linesPerSlot * 16;
-}
 
 // 8 data bytes of element stream `p` (bytes [8*line, 8*line+8)), zero padded.
 __device__ __forceinline__ uint64_t ll_load8(const char* p, int64_t line, int64_t nbytes) {

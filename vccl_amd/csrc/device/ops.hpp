@@ -508,13 +508,16 @@ __device__ __forceinline__ uint32_t e5m2x4_add_cvt(uint32_t a, uint32_t b) {
   r -= inf >> 7;  // 0x7c -> 0x7b in those bytes (no borrow: the byte is >= 0x7c)
   return (r & ~(n | n7f)) | n7f;
 }
-// Off by default: measured level with the per-element lowering for E5M2
-// (6.62-6.75 TB/s either way, interleaved, profiles/r01z/ab_fp8.log; bit-exact
-// in that run's tests under VCCL_LIB), and slower in round 2 (0.873 vs 0.889
-// of peak, profiles/r02/dtypes_*.log) although it cuts SQ_INSTS_VALU per
-// launch from 64.9 M to 26.3 M (profiles/r02/pmc_valu_e5m2_ab.csv): the
-// 1-byte kernels are not VALU-bound.  -DVCCL_F8_E5M2_CVT selects it.
-#ifdef VCCL_F8_E5M2_CVT
+// The default E5M2 sum (-DVCCL_F8_E5M2_ELEMENTWISE restores the per-element
+// widen-by-shift / _Float16 / integer-narrowing form).  Every 1-byte kernel is
+// power-bound, not VALU-bound, at config 2: on zero inputs E4M3, E5M2 and u8
+// all run at 7.85-7.92 TB/s (0.98-0.99 of peak), on random bytes at 7.0-7.2
+// (tools/rc_data.py, profiles/r02q).  This form issues 2.5x fewer VALU
+// instructions per launch (25.8 M vs 65.4 M, E4M3 26.9 M; SQ_ACTIVE_INST_VALU
+// 28.0 M vs 65.5 M quad-cycles, profiles/r02p/pmc_dtypes.log), so it draws
+// less power: +5 % on a box where the per-element form ran at 0.80 of peak
+// (profiles/r02p/ab_fp8.log, interleaved), -2 % on one where it ran at 0.89.
+#ifndef VCCL_F8_E5M2_ELEMENTWISE
 __device__ __forceinline__ u32x4 pack_reduce(const FnSum<f8e5m2_t>&, u32x4 a, u32x4 b) {
   return u32x4{e5m2x4_add_cvt(a.x, b.x), e5m2x4_add_cvt(a.y, b.y), e5m2x4_add_cvt(a.z, b.z),
                e5m2x4_add_cvt(a.w, b.w)};

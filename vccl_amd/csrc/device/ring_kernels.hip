@@ -10,6 +10,10 @@
 #include "ring_launch.hpp"
 #if VCCL_PART == 0
 #include "ring.hpp"
+#elif VCCL_PART == 1
+#include "ll.hpp"
+#else
+#include "direct.hpp"
 #endif
 
 #ifndef VCCL_KT

@@ -3,8 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "direct.hpp"
-#include "ll.hpp"
+#include "coll_types.hpp"
 #include "ring_types.hpp"
 
 namespace vccl {

@@ -15,7 +15,7 @@
 #include <thread>
 
 #include "../../../include/vccl_ext.h"
-#include "../device/direct.hpp"
+#include "../device/coll_types.hpp"
 #include "../device/ring_launch.hpp"
 #include "core.h"
 
