@@ -150,10 +150,11 @@ def bench_reduce_copy(args):
     return out
 
 
-def bench_rc_dtypes(nbytes, steps=20, warmup=3):
+def bench_rc_dtypes(nbytes, steps=20, warmup=3, preroll_s=0.1):
     """Config 2's shape (2 sources -> 1 destination, `nbytes` per buffer) for
     each element type's sum kernel: GB/s (3 x nbytes per launch / event time
-    on the launch stream) and the HBM-roofline fraction.  Not `value`."""
+    on the launch stream) and the HBM-roofline fraction, after an untimed
+    `preroll_s` of launches of that kernel.  Not `value`."""
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     L = nccl.lib()
@@ -178,6 +179,15 @@ def bench_rc_dtypes(nbytes, steps=20, warmup=3):
             if rc:
                 raise nccl.VcclError(rc, "vcclReduceCopy")
 
+        # Untimed pre-roll per kernel: a kernel's first use in a process can
+        # ramp for ~150 launches (E5M2: 2.0 -> 6.9 TB/s over 8 batches of 20,
+        # then 7.1 TB/s whenever used again; tools/dtype_rows.py first_use,
+        # profiles/r02u), so the row reads the steady state.
+        t_pre = time.perf_counter()
+        while time.perf_counter() - t_pre < preroll_s:
+            for _ in range(8):
+                step()
+            torch.cuda.synchronize()
         for _ in range(warmup):
             step()
         e0, e1 = _evt(), _evt()

@@ -11,6 +11,8 @@
 #        sweep:<mode>  tools/sweep_rc.py with SWEEP_MODE=<mode> (6 rounds)
 #        pmc       tools/pmc_traffic.py (separate FETCH_SIZE / WRITE_SIZE passes)
 #        lat:<n>   tools/coll_latency.py on n ranks sharing the GPU (LAT_* env)
+#        mprof:<n> the N>1 bench line on n ranks sharing the GPU, every rank
+#                  under rocprofv3 --kernel-trace --stats (tools/mp_prof.py)
 # Outputs go to gpurun_out/<label>/.  Every GPU step has its own time limit
 # and the chain stops at the first failure (no retries).
 set -e
@@ -32,6 +34,7 @@ for s in "$@"; do
     sweep:*) SWEEP_MODE=${s#sweep:} SWEEP_ROUNDS=${SWEEP_ROUNDS:-6} timeout -k 10 300 python -u tools/sweep_rc.py > $O/sweep_${s#sweep:}.log 2>&1 ;;
     pmc) timeout -k 10 400 python -u tools/pmc_traffic.py > $O/pmc_traffic.log 2>&1 && cp gpurun_out/pmc_traffic.json $O/ ;;
     lat:*) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#lat:} --master-addr 127.0.0.1 --master-port 29534 tools/coll_latency.py > $O/lat_n${s#lat:}.log 2> $O/lat_n${s#lat:}.err ;;
+    mprof:*) timeout -k 10 600 python -u tools/mp_prof.py ${s#mprof:} $O/mprof_n${s#mprof:} --steps 5 --warmup 2 > $O/mprof_n${s#mprof:}.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -49,6 +49,24 @@ def main():
         t = np.array(t)
         print(json.dumps({"dtype": k, "pattern": p, "median_gbs": round(float(np.median(3 * nbytes / (t / 1e3) / 1e9)), 1),
                           "median_us": round(float(np.median(t)) * 1e3, 2)}), flush=True)
+    # Sustained: K launches back to back under ONE event pair (bench.py's
+    # per-dtype leg uses K = 20), after 3 warmup launches, 3 repetitions.
+    for k in dts:
+        a, b = pats["uniform_f32" if k == "f32" else "rand&77"]
+        n = nbytes // (4 if k == "f32" else 1)
+        for K in (8, 20, 60):
+            res = []
+            for _ in range(3):
+                for _ in range(3):
+                    nccl.reduce_copy(0, dts[k], 0, [a.data_ptr(), b.data_ptr()], [d.data_ptr()], n, s.cuda_stream)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(K):
+                    nccl.reduce_copy(0, dts[k], 0, [a.data_ptr(), b.data_ptr()], [d.data_ptr()], n, s.cuda_stream)
+                e1.record(s)
+                torch.cuda.synchronize()
+                res.append(round(3 * nbytes * K / (e0.elapsed_time(e1) / 1e3) / 1e9, 1))
+            print(json.dumps({"dtype": k, "sustained_launches": K, "gbs": res}), flush=True)
 
 
 if __name__ == "__main__":
