@@ -51,6 +51,15 @@
 
 namespace vccl {
 
+// 16-byte packs per thread in flight in the single-source copies (scatter,
+// broadcast, gather); the n-source folds keep kDirectUnroll.  4 was A/B'd in
+// the 4-rank rehearsal (profiles/r02x): reduce-scatter 64 MiB -10 %, all-
+// reduce / all-gather level, small buckets noisier — left at 2.
+#ifndef VCCL_DIRECT_COPY_UNROLL
+#define VCCL_DIRECT_COPY_UNROLL 2
+#endif
+constexpr int kDirectCopyUnroll = VCCL_DIRECT_COPY_UNROLL;
+
 // Fold up to kDirectMaxRanks sources into up to kDirectMaxRanks destinations:
 // dst_d[i] = postOp(pre?(src_0[i]) (+) pre?(src_1[i]) (+) ...), preOp on
 // sources s < preN.  All sources' loads of a hunk are issued before the first
@@ -324,7 +333,7 @@ __device__ void direct_allreduce(const DirectWork& w) {
       block_of(p, &off, &len);
       const char* s[kDirectMaxRanks] = {in + off * (int64_t)sizeof(T)};
       char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + inOff};
-      direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+      direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
     }
     direct_post(w, P, 0, b, e);
 
@@ -382,7 +391,7 @@ __device__ void direct_allreduce(const DirectWork& w) {
             d[j] = j < n - 1 ? P.buf[dst] + direct_region_off(1, me, n, w.regionBytes) + inOff + cur * esz
                              : nullptr;
           }
-          direct_bcast<kDirectUnroll>(s[0], d, n - 1, (end - cur) * esz, lane, 64);
+          direct_bcast<kDirectCopyUnroll>(s[0], d, n - 1, (end - cur) * esz, lane, 64);
         }
         cur = end;
       }
@@ -397,7 +406,7 @@ __device__ void direct_allreduce(const DirectWork& w) {
         block_of(o, &off, &len);
         const char* s[kDirectMaxRanks] = {myBuf + direct_region_off(1, o, n, w.regionBytes) + inOff};
         char* d[kDirectMaxRanks] = {out + off * (int64_t)sizeof(T)};
-        direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+        direct_rc<Fn, kDirectCopyUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
       }
     }
     __syncthreads();  // the region reads of this chunk precede the next chunk's posts
@@ -452,7 +461,7 @@ __device__ void direct_reducescatter(const DirectWork& w) {
       const int p = me + k < n ? me + k : me + k - n;
       const char* s[kDirectMaxRanks] = {in + ((int64_t)p * count + lo) * esz};
       char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + rOff};
-      direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+      direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
     }
     direct_post(w, P, 0, b, e);
     // Phase 2: fold per channel part in its ring's order.
@@ -531,7 +540,7 @@ __device__ __forceinline__ void direct_allgather(const DirectWork& w) {
         const int p = me + 1 + j < n ? me + 1 + j : me + 1 + j - n;
         d[j] = j < n - 1 ? P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + rOff : nullptr;
       }
-      direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, n - 1, len, tid, nt);
+      direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, n - 1, len, tid, nt);
     }
     direct_post(w, P, 0, b, e);
     // Phase 2: gather every rank's block b into the output.
@@ -542,7 +551,7 @@ __device__ __forceinline__ void direct_allgather(const DirectWork& w) {
                                                   : myBuf + direct_region_off(0, o, n, w.regionBytes) + rOff};
         char* d[kDirectMaxRanks] = {out + (int64_t)o * count + lo};
         if (o == me && s[0] == d[0]) continue;  // in place: my block is already there
-        direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+        direct_rc<Fn, kDirectCopyUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
       }
     }
     direct_post(w, P, 1, b, e);

@@ -32,6 +32,9 @@ namespace vccl {
 // ~137 VGPRs, above the 128 a 1024-thread workgroup allows (that spilled in
 // the hot loop).  Channel count, not threads per channel, sets ring
 // bandwidth.
+template <class Fn>
+constexpr int ring_unroll() { return IsF8<typename Fn::EltType>::value ? 2 : kRingUnroll; }
+
 template <int COLL, class Fn, int UNROLL>
 __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingWork w) {
   __shared__ int shAbort;
@@ -76,10 +79,10 @@ hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingWork& w, int nthr
     if constexpr (std::is_same<Fn, FnCopy<T>>::value) {
       err = hipErrorInvalidValue;
     } else if (coll == kCollAllReduce) {
-      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, kRingUnroll>), grid, block, 0, stream, w);
+      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, ring_unroll<Fn>()>), grid, block, 0, stream, w);
       err = hipGetLastError();
     } else if (coll == kCollReduceScatter) {
-      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, kRingUnroll>), grid, block, 0, stream, w);
+      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, ring_unroll<Fn>()>), grid, block, 0, stream, w);
       err = hipGetLastError();
     }
   });

@@ -9,7 +9,15 @@
 namespace vccl {
 
 enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2 };
-constexpr int kRingUnroll = 2;
+// 16-byte packs per thread per operand in flight in a ring step: 4 (2 for
+// the fp8 types, whose per-element prod / min / max / PreMulSum kernels
+// spill at 4).  Twice round 1's 2 keeps twice the write-through stores in
+// flight per channel: the 2-rank rehearsal's all-gather 1 GiB 2614 ->
+// 1714 us, all-reduce -2 %, reduce-scatter -1 % (profiles/r02w).
+#ifndef VCCL_RING_UNROLL
+#define VCCL_RING_UNROLL 4
+#endif
+constexpr int kRingUnroll = VCCL_RING_UNROLL;
 constexpr int kRingMaxThreads = 512;  // k_ring launch bound (ring_kernels.hip)
 
 template <int K>
