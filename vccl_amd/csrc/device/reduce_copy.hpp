@@ -606,14 +606,43 @@ __device__ __forceinline__ void rc_hunks_shifted(const Fn& fn, const RCArgs& a, 
       }
       if (Fn::kPostOp && a.postOp) acc[u] = pack_postop(fn, acc[u]);
     }
+    // Halo: the previous span's last pack (pw - 1), recomputed here — the
+    // same loads and fold, so the same bits — lets lane 0 store the aligned
+    // destination pack that straddles the span boundary in ONE full 16-byte
+    // store; the previous span then stores no tail piece.  Only the body's
+    // first span (pw == 0) and the last pack keep partial pieces.
+    u32x4 halo = acc[0];
+    bool useHalo = false;
+    if constexpr (DSTR) {
+      bool anyKd = false;
+#pragma unroll
+      for (int d = 0; d < ND; d++) anyKd = anyKd || kd[d] != 0;
+      const int64_t pw = p0 - lane;  // first pack of this wave's span
+      if (anyKd && pw > 0) {
+        auto hsrc = [&](int s) __attribute__((always_inline)) -> u32x4 {
+          const u32x4 raw = ld16_body_src<POLS>(a, s, k[s], pw - 1, nPacks);
+          return k[s] ? funnel16(raw, lane0_of(cur[s][0]), k[s]) : raw;
+        };
+        halo = hsrc(0);
+        if (Fn::kPreOp && a.preOpSrcs > 0) halo = pack_preop(fn, halo);
+#pragma unroll
+        for (int s = 1; s < NS; s++) {
+          u32x4 v = hsrc(s);
+          if (Fn::kPreOp && s < a.preOpSrcs) v = pack_preop(fn, v);
+          halo = pack_reduce(fn, halo, v);
+        }
+        if (Fn::kPostOp && a.postOp) halo = pack_postop(fn, halo);
+        useHalo = true;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < UNROLL; u++) {
       const int64_t p = p0 + 64 * u;
 #pragma unroll
       for (int d = 0; d < ND; d++) {
         if constexpr (DSTR)
-          st16_dst_realigned<POLS>(a, d, kd[d], p, acc[u], u > 0 ? lane63_of(acc[u > 0 ? u - 1 : 0]) : acc[u],
-                                   u > 0, u + 1 == UNROLL, p < nPacks, p + 1 < nPacks);
+          st16_dst_realigned<POLS>(a, d, kd[d], p, acc[u], u > 0 ? lane63_of(acc[u > 0 ? u - 1 : 0]) : halo,
+                                   u > 0 || useHalo, false, p < nPacks, p + 1 < nPacks);
         else if (p < nPacks)
           st16_dst<POLS>(a, d, p * 16, acc[u]);
       }
