@@ -600,14 +600,19 @@ static ncclResult_t launch_task(const Task& t) {
     if (old != t.comm->device) (void)hipSetDevice(old);
     return ncclSuccess;
   }
+  // One rank: the copy / PreMulSum kernel goes straight onto the caller's
+  // stream with no cross-stream ordering, as ncclLaunchOneRank does
+  // (enqueue.cc:2386-2388 — it bypasses the plan and the strong stream).
+  if (t.comm->nRanks == 1) {
+    const ncclResult_t r = launch_one_rank(t);
+    t.comm->opCount++;
+    if (old != t.comm->device) (void)hipSetDevice(old);
+    return r;
+  }
   ncclResult_t r = stream_order(t.comm, t.stream);
   if (r == ncclSuccess) {
-    if (t.comm->nRanks == 1) {
-      r = launch_one_rank(t);
-    } else {
-      const int algo = choose_algo(t);
-      r = algo == kAlgoLL ? launch_ll(&t, 1) : algo == kAlgoDirect ? launch_direct(t) : launch_ring(t);
-    }
+    const int algo = choose_algo(t);
+    r = algo == kAlgoLL ? launch_ll(&t, 1) : algo == kAlgoDirect ? launch_direct(t) : launch_ring(t);
   }
   if (r == ncclSuccess) r = stream_mark(t.comm, t.stream);
   t.comm->opCount++;
