@@ -207,11 +207,13 @@ static ncclResult_t capture_state(hipStream_t s, CaptureState* cs) {
   cs->id = id;
   return ncclSuccess;
 }
-static ncclResult_t stream_order(ncclComm* comm, hipStream_t s) {
-  CaptureState cs;
-  NCCLCHECK(capture_state(s, &cs));
-  if (cs.active) {
-    if (comm->capHasLast && comm->capId == cs.id && comm->capLastStream != s)
+// One capture query per call: stream_order fills `cs`, stream_mark and
+// stream_last_event reuse it (the capture state of s cannot change between
+// them — the caller holds the thread).
+static ncclResult_t stream_order(ncclComm* comm, hipStream_t s, CaptureState* cs) {
+  NCCLCHECK(capture_state(s, cs));
+  if (cs->active) {
+    if (comm->capHasLast && comm->capId == cs->id && comm->capLastStream != s)
       HIPCHECK(hipStreamWaitEvent(s, comm->capEvent, 0));
     return ncclSuccess;
   }
@@ -219,9 +221,7 @@ static ncclResult_t stream_order(ncclComm* comm, hipStream_t s) {
     HIPCHECK(hipStreamWaitEvent(s, comm->lastLaunch, 0));
   return ncclSuccess;
 }
-static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s) {
-  CaptureState cs;
-  NCCLCHECK(capture_state(s, &cs));
+static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s, const CaptureState& cs) {
   if (cs.active) {
     HIPCHECK(hipEventRecord(comm->capEvent, s));
     comm->capId = cs.id;
@@ -235,9 +235,7 @@ static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s) {
   return ncclSuccess;
 }
 // The event stream_mark just recorded on s (for joining other streams).
-static hipEvent_t stream_last_event(ncclComm* comm, hipStream_t s) {
-  CaptureState cs{false, 0};
-  (void)capture_state(s, &cs);
+static hipEvent_t stream_last_event(ncclComm* comm, const CaptureState& cs) {
   return cs.active ? comm->capEvent : comm->lastLaunch;
 }
 
@@ -609,12 +607,13 @@ static ncclResult_t launch_task(const Task& t) {
     if (old != t.comm->device) (void)hipSetDevice(old);
     return r;
   }
-  ncclResult_t r = stream_order(t.comm, t.stream);
+  CaptureState cs{false, 0};
+  ncclResult_t r = stream_order(t.comm, t.stream, &cs);
   if (r == ncclSuccess) {
     const int algo = choose_algo(t);
     r = algo == kAlgoLL ? launch_ll(&t, 1) : algo == kAlgoDirect ? launch_direct(t) : launch_ring(t);
   }
-  if (r == ncclSuccess) r = stream_mark(t.comm, t.stream);
+  if (r == ncclSuccess) r = stream_mark(t.comm, t.stream, cs);
   t.comm->opCount++;
   if (old != t.comm->device) (void)hipSetDevice(old);
   return r;
@@ -645,7 +644,8 @@ static ncclResult_t launch_ll_batch(const std::vector<Task>& ts) {
   for (const Task& t : ts)
     if (t.stream != s0 && std::find(others.begin(), others.end(), t.stream) == others.end())
       others.push_back(t.stream);
-  ncclResult_t r = stream_order(comm, s0);
+  CaptureState cs{false, 0};
+  ncclResult_t r = stream_order(comm, s0, &cs);
   for (hipStream_t s : others) {
     if (r != ncclSuccess) break;
     if (hipEventRecord(comm->joinEvent, s) != hipSuccess ||
@@ -653,8 +653,8 @@ static ncclResult_t launch_ll_batch(const std::vector<Task>& ts) {
       r = ncclUnhandledCudaError;
   }
   if (r == ncclSuccess) r = launch_ll(ts.data(), (int)ts.size());
-  if (r == ncclSuccess) r = stream_mark(comm, s0);
-  const hipEvent_t done = stream_last_event(comm, s0);
+  if (r == ncclSuccess) r = stream_mark(comm, s0, cs);
+  const hipEvent_t done = stream_last_event(comm, cs);
   for (hipStream_t s : others)
     if (r == ncclSuccess && hipStreamWaitEvent(s, done, 0) != hipSuccess)
       r = ncclUnhandledCudaError;
