@@ -635,6 +635,16 @@ def _flatten_ok(checks):
 def bench_allreduce(args):
     dist, rank, world, comm = _dist_setup()
     sp = torch.cuda.current_stream().cuda_stream
+    # One-time warm-up of the checker's own torch kernels (pattern fill /
+    # compare per dtype on 4 Ki elements: their first launches load code
+    # objects for ~0.1-0.2 s); reported as check_warmup_s, outside check_s.
+    t_w = time.perf_counter()
+    for tdt in _TDT.values():
+        w = torch.empty(4096, dtype=tdt, device="cuda")
+        pattern_fill(w, rank, world)
+        pattern_ok(w, world)
+    torch.cuda.synchronize()
+    check_warmup_s = time.perf_counter() - t_w
     xgmi = peer_copy_bench(dist, rank, world) if not args.no_peer else None
     sizes = [1 << p for p in range(3, 31)] if args.sweep else [args.bytes or (1 << 30)]
     rows = []
@@ -713,7 +723,7 @@ def bench_allreduce(args):
                         "spec_peak": round(links * XGMI_LINK_GBS, 2),
                         "measured_peer_copy": xgmi},
            "correct": {"all": correct_all, **checks, "initall_single_process": initall,
-                       "check_s": round(t_chk, 2),
+                       "check_s": round(t_chk, 2), "check_warmup_s": round(check_warmup_s, 3),
                        "line_s": round(line_s, 2),  # bench.py start (imports included) -> here
                        "check_frac": round(t_chk / line_s, 3),
                        "inputs": "integer-valued pattern (exact in any fold order), per timed path"}}
