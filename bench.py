@@ -10,8 +10,9 @@ N = 1 (default): BASELINE config 2 — 2-input fp32 sum reduce-copy, 256 MiB
 N > 1 (torch.distributed.run, one process per GPU): BASELINE config 3 at a
   fixed bucket — all-reduce fp32 sum through ncclAllReduce (the repo's own
   transport over xGMI peer memory, no RCCL; the library's algorithm choice,
-  reported as config.algorithm).  value = aggregate bus bandwidth
-  = sum over ranks of busbw, busbw = (S/t) * 2(n-1)/n (nccl-tests convention).
+  reported as config.algorithm).  value = bus bandwidth per rank, busbw =
+  (S/t) * 2(n-1)/n with t the max over ranks (nccl-tests convention); the sum
+  over ranks rides along as config.aggregate_busbw_all_ranks.
   torch.distributed (gloo, CPU tensors) only ships the unique id, barriers and
   the max-over-ranks time.  The same run adds `extras` (not `value`): config 3
   at a few sizes, config 5 (fp16 LL sizes), config 4 (RS + AG bf16, 4 GiB
@@ -255,40 +256,126 @@ def _nproc():
         return os.cpu_count() or 1
 
 
-def cpu_baseline(n_full, seconds=8.0):
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _cpulist(txt):
+    out = []
+    for part in (txt or "").split(","):
+        if "-" in part:
+            lo, hi = part.split("-")
+            out += range(int(lo), int(hi) + 1)
+        elif part:
+            out.append(int(part))
+    return out
+
+
+def host_topology():
+    """CPUs this process may run on, their NUMA nodes, sockets and physical
+    cores (sysfs), and the cgroup CPU quota if one is set."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+        list(range(os.cpu_count() or 1))
+    node_of = {}
+    base = "/sys/devices/system/node"
+    for name in sorted(os.listdir(base)) if os.path.isdir(base) else []:
+        if name.startswith("node") and name[4:].isdigit():
+            for c in _cpulist(_read(os.path.join(base, name, "cpulist"))):
+                node_of[c] = int(name[4:])
+    sock, core = {}, {}
+    for c in cpus:
+        t = f"/sys/devices/system/cpu/cpu{c}/topology"
+        sock[c] = int(_read(t + "/physical_package_id") or 0)
+        core[c] = (sock[c], int(_read(t + "/core_id") or c))
+    quota = None
+    cm = _read("/sys/fs/cgroup/cpu.max")
+    if cm and not cm.startswith("max"):
+        q, per = cm.split()[:2]
+        quota = int(q) / int(per)
+    phys, seen = [], set()
+    for c in cpus:
+        if core[c] not in seen:
+            seen.add(core[c])
+            phys.append(c)
+    nodes = sorted({node_of.get(c, 0) for c in cpus})
+    return {"cpus": cpus, "nproc": len(cpus), "physical_cores": phys,
+            "numa_nodes": len(nodes), "sockets": len({sock[c] for c in cpus}),
+            "node_of": node_of, "cgroup_cpu_quota": quota,
+            "machine_cpus": os.cpu_count()}
+
+
+def _spread(cands, k, node_of):
+    """k CPUs of `cands`, dealt round-robin over their NUMA nodes."""
+    by = {}
+    for c in cands:
+        by.setdefault(node_of.get(c, 0), []).append(c)
+    out, lists = [], list(by.values())
+    while len(out) < k and any(lists):
+        for lst in lists:
+            if lst and len(out) < k:
+                out.append(lst.pop(0))
+    return out
+
+
+def _host_register():
+    """hipHostRegister (torch's cudart binding) of an existing host range: pins
+    the pages where their first touch placed them.  Returns an undo callable,
+    or None when registration is unavailable."""
+    try:
+        rt = torch.cuda.cudart()
+    except Exception:  # noqa: BLE001
+        return None
+
+    def reg(ptr, nbytes):
+        if int(rt.cudaHostRegister(ptr, nbytes, 0)) != 0:
+            return None
+        return lambda: rt.cudaHostUnregister(ptr)
+    return reg
+
+
+def cpu_baseline(n_full, seconds=5.0):
     """SURVEY.md §8(d) CPU baseline: the oracle's C restatement (oracle/
-    reduce_ref.c, -O3) of the same 2-src f32 sum over the SAME shape as the
-    device step (2 x 256 MiB -> 256 MiB) in pinned host memory (torch
-    pin_memory = hipHostMalloc), on 1 core and on every core of the box
-    (`nproc` threads), each for a bounded sample of ~`seconds`.  `value` is the
-    all-cores figure; the 1-core figure rides along.  A reported baseline only
-    (the reference has no CPU reduce path)."""
+    reduce_ref.c) of the same 2-src f32 sum over the SAME shape as the device
+    step (2 x 256 MiB -> 256 MiB), compiled -O3 -march=native on this host
+    (oracle.native_lib), on persistent worker threads pinned one per CPU, each
+    first-touching its own page-aligned slices (so every slice sits on the
+    NUMA node of the core that reduces it), the pages then pinned with
+    hipHostRegister (page-locked host memory, as the survey specifies, left
+    where the first touch put them).  Runs on 1 core, on every CPU this
+    process may use, on one thread per physical core, and — when a cgroup CPU
+    quota is set — on that many physical cores spread over the NUMA nodes;
+    each a bounded ~`seconds` sample checked bit-exactly.  `value` is the best
+    multi-core figure.  A reported baseline only (the reference has no CPU
+    reduce path)."""
     from oracle import oracle as O
     n = n_full
-    a_t = torch.empty(n, dtype=torch.float32, pin_memory=True)
-    b_t = torch.empty(n, dtype=torch.float32, pin_memory=True)
-    d_t = torch.empty(n, dtype=torch.float32, pin_memory=True)
-    a, b, d = a_t.numpy(), b_t.numpy(), d_t.numpy()
-    a[:] = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
-    b[:] = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
-    nproc = _nproc()
+    topo = host_topology()
+    reg = _host_register()
+    runs = {"one_core": [topo["cpus"][0]], "all_cpus": topo["cpus"]}
+    if len(topo["physical_cores"]) != len(topo["cpus"]):
+        runs["physical_cores"] = topo["physical_cores"]
+    q = topo["cgroup_cpu_quota"]
+    if q and int(q) < len(topo["cpus"]) and int(q) >= 2:
+        runs["quota_cores"] = _spread(topo["physical_cores"], int(q), topo["node_of"])
     res = {}
-    for name, threads in (("one_core", 1), ("all_cores", nproc)):
-        O.reduce_copy(0, 7, 0, [a, b], out=[d], nthreads=threads)  # page in / warm
-        iters, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds:
-            O.reduce_copy(0, 7, 0, [a, b], out=[d], nthreads=threads)
-            iters += 1
-        dt = time.perf_counter() - t0
-        res[name] = {"GB/s": round(3 * n * 4 * iters / dt / 1e9, 2), "threads": threads,
-                     "iters": iters, "s": round(dt, 2)}
-    assert np.array_equal(d, a + b), "cpu baseline mismatch"
-    return {"value": res["all_cores"]["GB/s"], "unit": "GB/s", "cores": nproc, "kind": "port",
-            "sample": f"2-src f32 sum over {n} elems (3 x {n * 4 >> 20} MiB pinned host buffers), "
-                      f"oracle/reduce_ref.c -O3: {res['all_cores']['iters']} calls in "
-                      f"{res['all_cores']['s']} s on {nproc} pthreads (= nproc); "
-                      f"{res['one_core']['iters']} calls in {res['one_core']['s']} s on 1 thread",
-            "one_core": res["one_core"]["GB/s"], "nproc": nproc}
+    for name, cpus in runs.items():
+        res[name] = O.cpu_bench(n, cpus, seconds, register=reg)
+    multi = {k: v for k, v in res.items() if k != "one_core"}
+    best = max(multi, key=lambda k: multi[k]["GB/s"])
+    assert all(v["correct"] for v in res.values()), "cpu baseline mismatch"
+    return {"value": res[best]["GB/s"], "unit": "GB/s", "cores": res[best]["threads"], "kind": "port",
+            "sample": f"2-src f32 sum over {n} elems (3 x {n * 4 >> 20} MiB host buffers, "
+                      f"first-touched per worker, pinned={res[best]['pinned']}), oracle/reduce_ref.c "
+                      f"-O3 -march={res[best]['march']}: {res[best]['iters']} passes in {res[best]['s']} s "
+                      f"on {res[best]['threads']} pinned threads ({best}); every run checked bit-exactly",
+            "best": best, "runs": res, "one_core": res["one_core"]["GB/s"],
+            "nproc": topo["nproc"], "physical_cores": len(topo["physical_cores"]),
+            "numa_nodes": topo["numa_nodes"], "sockets": topo["sockets"],
+            "cgroup_cpu_quota": q, "machine_cpus": topo["machine_cpus"]}
 
 
 def _dist_setup():
@@ -705,28 +792,29 @@ def bench_allreduce(args):
     line_s = time.perf_counter() - _T_START
     last = rows[-1]
     links = {2: 1, 4: 3, 8: 7}.get(world, 1)
+    peak = links * XGMI_LINK_GBS  # spec, per link and direction (not a measurement)
     measured_link = (xgmi or {}).get("one_peer_GBs")
-    per_link = measured_link if measured_link else XGMI_LINK_GBS
-    peak = links * per_link
     correct_all = _flatten_ok(checks) and (initall is None or initall.get("ok") is True)
     out = {"metric": "device reduce-copy GB/s vs HBM peak; all-reduce busbw at 1/2/4/8 GPUs",
-           "value": round(last["busbw"] * world, 2), "unit": "GB/s", "n_gpus": world,
+           "value": round(last["busbw"], 2), "unit": "GB/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(last["us"] / 1e3, 4),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "data": "synthetic uniform[-1,1) seed 1000+rank (device-resident)",
            "config": {"workload": f"all-reduce fp32 sum, {last['bytes']} B per rank "
-                                  "(BASELINE config 3), value = aggregate busbw over ranks",
+                                  "(BASELINE config 3), value = busbw per rank (nccl-tests "
+                                  "convention: (S/t) * 2(n-1)/n, max time over ranks)",
                       "algorithm": last["algo"],
                       "bytes_per_rank": last["bytes"], "busbw_per_rank": round(last["busbw"], 2),
+                      "aggregate_busbw_all_ranks": round(last["busbw"] * world, 2),
                       "algbw": round(last["algbw"], 2), "parallelism": f"{last['algo']} x{world}",
                       "async_error": err, "correct": correct_all},
            "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": round(peak, 2),
                         "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
-                        "note": (f"per-rank busbw vs {links} links x {per_link:.1f} GB/s per link and "
-                                 "direction, " + ("measured (one-peer copy below)" if measured_link
-                                                 else f"spec {XGMI_LINK_GBS} GB/s (no measurement)")),
-                        "spec_peak": round(links * XGMI_LINK_GBS, 2),
-                        "measured_peer_copy": xgmi},
+                        "note": (f"per-rank busbw vs {links} link(s) x {XGMI_LINK_GBS} GB/s per link and "
+                                 "direction (MI355X spec 153.6 GB/s per link, bidirectional)"),
+                        "measured_peer_copy": xgmi,
+                        "frac_of_measured_copy": (round(last["busbw"] / (links * measured_link), 4)
+                                                  if measured_link else None)},
            "correct": {"all": correct_all, **checks, "initall_single_process": initall,
                        "check_s": round(t_chk, 2), "check_warmup_s": round(check_warmup_s, 3),
                        "line_s": round(line_s, 2),  # bench.py start (imports included) -> here
@@ -880,11 +968,12 @@ def bench_rs_ag(args):
     if rank:
         return None
     return {"metric": "reduce-scatter + all-gather busbw (BASELINE config 4)",
-            "value": round((r["rs_busbw"] + r["ag_busbw"]) / 2 * world, 2), "unit": "GB/s",
+            "value": round((r["rs_busbw"] + r["ag_busbw"]) / 2, 2), "unit": "GB/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": r["ms_per_rs_ag"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"workload": f"RS+AG bf16 {r['bytes']} B bucket", "rs_busbw": r["rs_busbw"],
+            "config": {"workload": f"RS+AG bf16 {r['bytes']} B bucket, value = mean of the RS and AG "
+                                   "busbw per rank", "rs_busbw": r["rs_busbw"],
                        "ag_busbw": r["ag_busbw"], "correct": {"rs": rs_ok, "ag": ag_ok}}}
 
 

@@ -54,11 +54,15 @@ typedef struct {
   int unroll;       /* 16-byte packs in flight per thread per source: 1, 2, 4 or 8 */
   int gridBlocks;   /* workgroups in the grid */
   int ntLoads;      /* load policy: 0 plain, 1 nontemporal, 2 sc0 sc1, 3 sc1 nt */
-  int ntStores;     /* store policy: same encoding */
-  int order;        /* hunk order: 0 round-robin, 1 XCD-contiguous */
+  int ntStores;     /* store policy: same encoding; 16 | d0 | d1 << 2 sets the
+                       two destinations' policies separately */
+  int order;        /* hunk order: 0 round-robin, 1 XCD-contiguous, 2 LDS-staged,
+                       3 stores interleaved across destinations, 4 pipelined */
 } vcclLaunchConfig;
-/* Sweep variants other than the defaults exist only for the 2-source fp32 sum
- * shape; other shapes always run the tuned default. */
+/* Sweep variants other than the defaults exist only for the fp32 sum shapes
+ * 2 -> 1 (every field), 2 -> 2 (unroll 2/4, per-destination store policies,
+ * order 0/3/4) and 1 -> 1 (unroll 2/4); other shapes always run the tuned
+ * default. */
 
 ncclResult_t vcclReduceCopyEx(vcclDevRedOp_t devOp, ncclDataType_t datatype, uint64_t redArg,
                               int preOpSrcs, int postOp, int nSrcs, const void* const* srcs,

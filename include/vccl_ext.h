@@ -39,7 +39,10 @@
  *                     call (host only): VCCL's cbd split and chunking
  *                     (scheduleCollTasksToPlan, src/enqueue.cc:518-644, for a
  *                     plan of one collective) for `nChannels` channels and a
- *                     FIFO slot of `slotBytes` (NCCL_BUFFSIZE / 8).  out[0..7]
+ *                     FIFO slot of `slotBytes` (NCCL_BUFFSIZE / 8) and
+ *                     `nThreads` ring threads (NCCL_NTHREADS: the channel
+ *                     tuning's maxThreads[RING][SIMPLE], tuning.cc:198-200).
+ *                     out[0..7]
  *                     = channelLo, channelHi, countLo, countMid, countHi,
  *                     chunkLo, chunkMid, chunkHi (elements; bytes for
  *                     all-gather, which the reference runs as int8).
@@ -78,9 +81,9 @@ ncclResult_t vcclCommNetStats(ncclComm_t comm, uint64_t* bytesSent, uint64_t* by
 ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences);
 ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoch, uint32_t directEpoch);
 ncclResult_t vcclRingPartition(int coll, size_t count, ncclDataType_t datatype, int nRanks,
-                               int nChannels, size_t slotBytes, int64_t* out);
+                               int nChannels, size_t slotBytes, int nThreads, int64_t* out);
 ncclResult_t vcclRingChunkOf(size_t count, ncclDataType_t datatype, int nRanks, int nChannels,
-                             size_t slotBytes, size_t i, int64_t* out);
+                             size_t slotBytes, int nThreads, size_t i, int64_t* out);
 
 #ifdef __cplusplus
 }

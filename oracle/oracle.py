@@ -64,6 +64,72 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+def _bind_cpu_bench(L):
+    sz, i32, vp, dbl = ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_double
+    L.ref_cpu_bench_alloc.argtypes = [sz, i32, ctypes.POINTER(i32), ctypes.POINTER(vp),
+                                      ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    L.ref_cpu_bench_run.argtypes = [vp, vp, vp, sz, i32, ctypes.POINTER(i32), dbl,
+                                    ctypes.POINTER(ctypes.c_long), ctypes.POINTER(dbl)]
+    L.ref_cpu_bench_free.argtypes = [vp, vp, vp, sz]
+    L.ref_reduce_copy.argtypes = [i32, i32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), i32,
+                                  i32, i32, ctypes.POINTER(vp), i32, ctypes.POINTER(vp), sz, i32]
+    return L
+
+
+_native = None
+
+
+def native_lib(outdir: str | None = None):
+    """The oracle's reduce_ref.c + cpu_bench.c compiled for THIS host
+    (-O3 -march=native, same IEEE flags as the checker build) into a scratch
+    directory — the CPU baseline's build; falls back to the
+    portable checker build (-march=x86-64-v3) when no compiler is present.
+    Returns (CDLL, march)."""
+    global _native
+    if _native is None:
+        import tempfile
+        d = outdir or tempfile.mkdtemp(prefix="vccl_cpu_native_")
+        so = os.path.join(d, "liboracle_native.so")
+        cmd = ["gcc", "-O3", "-march=native", "-fno-fast-math", "-ffp-contract=off", "-fPIC",
+               "-std=gnu11", "-shared", "-o", so, os.path.join(_HERE, "reduce_ref.c"),
+               os.path.join(_HERE, "cpu_bench.c"), "-lpthread", "-lm"]
+        try:
+            subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+            _native = (_bind_cpu_bench(ctypes.CDLL(so)), "native")
+        except (OSError, subprocess.SubprocessError):
+            _native = (_bind_cpu_bench(lib()), "x86-64-v3")
+    return _native
+
+
+def cpu_bench(n: int, cpus, seconds: float, register=None, native: bool = True) -> dict:
+    """f32 d = a + b over n elements on len(cpus) persistent workers pinned to
+    `cpus` (first-touched slices, see cpu_bench.c); `register(ptr, bytes)` /
+    its returned undo callable may pin the pages for the device
+    (hipHostRegister) between the first touch and the timed loop.  Returns
+    GB/s (3 x 4 n bytes per pass), passes, seconds, and the bit-exact check."""
+    L, march = native_lib() if native else (_bind_cpu_bench(lib()), "x86-64-v3")
+    nt = len(cpus)
+    cp = (ctypes.c_int * nt)(*cpus)
+    a, b, d = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    if L.ref_cpu_bench_alloc(n, nt, cp, ctypes.byref(a), ctypes.byref(b), ctypes.byref(d)) != 0:
+        raise MemoryError("cpu bench allocation")
+    undo = []
+    try:
+        if register is not None:
+            for p in (a, b, d):
+                undo.append(register(p.value, n * 4))
+        iters, el = ctypes.c_long(), ctypes.c_double()
+        ok = L.ref_cpu_bench_run(a, b, d, n, nt, cp, seconds, ctypes.byref(iters), ctypes.byref(el))
+    finally:
+        for u in undo:
+            if u:
+                u()
+        L.ref_cpu_bench_free(a, b, d, n)
+    return {"GB/s": round(3 * n * 4 * iters.value / el.value / 1e9, 2), "threads": nt,
+            "iters": iters.value, "s": round(el.value, 2), "correct": bool(ok), "march": march,
+            "pinned": register is not None and all(undo)}
+
+
 def host_to_dev_redop(op: int, dtype: int, nranks: int) -> tuple[int, int]:
     d, a = ctypes.c_int(), ctypes.c_uint64()
     rc = lib().ref_host_to_dev_redop(op, dtype, nranks, ctypes.byref(d), ctypes.byref(a))

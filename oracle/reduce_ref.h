@@ -80,6 +80,15 @@ void ref_ring_fold(int devOp, int type, uint64_t redArg, int preOp, int nranks,
 void ref_chain_fold(int devOp, int type, uint64_t redArg, int preOp, int nranks,
                     const void* const* inputs, void* out, size_t nElts);
 
+/* Host-core baseline (cpu_bench.c; bench.py's cpu_baseline leg only): the
+ * config-2 shape (f32 d = a + b over n elements) on `nthreads` persistent
+ * workers pinned to cpus[t] (NULL = unpinned), buffers first-touched by
+ * their owners.  run returns 1 when the result checks bit-exactly. */
+int ref_cpu_bench_alloc(size_t n, int nthreads, const int* cpus, void** a, void** b, void** d);
+int ref_cpu_bench_run(void* a, void* b, void* d, size_t n, int nthreads, const int* cpus,
+                      double seconds, long* iters, double* elapsed);
+void ref_cpu_bench_free(void* a, void* b, void* d, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -217,3 +217,32 @@ def channel_of(work: CbdWork, count):
         chan[off:off + length] = c
     assert (chan >= 0).all(), "partition does not cover the block"
     return chan
+
+
+def allreduce_owner_at(work: CbdWork, count, nranks, idx):
+    """allreduce_owner for selected elements only (sampled windows of
+    buffers too large for the full map): (channel, finishing ring index) of
+    every index in `idx`."""
+    idx = np.asarray(idx, dtype=np.int64)
+    chan = np.full(idx.size, -1, np.int32)
+    owner = np.full(idx.size, -1, np.int32)
+    elt_align = max(1, 16 // work.elt_size)
+    for c in range(work.channel_lo, work.channel_hi + 1):
+        off, length, chunk = work.part(c)
+        sel = (idx >= off) & (idx < off + length)
+        if not sel.any():
+            continue
+        local = idx[sel] - off
+        loop = nranks * chunk
+        n_full = length // loop
+        tail0 = n_full * loop            # start of the short last loop (if any)
+        k = (local % loop) // chunk
+        rem = length - tail0
+        if rem > 0:
+            short = _align_up(_div_up(rem, nranks), elt_align)
+            in_tail = local >= tail0
+            k = np.where(in_tail, (local - tail0) // short, k)
+        chan[sel] = c
+        owner[sel] = k
+    assert (chan >= 0).all(), "index outside the partition"
+    return chan, owner

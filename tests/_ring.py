@@ -45,7 +45,7 @@ def _div_up(x, a):
     return (x + a - 1) // a
 
 
-def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None):
+def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=512):
     """Exact expected ring all-reduce output (identical on every rank): the
     oracle's restatement of VCCL's channel partition and chunking
     (oracle/vccl_sched.py) decides channel and finishing ring index per
@@ -56,7 +56,8 @@ def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None):
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size
     esz = inputs[0].dtype.itemsize
-    work = S.cbd_schedule("ar", count, esz, n, nch, buff_size=slot_bytes * S.NCCL_STEPS)
+    work = S.cbd_schedule("ar", count, esz, n, nch, buff_size=slot_bytes * S.NCCL_STEPS,
+                          nthreads=nthreads)
     chan, owner = S.allreduce_owner(work, count, n)
     out = np.empty_like(inputs[0])
     for c in range(work.channel_lo, work.channel_hi + 1):
@@ -69,7 +70,7 @@ def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None):
     return out
 
 
-def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=None):
+def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=None, nthreads=512):
     """Per-rank expected outputs; inputs[r] has n*recvcount elements.  Rank
     r's block is folded on the ring of each element's channel (VCCL's cbd
     partition of the recvcount block), finishing at r."""
@@ -79,7 +80,7 @@ def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=N
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size // n
     work = S.cbd_schedule("rs", count, inputs[0].dtype.itemsize, n, nch,
-                          buff_size=slot_bytes * S.NCCL_STEPS)
+                          buff_size=slot_bytes * S.NCCL_STEPS, nthreads=nthreads)
     chan = S.channel_of(work, count)
     outs = [np.empty(count, inputs[0].dtype) for _ in range(n)]
     for c in range(work.channel_lo, work.channel_hi + 1):

@@ -6,7 +6,8 @@ Captures [LL all-reduce (small), direct all-reduce (mid), ring all-reduce
 (large), ring reduce-scatter]
 into one graph on a side stream (after an eager call on the current stream,
 and followed by another), replays it 4 times with new integer-valued inputs (exact in any
-fold order) and checks every output; exit code 0 = all replays correct."""
+fold order) and checks every output; then two captures interleaved on the
+same comm (interleaved_captures); exit code 0 = all replays correct."""
 import os
 import sys
 
@@ -16,6 +17,50 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 from vccl_amd import nccl  # noqa: E402
+
+
+def interleaved_captures(comm, rank, n):
+    """two captures on one comm, interleaved.  Capture A forks a
+    second stream sA2 before its first collective (X1 on sA), then capture B
+    records Y on sB, then A's second collective X2 goes onto sA2.  X2 must
+    wait for X1 inside graph A (the comm's ordering is kept per capture id),
+    or the replay runs two collectives of the comm at once."""
+    big = 3 << 20  # the ring / direct paths: concurrent calls would share FIFOs
+    x1, x2, xb = (torch.empty(big, device="cuda") for _ in range(3))
+    y1, y2, yb = (torch.empty(big, device="cuda") for _ in range(3))
+    sA, sA2, sB = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    gA, gB = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    f32, add = nccl.ncclFloat32, nccl.ncclSum
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sA):
+        gA.capture_begin(capture_error_mode="relaxed")
+    sA2.wait_stream(sA)  # sA2 joins capture A before X1 exists
+    comm.all_reduce(x1.data_ptr(), y1.data_ptr(), big, f32, add, sA.cuda_stream)
+    with torch.cuda.stream(sB):
+        gB.capture_begin(capture_error_mode="relaxed")
+    comm.all_reduce(xb.data_ptr(), yb.data_ptr(), big, f32, add, sB.cuda_stream)
+    comm.all_reduce(x2.data_ptr(), y2.data_ptr(), big, f32, add, sA2.cuda_stream)
+    sA.wait_stream(sA2)
+    with torch.cuda.stream(sB):
+        gB.capture_end()
+    with torch.cuda.stream(sA):
+        gA.capture_end()
+    ok = True
+    for it in range(3):
+        def val(r, k):
+            return ((torch.arange(big, device="cuda") * (r + 5 + k) + 11 * it) % 89).float()
+        x1.copy_(val(rank, 1))
+        x2.copy_(val(rank, 2))
+        xb.copy_(val(rank, 3))
+        torch.cuda.synchronize()
+        gA.replay()
+        gB.replay()
+        torch.cuda.synchronize()
+        for y, k in ((y1, 1), (y2, 2), (yb, 3)):
+            ok &= torch.equal(y, sum(val(r, k) for r in range(n)))
+    if not ok:
+        print(f"rank {rank}: interleaved captures mismatch", flush=True)
+    return ok
 
 
 def main():
@@ -69,6 +114,7 @@ def main():
                     torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     ok &= torch.equal(eager_y, exp_eager)
+    ok &= interleaved_captures(comm, rank, n)
     ok &= comm.async_error() == 0
     comm.destroy()
     sys.exit(0 if ok else 4)

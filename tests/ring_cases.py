@@ -67,6 +67,12 @@ CASES = [
     ("rs_f16_prod_direct", "rs", 1, 6, 600_001),
     ("ag_f32_direct", "ag", 0, 7, 300_001),
     ("ag_u8_direct_odd", "ag", 0, 1, 1_500_007),
+] + [
+    # BASELINE config 5: fp16 sum at every power of two from 8 B to 128 KiB
+    # (the one-hop LL all-reduce wherever the geometry's LL threshold admits
+    # it — 8 ranks included — checked bit-exactly against the oracle's chain
+    # fold, and within tolerance of VCCL's ring result)
+    (f"ar_f16_sum_ll_{1 << p}B", "ar", 0, 6, (1 << p) // 2) for p in range(3, 18)
 ]
 
 # VCCL's ring schedule on the geometry its own tuner would pick on an 8-GPU
@@ -142,13 +148,16 @@ def gen_group_input(gi, rank):
     return rng.uniform(-1, 1, count).astype(O.NP_DTYPE[dt])
 
 
-def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20):
+def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
+                   nthreads=512):
     name, op, dt, count = GROUP_CASES[gi]
     ins = [gen_group_input(gi, r) for r in range(n_ranks)]
-    return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk)
+    return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
+                       nthreads)
 
 
-def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk):
+def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
+                nthreads=512):
     """All-reduce result: LL chain fold up to ll_max bytes, the ring's
     owner-map fold (VCCL's ring schedule on these channels) above — for the
     two-shot direct path too, which folds every element in the ring's order
@@ -159,10 +168,11 @@ def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direc
     if count * ins[0].dtype.itemsize <= ll_max:
         dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
         return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
-    return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes)
+    return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes, nthreads=nthreads)
 
 
-def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20):
+def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
+             nthreads=512):
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
     (oracle ref_chain_fold); larger ones the two-shot direct path (up to
@@ -170,10 +180,11 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
     name, coll, op, dt, count = CASES[case_idx]
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace", "ar_mis"):
-        e = expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk)
+        e = expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
+                        nthreads)
         return [e] * n_ranks
     if coll == "rs":
-        return _ring.expected_reducescatter(op, dt, ins, nch)
+        return _ring.expected_reducescatter(op, dt, ins, nch, nthreads=nthreads)
     full = np.concatenate(ins)
     return [full] * n_ranks
 

@@ -45,13 +45,13 @@ DIRECT_TEST = 4 << 20
 DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in chunks
 
 
-def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST):
+def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST, nthreads=512):
     """Bit-exact against the path's own fold order (the ring's IS VCCL's
     schedule on our rings and channels); for fp sum / prod additionally
     within the §8c tolerance of the exact value and of VCCL's result on its
     reference geometry (RC.vccl_reference)."""
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk)
+    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk, nthreads)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
     vref = RC.vccl_reference(ci, n)
@@ -172,6 +172,7 @@ def test_multi_process_ranks(n, geom):
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
     ll_max, direct_max, chunk = LL_DEFAULT, DIRECT_TEST, DIRECT_CHUNK_TEST
+    nthreads = 512
     if geom in ("test", "ring_only", "direct_only"):
         env.update(TEST_GEOM)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
@@ -197,6 +198,7 @@ def test_multi_process_ranks(n, geom):
                    VCCL_DIRECT_MAX_BLOCKS="16", VCCL_NTHREADS="256", VCCL_CHANNELS_PER_RING="2")
         nch, slot = _ring.n_channels(n, per_ring=2), 512 << 10
         ll_max, direct_max, chunk = 128 << 10, 64 << 20, 16 << 20
+        nthreads = 256  # NCCL_NTHREADS steers VCCL's channel tuning too
     else:  # library defaults (2 ranks x 32 channels x 1024 threads fit on one GPU)
         for k in TEST_GEOM:
             env.pop(k, None)
@@ -222,9 +224,10 @@ def test_multi_process_ranks(n, geom):
         assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
-            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk)
+            _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk,
+                   nthreads)
         _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot, ll_max,
-                     direct_max, chunk)
+                     direct_max, chunk, nthreads)
         fused = int(res[0]["launch_stats"][1])
         assert (fused > 0) == (ll_max > 0), f"fused group launches: {fused} (LL max {ll_max})"
         for r in range(n):
@@ -266,9 +269,9 @@ def test_beyond_2gib_two_ranks():
     assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
 
 
-def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk):
+def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512):
     for gi, (name, op, dt, count) in enumerate(RC.GROUP_CASES):
-        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk)
+        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads)
         for r in range(n):
             assert_bitexact(dt, outs[r][name], exp, minmax=op in (2, 3),
                             what=f"group {name} n={n} rank {r}")

@@ -34,16 +34,18 @@ def _sizes():
 def test_library_partition_equals_oracle(coll, n):
     for nch in (1, 2, 7, 14, 32, 56, 64):
         for dt in (7, 9, 0, 8):
-            for slot in (4096, 256 << 10, 512 << 10):
+            # NCCL_NTHREADS: 256 changes the channel tuning
+            # (enqueue.cc:1921-1924) and with it every part boundary
+            for slot, nt in ((4096, 512), (256 << 10, 512), (512 << 10, 512), (512 << 10, 256)):
                 for count in _sizes():
-                    lib = nccl.ring_partition(COLLS[coll], count, dt, n, nch, slot)
+                    lib = nccl.ring_partition(COLLS[coll], count, dt, n, nch, slot, nt)
                     w = S.cbd_schedule(coll, count, ESZ[dt], n, nch,
-                                       buff_size=slot * S.NCCL_STEPS)
+                                       buff_size=slot * S.NCCL_STEPS, nthreads=nt)
                     per = S.grain_size(w.proto) // w.elt_size
                     ref = (w.channel_lo, w.channel_hi, w.count_lo, w.count_mid, w.count_hi,
                            w.chunk_grains_lo * per, w.chunk_grains_mid * per, w.chunk_grains_hi * per)
                     # chunk sizes of absent parts are unused on the device
-                    assert lib[:5] == ref[:5], (coll, n, nch, dt, slot, count, lib, ref)
+                    assert lib[:5] == ref[:5], (coll, n, nch, dt, slot, nt, count, lib, ref)
                     for i, cnt in ((5, w.count_lo), (6, w.count_mid), (7, w.count_hi)):
                         if cnt:
                             assert lib[i] == ref[i], (coll, n, nch, dt, slot, count, i)
@@ -100,6 +102,10 @@ def test_hand_derived_cases():
     # the per-call channel tuning: 1 MiB all-reduce < nc * 512 thr * 64 B for
     # nc > 32, so at most 32 channels carry it (enqueue.cc:1921-1924)
     assert S.ring_n_max_channels("ar", 1 << 18, 4, 8, 56) == 32
+    # NCCL_NTHREADS=256 halves the per-channel threshold: 64 channels' worth
+    assert S.ring_n_max_channels("ar", 1 << 18, 4, 8, 56, nthreads=256) == 56
+    assert nccl.ring_partition(0, 1 << 18, 7, 8, 56, 512 << 10, 256)[1] > \
+        nccl.ring_partition(0, 1 << 18, 7, 8, 56, 512 << 10, 512)[1]
 
 
 @pytest.mark.parametrize("n", [2, 3, 4, 8])

@@ -9,6 +9,7 @@
 #        smoke     __graft_entry__.smoke()
 #        py:<file> python <file> (a tool script)
 #        sweep:<mode>  tools/sweep_rc.py with SWEEP_MODE=<mode> (6 rounds)
+#        pmcshapes tools/pmc_shapes.py (PMC passes over 2->2, copy, 2->1 shapes)
 #        pmc       tools/pmc_traffic.py (separate FETCH_SIZE / WRITE_SIZE passes)
 #        lat:<n>   tools/coll_latency.py on n ranks sharing the GPU (LAT_* env)
 #        mprof:<n> the N>1 bench line on n ranks sharing the GPU, every rank
@@ -32,6 +33,7 @@ for s in "$@"; do
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
     py:*) timeout -k 10 600 python -u ${s#py:} > $O/$(basename ${s#py:} .py).log 2>&1 ;;
     sweep:*) SWEEP_MODE=${s#sweep:} SWEEP_ROUNDS=${SWEEP_ROUNDS:-6} timeout -k 10 300 python -u tools/sweep_rc.py > $O/sweep_${s#sweep:}.log 2>&1 ;;
+    pmcshapes) timeout -k 10 200 python -u tools/rc_shape_driver.py > $O/rc_shape_driver.log 2>&1 && timeout -k 10 500 python -u tools/pmc_shapes.py > $O/pmc_shapes.log 2>&1 && cp gpurun_out/pmc_shapes.json $O/ ;;
     pmc) timeout -k 10 400 python -u tools/pmc_traffic.py > $O/pmc_traffic.log 2>&1 && cp gpurun_out/pmc_traffic.json $O/ ;;
     lat:*) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#lat:} --master-addr 127.0.0.1 --master-port 29534 tools/coll_latency.py > $O/lat_n${s#lat:}.log 2> $O/lat_n${s#lat:}.err ;;
     mprof:*) timeout -k 10 600 python -u tools/mp_prof.py ${s#mprof:} $O/mprof_n${s#mprof:} --steps 5 --warmup 2 > $O/mprof_n${s#mprof:}.log 2>&1 ;;

@@ -33,6 +33,8 @@ def main():
         return misaligned(n, rounds, reps)
     if mode.startswith("dtype"):  # dtype<code>: geometry sweep of one element type's sum kernel
         return dtype_geometry(int(mode[5:]), n * 4, rounds, reps)
+    if mode == "twodst":
+        return two_dst(n, rounds, reps)
     if mode == "policies":
         # load/store policy: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1 nt; order 1 = XCD-contiguous hunks
         for block, unroll, ld, st, order in itertools.product(
@@ -123,6 +125,69 @@ def misaligned(n, rounds, reps):
         print(json.dumps({"cfg": name, "offsets": [so, do],
                           "median_gbs": round(float(np.median(nbytes / (t / 1e3) / 1e9)), 1),
                           "median_us": round(float(np.median(t)) * 1e3, 2)}))
+
+
+POL = {"plain": 0, "nt": 1, "sys": 2, "sc1nt": 3}
+
+
+def two_dst(n, rounds, reps):
+    """The two-destination shape (2 x n f32 -> 2 x n: the ring's final reduce
+    step and every recv-copy-send step) against its read/write-mix reference,
+    the 1 -> 1 copy (ours and torch's), interleaved in one process.  2 -> 2
+    variants: unroll x per-destination store policy x store order (0
+    destination-major, 3 interleaved, 4 pipelined).  GB/s = (srcs + dsts) x
+    bytes / kernel time."""
+    a = torch.rand(n, device="cuda") * 2 - 1
+    b = torch.rand(n, device="cuda") * 2 - 1
+    d0, d1 = torch.empty_like(a), torch.empty_like(a)
+    ref = a + b
+    s = torch.cuda.current_stream()
+    hunk = lambda u: 256 * u * 16  # noqa: E731
+    variants = []  # (name, nsrc, ndst, cfg)
+    for u, (p0, p1), order in itertools.product(
+            (2, 4), (("sys", "sys"), ("nt", "nt"), ("plain", "plain"), ("sys", "nt"), ("nt", "sys"),
+                     ("sys", "plain"), ("plain", "sys"), ("sc1nt", "sc1nt")), (0, 3, 4)):
+        cfg = {"blockSize": 256, "unroll": u, "gridBlocks": (n * 4 + hunk(u) - 1) // hunk(u),
+               "ntLoads": 1, "ntStores": 16 | POL[p0] | POL[p1] << 2, "order": order}
+        variants.append((f"2to2_u{u}_{p0}_{p1}_o{order}", 2, 2, cfg))
+    variants.append(("2to2_default", 2, 2, None))
+    for u, ld, st in itertools.product((2, 4), ("nt", "plain"), ("sys", "nt", "plain")):
+        cfg = {"blockSize": 256, "unroll": u, "gridBlocks": (n * 4 + hunk(u) - 1) // hunk(u),
+               "ntLoads": POL[ld], "ntStores": POL[st], "order": 0}
+        variants.append((f"copy_u{u}_{ld}_{st}", 1, 1, cfg))
+    variants.append(("copy_torch", 1, 1, "torch_copy"))
+    variants.append(("2to1_default", 2, 1, None))
+    times = {v[0]: [] for v in variants}
+    for r in range(rounds):
+        order = list(range(len(variants)))
+        np.random.default_rng(r).shuffle(order)
+        for i in order:
+            name, ns, nd, cfg = variants[i]
+            srcs = [a.data_ptr(), b.data_ptr()][:ns]
+            dsts = [d0.data_ptr(), d1.data_ptr()][:nd]
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(reps)]
+            for e0, e1 in ev:
+                e0.record(s)
+                if cfg == "torch_copy":
+                    d0.copy_(a)
+                else:
+                    nccl.reduce_copy(0, 7, 0, srcs, dsts, n, s.cuda_stream, config=cfg)
+                e1.record(s)
+            torch.cuda.synchronize()
+            times[name] += [e0.elapsed_time(e1) for e0, e1 in ev]
+            if r == 0:
+                want = ref if ns == 2 else a
+                assert torch.equal(d0, want) and (nd == 1 or torch.equal(d1, want)), name
+    rows = []
+    for name, ns, nd, cfg in variants:
+        t = np.array(times[name][reps:])
+        gbs = (ns + nd) * n * 4 / (t / 1e3) / 1e9
+        rows.append({"cfg": name, "median_gbs": round(float(np.median(gbs)), 1),
+                     "max_gbs": round(float(gbs.max()), 1), "median_us": round(float(np.median(t)) * 1e3, 2)})
+    rows.sort(key=lambda x: -x["median_gbs"])
+    for row in rows:
+        print(json.dumps(row))
 
 
 def dtype_geometry(dt, nbytes, rounds, reps):

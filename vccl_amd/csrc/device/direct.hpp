@@ -64,7 +64,10 @@ constexpr int kDirectCopyUnroll = VCCL_DIRECT_COPY_UNROLL;
 // dst_d[i] = postOp(pre?(src_0[i]) (+) pre?(src_1[i]) (+) ...), preOp on
 // sources s < preN.  All sources' loads of a hunk are issued before the first
 // reduce (the inbox latency is paid once per hunk, not once per source).
-// DST_LAST: policy of the last destination (the own output); others kSys.
+// STP_LAST: policy of the last destination (the own output); others STP.
+// Own outputs that are the only destination are stored write-through (sc0
+// sc1): the copy shape runs at 7.13 TB/s that way against 6.68 with plain
+// stores (tools/sweep_rc.py twodst, profiles/r03a).
 template <class Fn, int U, int LDP, int STP, int STP_LAST>
 __device__ __forceinline__ void direct_rc(const Fn& fn, const char* const (&src)[kDirectMaxRanks],
                                           int nS, int preN, bool post,
@@ -406,7 +409,7 @@ __device__ void direct_allreduce(const DirectWork& w) {
         block_of(o, &off, &len);
         const char* s[kDirectMaxRanks] = {myBuf + direct_region_off(1, o, n, w.regionBytes) + inOff};
         char* d[kDirectMaxRanks] = {out + off * (int64_t)sizeof(T)};
-        direct_rc<Fn, kDirectCopyUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+        direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
       }
     }
     __syncthreads();  // the region reads of this chunk precede the next chunk's posts
@@ -480,7 +483,7 @@ __device__ void direct_reducescatter(const DirectWork& w) {
           s[j] = q == me ? in + ((int64_t)me * count + cur) * esz
                          : myBuf + direct_region_off(0, q, n, w.regionBytes) + ro;
         }
-        direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, 1,
+        direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, n, w.preOp ? n : 0, true, d, 1,
                                                            end - cur, tid, nt);
         cur = end;
       }
@@ -551,7 +554,7 @@ __device__ __forceinline__ void direct_allgather(const DirectWork& w) {
                                                   : myBuf + direct_region_off(0, o, n, w.regionBytes) + rOff};
         char* d[kDirectMaxRanks] = {out + (int64_t)o * count + lo};
         if (o == me && s[0] == d[0]) continue;  // in place: my block is already there
-        direct_rc<Fn, kDirectCopyUnroll, kSys, kPlain, kPlain>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+        direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
       }
     }
     direct_post(w, P, 1, b, e);

@@ -19,6 +19,15 @@ constexpr int kRcMaxGrid = 65536;
 constexpr int kRcDefLd = kLdNT;
 constexpr int kRcDefSt = kSys;
 constexpr int kRcDefOrder = 0;
+// With two or more destinations their stores alternate write-through (sc0
+// sc1) and nt: 2 -> 2 f32 runs at 7.13 TB/s so, 6.0 with every destination
+// write-through (tools/sweep_rc.py twodst, profiles/r03a).  ND = 0: runtime
+// destination count.
+constexpr int rc_def_pols(int nd) {
+  return nd == 1 ? uniform_pol(kRcDefLd, kRcDefSt)
+                 : mkpol(kRcDefLd, kRcDefLd, kRcDefLd, kRcDefLd, kSys, kNT, kSys, kNT);
+}
+constexpr int kRcDefSt2 = 16 | kSys | kNT << 2;  // the same, in vcclLaunchConfig's encoding
 
 // Internal entry used by both the C ABI and the one-rank path.  `a` holds the
 // pointers; geometry from cfg (nullptr = defaults).

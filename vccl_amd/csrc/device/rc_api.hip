@@ -30,9 +30,12 @@ hipError_t reduce_copy_launch(int devOp, int datatype, uint64_t redArg, RCArgs a
     return hipErrorInvalidValue;
   if (lg.unroll != 1 && lg.unroll != 2 && lg.unroll != 4 && lg.unroll != 8) return hipErrorInvalidValue;
   lg.ntLoads = cfg ? cfg->ntLoads : kRcDefLd;
-  lg.ntStores = cfg ? cfg->ntStores : kRcDefSt;
+  lg.ntStores = cfg ? cfg->ntStores : (a.nDsts >= 2 ? kRcDefSt2 : kRcDefSt);
   lg.order = cfg ? cfg->order : kRcDefOrder;
-  if (lg.ntLoads < 0 || lg.ntLoads > 3 || lg.ntStores < 0 || lg.ntStores > 3) return hipErrorInvalidValue;
+  // ntStores 16..31: per-destination policies (two-destination sweep only)
+  if (lg.ntLoads < 0 || lg.ntLoads > 3 || lg.ntStores < 0 || lg.ntStores > 31 ||
+      (lg.ntStores > 3 && lg.ntStores < 16))
+    return hipErrorInvalidValue;
   const int64_t bytes = nElts * elt_size_of_kt(k);
   const int64_t hunk = (int64_t)lg.block * lg.unroll * 16;
   const int64_t want = (bytes + hunk - 1) / hunk;

@@ -13,11 +13,13 @@
 
 namespace vccl {
 
-template <class Fn, int NS, int ND, int UNROLL, int LD, int ST, int ORDER>
+// POLS: per-operand memory policies (mkpol); ORDER 4 = the software-pipelined
+// hunk loop (next hunk's loads issued before this hunk's stores).
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER>
 __global__ __launch_bounds__(1024) void k_reduce_copy(RCArgs a, int64_t nElts, uint64_t redArg) {
   Fn fn(load_op_arg(a.argPtr, a.argBytes, redArg));
-  reduce_copy<Fn, NS, ND, UNROLL, uniform_pol(LD, ST), ORDER>(fn, a, nElts, blockIdx.x, gridDim.x,
-                                                           threadIdx.x, blockDim.x);
+  reduce_copy<Fn, NS, ND, UNROLL, POLS, ORDER == 4 ? 0 : ORDER, ORDER == 4>(
+      fn, a, nElts, blockIdx.x, gridDim.x, threadIdx.x, blockDim.x);
 }
 
 // LDS-staged variant (benchmark sweep only, `order` 2): the north-star's
@@ -80,13 +82,52 @@ __global__ __launch_bounds__(256) void k_reduce_copy_lds(RCArgs a, int64_t nTile
   }
 }
 
-// Launch one instantiation.
+// Launch one instantiation (uniform load policy L, store policy S).
 template <class Fn, int NS, int ND, int U, int L, int S, int O>
 static hipError_t launch_one(const RCArgs& a, int64_t nElts, uint64_t redArg, const LaunchGeom& lg,
                              hipStream_t s) {
-  hipLaunchKernelGGL((k_reduce_copy<Fn, NS, ND, U, L, S, O>), dim3(lg.grid), dim3(lg.block), 0, s,
-                     a, nElts, redArg);
+  hipLaunchKernelGGL((k_reduce_copy<Fn, NS, ND, U, uniform_pol(L, S), O>), dim3(lg.grid),
+                     dim3(lg.block), 0, s, a, nElts, redArg);
   return hipGetLastError();
+}
+
+// Two-destination sweep (the ring's final-reduce / recv-copy-send shape,
+// 2 sources -> 2 destinations, measurement only): nt loads, unroll {2, 4},
+// a store policy PER destination (ntStores = 16 | d0 | d1 << 2; below 16 the
+// uniform encoding), store order {0 destination-major, 3 interleaved,
+// 4 pipelined}.
+template <class Fn, int U, int D0, int D1>
+static hipError_t launch_2dst_pol(const RCArgs& a, int64_t n, uint64_t r, const LaunchGeom& lg,
+                                  hipStream_t s) {
+  constexpr int P = mkpol(kNT, kNT, kNT, kNT, D0, D1, D1, D1);
+  auto go = [&]<int O>() {
+    hipLaunchKernelGGL((k_reduce_copy<Fn, 2, 2, U, P, O>), dim3(lg.grid), dim3(lg.block), 0, s, a,
+                       n, r);
+    return hipGetLastError();
+  };
+  if (lg.order == 3) return go.template operator()<3>();
+  if (lg.order == 4) return go.template operator()<4>();
+  return go.template operator()<0>();
+}
+template <class Fn, int U>
+static hipError_t sweep_2dst(const RCArgs& a, int64_t n, uint64_t r, const LaunchGeom& lg,
+                             hipStream_t s) {
+  const int d0 = lg.ntStores >= 16 ? (lg.ntStores & 3) : lg.ntStores;
+  const int d1 = lg.ntStores >= 16 ? ((lg.ntStores >> 2) & 3) : lg.ntStores;
+  auto by_d1 = [&]<int D0>() -> hipError_t {
+    switch (d1) {
+      case kNT: return launch_2dst_pol<Fn, U, D0, kNT>(a, n, r, lg, s);
+      case kSys: return launch_2dst_pol<Fn, U, D0, kSys>(a, n, r, lg, s);
+      case kSc1NT: return launch_2dst_pol<Fn, U, D0, kSc1NT>(a, n, r, lg, s);
+      default: return launch_2dst_pol<Fn, U, D0, kPlain>(a, n, r, lg, s);
+    }
+  };
+  switch (d0) {
+    case kNT: return by_d1.template operator()<kNT>();
+    case kSys: return by_d1.template operator()<kSys>();
+    case kSc1NT: return by_d1.template operator()<kSc1NT>();
+    default: return by_d1.template operator()<kPlain>();
+  }
 }
 
 // Sweep dispatch (benchmark shape only): unroll {1,2,4,8} x load policy
@@ -137,9 +178,18 @@ static hipError_t launch_nsnd(const RCArgs& a, int64_t nElts, uint64_t redArg,
   // Only the benchmark shape (2-src f32 sum) carries the full sweep set; every
   // other functor gets the tuned default (keeps the code object small).
   constexpr bool kSweep = std::is_same<Fn, FnSum<float>>::value && NS == 2 && ND == 1;
-  if constexpr (!kSweep) {
-    return launch_one<Fn, NS, ND, kRcDefUnroll, kRcDefLd, kRcDefSt, kRcDefOrder>(a, nElts, redArg,
-                                                                                 lg, s);
+  constexpr bool kSweep2 = std::is_same<Fn, FnSum<float>>::value && NS == 2 && ND == 2;
+  if constexpr (kSweep2) {
+    if (lg.unroll == 4) return sweep_2dst<Fn, 4>(a, nElts, redArg, lg, s);
+    return sweep_2dst<Fn, 2>(a, nElts, redArg, lg, s);
+  } else if constexpr (std::is_same<Fn, FnSum<float>>::value && NS == 1 && ND == 1) {
+    // the copy shape (1 -> 1): the read/write-mix reference for the above
+    if (lg.unroll == 4) return sweep_ls<Fn, NS, ND, 4>(a, nElts, redArg, lg, s);
+    return sweep_ls<Fn, NS, ND, 2>(a, nElts, redArg, lg, s);
+  } else if constexpr (!kSweep) {
+    hipLaunchKernelGGL((k_reduce_copy<Fn, NS, ND, kRcDefUnroll, rc_def_pols(ND), kRcDefOrder>),
+                       dim3(lg.grid), dim3(lg.block), 0, s, a, nElts, redArg);
+    return hipGetLastError();
   } else {
     if (lg.unroll == 8) return sweep_ls<Fn, NS, ND, 8>(a, nElts, redArg, lg, s);
     if (lg.unroll == 2) return sweep_ls<Fn, NS, ND, 2>(a, nElts, redArg, lg, s);

@@ -203,6 +203,8 @@ __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t 
   // ORDER 1: workgroups b, b+8, b+16, ... (one XCD under round-robin
   // dispatch) take consecutive hunks, so each XCD streams one contiguous
   // eighth of the buffer (speed only: any placement is correct).
+  // ORDER 3: destination stores interleaved (pack u to every destination,
+  // then pack u + 1) instead of destination by destination.
   if constexpr (ORDER == 1) {
     if (nWorkers % 8 == 0) worker = (worker % 8) * (nWorkers / 8) + worker / 8;
   }
@@ -245,7 +247,13 @@ __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t 
 #pragma unroll
       for (int u = 0; u < UNROLL; u++) st16_dst<POLS>(a, d, off + u * ustride, acc[u]);
     };
-    if constexpr (ND > 0) {
+    if constexpr (ORDER == 3 && ND > 0) {
+      // measurement variant: stores interleaved across destinations
+#pragma unroll
+      for (int u = 0; u < UNROLL; u++)
+#pragma unroll
+        for (int d = 0; d < ND; d++) st16_dst<POLS>(a, d, off + u * ustride, acc[u]);
+    } else if constexpr (ND > 0) {
 #pragma unroll
       for (int d = 0; d < ND; d++) store_dst(d);
     } else {

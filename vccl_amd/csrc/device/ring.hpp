@@ -91,11 +91,16 @@ struct RingCtx {
     if (aborted()) return;
     if (nelem > 0) {
       // Operand order and memory policy: own input streamed once (nt), FIFO
-      // slots system-coherent write-through (sc0 sc1), own output plain.
+      // slots system-coherent write-through (sc0 sc1).  Own output: sc0 sc1
+      // when it is the only destination, nt beside a FIFO slot — the
+      // two-destination shape runs at 7.13 TB/s with one write-through and
+      // one nt destination, 6.0 with both write-through, 5.5 with both plain
+      // (tools/sweep_rc.py twodst, profiles/r03a; PMC traffic = algorithmic
+      // in every case, so the policy mix, not the bytes, sets the rate).
       constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
       constexpr int ND = (SEND ? 1 : 0) + (DST ? 1 : 0);
       constexpr int S0 = SRC ? VCCL_RING_SRC_POL : kSys, S1 = kSys;
-      constexpr int D0 = SEND ? kSys : kPlain, D1 = kPlain;
+      constexpr int D0 = kSys, D1 = kNT;
       constexpr int POLS = mkpol(S0, S1, S1, S1, D0, D1, D1, D1);
       RCArgs a;
       int s = 0, d = 0;

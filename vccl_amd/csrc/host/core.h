@@ -140,11 +140,19 @@ struct ncclComm {
   hipEvent_t joinEvent = nullptr;     // joins other streams into a fused group launch
   hipStream_t lastStream = nullptr;
   bool hasLastLaunch = false;         // lastLaunch/lastStream are valid
-  // the same ordering inside a stream capture (recorded in the graph)
-  hipEvent_t capEvent = nullptr;
-  unsigned long long capId = 0;
-  hipStream_t capLastStream = nullptr;
-  bool capHasLast = false;
+  // the same ordering inside each stream capture, keyed by capture id (two
+  // captures on one comm may interleave): events recorded in the
+  // graph, a small pool reused least-recently-used first (never destroyed
+  // while the comm lives — a graph may still reference one)
+  struct CapOrder {
+    unsigned long long id = 0;
+    bool used = false;
+    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;
+    bool has = false;
+  };
+  static constexpr int kMaxCaptures = 16;
+  std::vector<CapOrder> caps;         // most recently used first
   uint64_t fusedLaunches = 0;         // group launches that carried > 1 collective
   // CTA (workgroup) bounds of every collective launch: ncclConfig_t
   // minCTAs / maxCTAs or NCCL_MIN_CTAS / NCCL_MAX_CTAS (init.cc:1478-1540)

@@ -207,14 +207,37 @@ static ncclResult_t capture_state(hipStream_t s, CaptureState* cs) {
   cs->id = id;
   return ncclSuccess;
 }
+// The ordering state of capture `id`: comm->caps is a pool of kMaxCaptures
+// entries created at init (no HIP object is created during a capture); a new
+// id takes the least recently used entry.
+static void capture_entry(ncclComm* comm, unsigned long long id, bool create,
+                          ncclComm::CapOrder** out) {
+  *out = nullptr;
+  auto& caps = comm->caps;
+  for (size_t i = 0; i < caps.size(); i++) {
+    if (caps[i].used && caps[i].id == id) {
+      std::rotate(caps.begin(), caps.begin() + i, caps.begin() + i + 1);  // to the front
+      *out = &caps[0];
+      return;
+    }
+  }
+  if (!create || caps.empty()) return;
+  std::rotate(caps.begin(), caps.end() - 1, caps.end());  // the oldest entry, to the front
+  caps[0].id = id;
+  caps[0].used = true;
+  caps[0].last = nullptr;
+  caps[0].has = false;
+  *out = &caps[0];
+}
 // One capture query per call: stream_order fills `cs`, stream_mark and
 // stream_last_event reuse it (the capture state of s cannot change between
 // them — the caller holds the thread).
 static ncclResult_t stream_order(ncclComm* comm, hipStream_t s, CaptureState* cs) {
   NCCLCHECK(capture_state(s, cs));
   if (cs->active) {
-    if (comm->capHasLast && comm->capId == cs->id && comm->capLastStream != s)
-      HIPCHECK(hipStreamWaitEvent(s, comm->capEvent, 0));
+    ncclComm::CapOrder* c;
+    capture_entry(comm, cs->id, false, &c);
+    if (c && c->has && c->last != s) HIPCHECK(hipStreamWaitEvent(s, c->ev, 0));
     return ncclSuccess;
   }
   if (comm->hasLastLaunch && comm->lastStream != s)
@@ -223,10 +246,12 @@ static ncclResult_t stream_order(ncclComm* comm, hipStream_t s, CaptureState* cs
 }
 static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s, const CaptureState& cs) {
   if (cs.active) {
-    HIPCHECK(hipEventRecord(comm->capEvent, s));
-    comm->capId = cs.id;
-    comm->capLastStream = s;
-    comm->capHasLast = true;
+    ncclComm::CapOrder* c;
+    capture_entry(comm, cs.id, true, &c);
+    if (!c) return ncclInternalError;
+    HIPCHECK(hipEventRecord(c->ev, s));
+    c->last = s;
+    c->has = true;
     return ncclSuccess;
   }
   HIPCHECK(hipEventRecord(comm->lastLaunch, s));
@@ -236,7 +261,7 @@ static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s, const CaptureStat
 }
 // The event stream_mark just recorded on s (for joining other streams).
 static hipEvent_t stream_last_event(ncclComm* comm, const CaptureState& cs) {
-  return cs.active ? comm->capEvent : comm->lastLaunch;
+  return cs.active ? comm->caps[0].ev : comm->lastLaunch;
 }
 
 // ncclLaunchOneRank (onerank.cu:47-83): a copy, or the PreMulSum kernel.
@@ -284,17 +309,18 @@ struct CbdPlan {
   int64_t countLo, countMid, countHi;
   int64_t chunkLo, chunkMid, chunkHi;  // elements
 };
+// nThreads: maxThreads[RING][SIMPLE], i.e. NCCL_NTHREADS (tuning.cc:198-200;
+// the ring kernel's own block size here, comm->nThreads).
 static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
-                            int64_t slotBytes) {
+                            int64_t slotBytes, int64_t nThreads) {
   constexpr int64_t kMinTraffic = 16 << 10;         // enqueue.cc:528
-  constexpr int64_t kSimpleThreads = 512;          // maxThreads[RING][SIMPLE] (tuning.cc:198-200)
   constexpr int64_t kSimpleThreshold = 64;         // NCCL_SIMPLE_THREAD_THRESHOLD (comm.h:40)
   constexpr int64_t kGrain = 512;                  // ncclProtoGrainSize(SIMPLE) (device.h:290-295)
   auto divUp = [](int64_t a, int64_t b) { return (a + b - 1) / b; };
   const int64_t tpb = coll == kAllReduce ? 2 : nRanks;  // ncclFuncTrafficPerByte (enqueue.cc:67-74)
   const int64_t nBytes = eltSize * (coll == kAllReduce ? count : (int64_t)nRanks * count);
   int64_t nc = commChannels;                        // enqueue.cc:1921-1924
-  while (nBytes < nc * kSimpleThreads * kSimpleThreshold && nc >= 2) nc--;
+  while (nBytes < nc * nThreads * kSimpleThreshold && nc >= 2) nc--;
   const int64_t traffic = std::max(kMinTraffic, count * eltSize * tpb);
   const int64_t nMax = commChannels;
   const int64_t trafficPerChannel = std::max(kMinTraffic, traffic / std::min(nc, nMax));
@@ -369,7 +395,7 @@ static ncclResult_t launch_ring(const Task& t) {
   {
     const int64_t esz = t.coll == kAllGather ? 1 : type_size(t.datatype);
     const CbdPlan p = cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
-                                   comm->slotBytes);
+                                   comm->slotBytes, comm->nThreads);
     if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
       return ncclInternalError;
     w.channelLo = p.channelLo;
@@ -428,7 +454,7 @@ static int dev_coll(int coll) {
 // reduce-scatters' per-channel fold order (the ring's own, cbd_schedule).
 static CbdLite rs_cbd(const ncclComm* comm, const Task& t) {
   const CbdPlan p = cbd_schedule(kReduceScatter, (int64_t)t.count, type_size(t.datatype), comm->nRanks,
-                                 comm->nChannels, comm->slotBytes);
+                                 comm->nChannels, comm->slotBytes, comm->nThreads);
   return CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)t.count};
 }
 
@@ -470,13 +496,16 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   if (lines > comm->llLines) return ncclInternalError;
   const int kt = t.coll == kAllGather ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
-  // A bounded grid (<= VCCL_LL_MAX_BLOCKS 256-thread workgroups, each thread
-  // looping over lines): every rank's LL workgroups must be resident at once
-  // for the peers' spins to complete; 256 x 4 waves is 1/8 of a GPU's
-  // residency.  Tests that put 8 ranks on ONE GPU lower it.
+  // A bounded grid (256-thread workgroups, each thread looping over lines):
+  // one workgroup per 256 lines, within the comm's CTA bounds (minCTAs /
+  // maxCTAs, default 1 / 64), and never above VCCL_LL_MAX_BLOCKS (256): every
+  // rank's LL workgroups must be resident at once for the peers' spins to
+  // complete, so that co-residency cap is applied LAST (tests that
+  // put 8 ranks on ONE GPU lower it).
   const int maxBlocks = (int)std::max<int64_t>(1, param_int("LL_MAX_BLOCKS", 256));
-  int grid = (int)std::max<int64_t>(1, std::min<int64_t>((lines + 255) / 256, maxBlocks));
+  int grid = (int)std::max<int64_t>(1, (lines + 255) / 256);
   grid = std::max(std::min(grid, comm->maxCTAs), comm->minCTAs);
+  grid = std::max(1, std::min(grid, maxBlocks));
   const int coll = dev_coll(t.coll), devOp = t.coll == kAllGather ? OP_COPY : t.devOp;
   const hipError_t e = by_kernel_type(kt, [&]<int K>() { return ll_launch<K>(coll, devOp, w, grid, t.stream); });
   if (e != hipSuccess) {
@@ -518,7 +547,8 @@ static ncclResult_t launch_direct(const Task& t) {
     shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
     // the ring's partition of this bucket: phase 2 folds every element in the
     // order VCCL's ring all-reduce gives it on these channels (ar_chunk_of)
-    const CbdPlan p = cbd_schedule(kAllReduce, count, esz, n, comm->nChannels, comm->slotBytes);
+    const CbdPlan p = cbd_schedule(kAllReduce, count, esz, n, comm->nChannels, comm->slotBytes,
+                                   comm->nThreads);
     w.cbd = CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, count};
     w.arChunk = p.chunkLo;
   } else {
@@ -531,9 +561,11 @@ static ncclResult_t launch_direct(const Task& t) {
   w.nChunks = (int)((count + w.chunkElts - 1) / w.chunkElts);
   // Blocks of >= 16 KiB (one 512-thread x 2-pack hunk), at most the cap.
   const int64_t minBlk = (16 << 10) / esz;
-  int64_t nb = std::min<int64_t>((shard0 + minBlk - 1) / minBlk, comm->directMaxBlocks);
+  // CTA bounds first, then the co-residency caps (directMaxBlocks,
+  // kDirectMaxBlocks) last, so NCCL_MIN_CTAS cannot push past them.
+  int64_t nb = (shard0 + minBlk - 1) / minBlk;
   nb = std::max<int64_t>(std::min<int64_t>(nb, comm->maxCTAs), comm->minCTAs);
-  nb = std::max<int64_t>(1, std::min<int64_t>(nb, kDirectMaxBlocks));
+  nb = std::max<int64_t>(1, std::min<int64_t>({nb, (int64_t)comm->directMaxBlocks, (int64_t)kDirectMaxBlocks}));
   w.blkElts = align_up((shard0 + nb - 1) / nb, eltAlign);
   w.nBlocks = (int)((shard0 + w.blkElts - 1) / w.blkElts);
   w.regionBytes = comm->dRegionBytes;
@@ -931,14 +963,14 @@ extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count
 
 extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition(
     int coll, size_t count, ncclDataType_t datatype, int nRanks, int nChannels, size_t slotBytes,
-    int64_t* out) {
+    int nThreads, int64_t* out) {
   if (!out || coll < 0 || coll > 2 || type_size(datatype) < 1 || nRanks < 1 ||
-      nChannels < 1 || nChannels > kMaxChannels || count == 0 || slotBytes < 4096)
+      nChannels < 1 || nChannels > kMaxChannels || count == 0 || slotBytes < 4096 || nThreads < 64)
     return ncclInvalidArgument;
   const int c = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : kAllGather;
   const int64_t esz = c == kAllGather ? 1 : type_size(datatype);
   const int64_t cnt = c == kAllGather ? (int64_t)count * type_size(datatype) : (int64_t)count;
-  const CbdPlan p = cbd_schedule(c, cnt, esz, nRanks, nChannels, (int64_t)slotBytes);
+  const CbdPlan p = cbd_schedule(c, cnt, esz, nRanks, nChannels, (int64_t)slotBytes, nThreads);
   const int64_t v[8] = {p.channelLo, p.channelHi, p.countLo, p.countMid,
                         p.countHi,   p.chunkLo,   p.chunkMid, p.chunkHi};
   memcpy(out, v, sizeof(v));
@@ -946,13 +978,14 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition
 }
 
 extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingChunkOf(
-    size_t count, ncclDataType_t datatype, int nRanks, int nChannels, size_t slotBytes, size_t i,
-    int64_t* out) {
+    size_t count, ncclDataType_t datatype, int nRanks, int nChannels, size_t slotBytes, int nThreads,
+    size_t i, int64_t* out) {
   if (!out || type_size(datatype) < 1 || nRanks < 1 || nChannels < 1 || nChannels > kMaxChannels ||
-      count == 0 || i >= count || slotBytes < 4096)
+      count == 0 || i >= count || slotBytes < 4096 || nThreads < 64)
     return ncclInvalidArgument;
   const int64_t esz = type_size(datatype);
-  const CbdPlan p = cbd_schedule(kAllReduce, (int64_t)count, esz, nRanks, nChannels, (int64_t)slotBytes);
+  const CbdPlan p = cbd_schedule(kAllReduce, (int64_t)count, esz, nRanks, nChannels, (int64_t)slotBytes,
+                                 nThreads);
   const CbdLite cbd{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)count};
   int k;
   int64_t end;

@@ -89,8 +89,10 @@ static void free_resources(ncclComm* c) {
   if (c->errorFlag) (void)hipHostFree(c->errorFlag);
   if (c->lastLaunch) (void)hipEventDestroy(c->lastLaunch);
   if (c->joinEvent) (void)hipEventDestroy(c->joinEvent);
-  if (c->capEvent) (void)hipEventDestroy(c->capEvent);
-  c->joinEvent = c->capEvent = nullptr;
+  for (auto& cap : c->caps)
+    if (cap.ev) (void)hipEventDestroy(cap.ev);
+  c->caps.clear();
+  c->joinEvent = nullptr;
   c->fifoBuf = c->flagBuf = nullptr;
   c->devComm = nullptr;
   c->devChannels = nullptr;
@@ -184,7 +186,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   *c->errorFlag = 0;
   HIPCHECK(hipEventCreateWithFlags(&c->lastLaunch, hipEventDisableTiming));
   HIPCHECK(hipEventCreateWithFlags(&c->joinEvent, hipEventDisableTiming));
-  HIPCHECK(hipEventCreateWithFlags(&c->capEvent, hipEventDisableTiming));
+  c->caps.resize(ncclComm::kMaxCaptures);
+  for (auto& cap : c->caps) HIPCHECK(hipEventCreateWithFlags(&cap.ev, hipEventDisableTiming));
 
   PeerMap me{};
   me.pid = (int)getpid();

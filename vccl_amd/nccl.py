@@ -104,10 +104,11 @@ def lib() -> ctypes.CDLL:
         "vcclKernelTypeOf": [c_int, c_int],
         "vcclBootstrapAllGather": [ctypes.POINTER(ncclUniqueId), c_int, c_int, vp, c_size],
         "vcclCommSetFences": [vp, c_int],
-        "vcclRingPartition": [c_int, c_size, c_int, c_int, c_int, c_size,
+        "vcclRingPartition": [c_int, c_size, c_int, c_int, c_int, c_size, c_int,
                               ctypes.POINTER(ctypes.c_int64)],
         "vcclCommDebugSetEpochs": [vp, ctypes.c_uint32, ctypes.c_uint32],
-        "vcclRingChunkOf": [c_size, c_int, c_int, c_int, c_size, c_size, ctypes.POINTER(ctypes.c_int64)],
+        "vcclRingChunkOf": [c_size, c_int, c_int, c_int, c_size, c_int, c_size,
+                            ctypes.POINTER(ctypes.c_int64)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -171,21 +172,23 @@ def kernel_type_of(dev_op: int, dtype: int) -> int:
 
 
 def ring_partition(coll: int, count: int, dtype: int, nranks: int, nchannels: int,
-                   slot_bytes: int) -> tuple[int, ...]:
+                   slot_bytes: int, nthreads: int = 512) -> tuple[int, ...]:
     """vcclRingPartition: (channelLo, channelHi, countLo, countMid, countHi,
-    chunkLo, chunkMid, chunkHi) of the ring's cbd partition (host only)."""
+    chunkLo, chunkMid, chunkHi) of the ring's cbd partition (host only);
+    nthreads = NCCL_NTHREADS (the ring kernel's block size)."""
     out = (ctypes.c_int64 * 8)()
-    check(lib().vcclRingPartition(coll, count, dtype, nranks, nchannels, slot_bytes, out),
+    check(lib().vcclRingPartition(coll, count, dtype, nranks, nchannels, slot_bytes, nthreads, out),
           "vcclRingPartition")
     return tuple(out)
 
 
 def ring_chunk_of(count: int, dtype: int, nranks: int, nchannels: int, slot_bytes: int,
-                  i: int) -> tuple[int, int, int]:
+                  i: int, nthreads: int = 512) -> tuple[int, int, int]:
     """vcclRingChunkOf: (channel, ring chunk c, chunk end) of all-reduce
     element i on the ring's partition (the direct all-reduce's fold lookup)."""
     out = (ctypes.c_int64 * 3)()
-    check(lib().vcclRingChunkOf(count, dtype, nranks, nchannels, slot_bytes, i, out), "vcclRingChunkOf")
+    check(lib().vcclRingChunkOf(count, dtype, nranks, nchannels, slot_bytes, nthreads, i, out),
+          "vcclRingChunkOf")
     return tuple(out)
 
 
