@@ -1,0 +1,41 @@
+"""LL128-style line tearing probe on the GPU (tools/line_probe.hip).
+
+VCCL's LL128 trusts a 128-byte line's 15 data words once its flag word shows
+the step (src/device/prims_ll128.h:176-324).  The probe writes lines with sc0
+sc1 16-byte stores from one XCD and polls them from another, counting lines
+whose flag is visible before their data.  Both line sizes run (128 B as
+LL128, 64 B as a half-line variant); the counts are printed for DESIGN.md.
+The assertion is on the probe itself (every line checked, no timeout); the
+tear counts are the measurement.
+"""
+import ctypes
+import json
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("line_bytes", [128, 64])
+def test_line_tearing_probe(line_bytes):
+    L = ctypes.CDLL(os.path.join(ROOT, "vccl_amd", "lib", "libvccl_probe.so"))
+    L.vcclProbeLineTearing.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_double, ctypes.POINTER(ctypes.c_ulonglong)]
+    pairs, lines, iters = 64, 128, 4000
+    counts = (ctypes.c_ulonglong * 4)()
+    rc = L.vcclProbeLineTearing(pairs, lines, iters, line_bytes, 20.0, counts)
+    assert rc == 0, rc
+    checked, flag_first, data_ahead, timeouts = list(counts)
+    print(json.dumps({"line_bytes": line_bytes, "pairs": pairs, "lines_per_pair": lines,
+                      "iters": iters, "lines_checked": checked, "flag_before_data": flag_first,
+                      "data_ahead_of_flag": data_ahead, "timeouts": timeouts}))
+    assert timeouts == 0
+    assert checked == pairs * lines * iters
+    assert data_ahead == 0  # the writer waits for the reader's acknowledgement
