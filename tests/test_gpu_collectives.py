@@ -228,8 +228,9 @@ def test_multi_process_ranks(n, geom):
                    nthreads)
         _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot, ll_max,
                      direct_max, chunk, nthreads)
+        # every geometry fuses the group's runs (LL, direct or ring batches)
         fused = int(res[0]["launch_stats"][1])
-        assert (fused > 0) == (ll_max > 0), f"fused group launches: {fused} (LL max {ll_max})"
+        assert fused > 0, f"fused group launches: {fused}"
         for r in range(n):
             sent, recvd, conns = (int(v) for v in res[r]["net_stats"])
             if geom == "net":  # one send and one receive connection per channel
@@ -381,3 +382,48 @@ def test_initall_single_process_worker():
     import json
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["ok"], res
+
+
+@pytest.mark.parametrize("n,geom", [(2, "default"), (4, "test"), (4, "ring_only")])
+def test_group_zero_pattern(n, geom):
+    """a group of 16 x 8 MiB bf16 reduce-scatters (a ZeRO
+    bucket loop) launches ONCE, and a group of 8 mid-size fp32 all-reduces
+    once (vcclCommLaunchStats), each on the path the library picks for it —
+    the ring at 2 ranks and with NCCL_ALGO=Ring, the one-hop / two-shot
+    direct path at 4 ranks — and every output is bit-exact against the
+    oracle's fold in VCCL's ring order (tests/mp_group_worker.py)."""
+    from tests import mp_group_worker as G
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    if geom in ("test", "ring_only"):
+        env.update(TEST_GEOM)
+        nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+        if geom == "ring_only":
+            env["NCCL_ALGO"] = "Ring"
+    else:
+        for k in TEST_GEOM:
+            env.pop(k, None)
+        env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
+        nch, slot = _ring.n_channels(n), 512 << 10
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_group_worker.py"),
+                                   str(r), str(n), hexid, d], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
+    want = {"default": ("ring", "ring"), "test": ("direct", "direct"), "ring_only": ("ring", "ring")}[geom]
+    assert (str(res[0]["algo_rs"]), str(res[0]["algo_ar"])) == want
+    assert int(res[0]["fused"]) == 2, int(res[0]["fused"])  # one RS launch + one AR launch
+    for name, dt, count in G.GROUP_RS:
+        ins = [G.gen(name, dt, count, r) for r in range(n)]
+        exp = _ring.expected_reducescatter(0, dt, ins, nch, slot)
+        for r in range(n):
+            assert_bitexact(dt, res[r][name], exp[r], what=f"{name} n={n} {geom} rank {r}")
+    for name, dt, count in G.GROUP_AR:
+        ins = [G.gen(name, dt, count, r) for r in range(n)]
+        exp = _ring.expected_allreduce(0, dt, ins, nch, slot)
+        for r in range(n):
+            assert_bitexact(dt, res[r][name], exp, what=f"{name} n={n} {geom} rank {r}")

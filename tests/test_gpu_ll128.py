@@ -28,14 +28,19 @@ def test_line_tearing_probe(line_bytes):
     L = ctypes.CDLL(os.path.join(ROOT, "vccl_amd", "lib", "libvccl_probe.so"))
     L.vcclProbeLineTearing.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_double, ctypes.POINTER(ctypes.c_ulonglong)]
-    pairs, lines, iters = 64, 128, 4000
+    pairs, lines, iters = 64, 128, 20000
     counts = (ctypes.c_ulonglong * 4)()
     rc = L.vcclProbeLineTearing(pairs, lines, iters, line_bytes, 20.0, counts)
     assert rc == 0, rc
     checked, flag_first, data_ahead, timeouts = list(counts)
-    print(json.dumps({"line_bytes": line_bytes, "pairs": pairs, "lines_per_pair": lines,
-                      "iters": iters, "lines_checked": checked, "flag_before_data": flag_first,
-                      "data_ahead_of_flag": data_ahead, "timeouts": timeouts}))
+    rec = {"line_bytes": line_bytes, "pairs": pairs, "lines_per_pair": lines, "iters": iters,
+           "lines_checked": checked, "flag_before_data": flag_first,
+           "data_ahead_of_flag": data_ahead, "timeouts": timeouts}
+    print(json.dumps(rec))
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"line_probe_{line_bytes}.json"), "w") as f:
+        json.dump(rec, f)
     assert timeouts == 0
     assert checked == pairs * lines * iters
     assert data_ahead == 0  # the writer waits for the reader's acknowledgement

@@ -94,13 +94,53 @@ __host__ __device__ __forceinline__ int64_t direct_shard_elts(int64_t cc, int n,
   return ((cc + n - 1) / n + eltAlign - 1) / eltAlign * eltAlign;
 }
 
-__host__ __device__ __forceinline__ size_t direct_region_off(int phase, int src, int nRanks,
+// Inbox: [2 phases][2 parities][nRanks sources][region]; flags likewise.
+// The all-reduce double-buffers its chunks by parity (direct.hpp); the
+// one-hop reduce-scatter / all-gather use parity 0.
+constexpr int kDirectInboxRegions = 4;  // regions per source: phases x parities
+__host__ __device__ __forceinline__ size_t direct_region_off(int phase, int parity, int src, int nRanks,
                                                              int64_t regionBytes) {
-  return ((size_t)phase * nRanks + src) * (size_t)regionBytes;
+  return (((size_t)phase * 2 + parity) * nRanks + src) * (size_t)regionBytes;
 }
-__host__ __device__ __forceinline__ size_t direct_flag_off(int phase, int src, int b) {
-  return (((size_t)phase * kDirectMaxRanks + src) * kDirectMaxBlocks + b) * kDirectFlagStride;
+__host__ __device__ __forceinline__ size_t direct_flag_off(int phase, int parity, int src, int b) {
+  return ((((size_t)phase * 2 + parity) * kDirectMaxRanks + src) * kDirectMaxBlocks + b) *
+         kDirectFlagStride;
 }
-constexpr size_t kDirectFlagBytes = (size_t)2 * kDirectMaxRanks * kDirectMaxBlocks * kDirectFlagStride;
+constexpr size_t kDirectFlagBytes =
+    (size_t)kDirectInboxRegions * kDirectMaxRanks * kDirectMaxBlocks * kDirectFlagStride;
+
+// Group aggregation of direct calls (DirectBatch: part 0 in `w`, the others
+// as DirectPart — what differs per call), run in order by one launch.
+constexpr int kDirectMaxWorks = 16;
+struct DirectPart {
+  const void* sendbuff;
+  void* recvbuff;
+  uint64_t count;
+  int nChunks;
+  int pad;
+  int64_t chunkElts, blkElts;
+  CbdLite cbd;
+  int64_t arChunk;
+};
+struct DirectBatch {
+  DirectWork w;
+  int nParts;
+  DirectPart more[kDirectMaxWorks - 1];
+};
+__host__ __device__ inline DirectPart direct_part_of(const DirectWork& w) {
+  return DirectPart{w.sendbuff, w.recvbuff, w.count, w.nChunks, 0, w.chunkElts, w.blkElts, w.cbd,
+                    w.arChunk};
+}
+__host__ __device__ inline DirectWork direct_work_with(DirectWork w, const DirectPart& p) {
+  w.sendbuff = p.sendbuff;
+  w.recvbuff = p.recvbuff;
+  w.count = p.count;
+  w.nChunks = p.nChunks;
+  w.chunkElts = p.chunkElts;
+  w.blkElts = p.blkElts;
+  w.cbd = p.cbd;
+  w.arChunk = p.arChunk;
+  return w;
+}
 
 }  // namespace vccl

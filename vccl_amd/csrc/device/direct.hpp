@@ -237,13 +237,13 @@ __device__ __forceinline__ void direct_bcast(const char* src, char* const (&dst)
   }
 }
 
-// Wait until every peer's flag (phase, peer, b) in MY flag array equals e.
-// Lane p of wave 0 polls peer p; bounded like RingCtx::spin_ge.
+// Wait until every peer's flag (phase, parity, peer, b) in MY flag array
+// equals e.  Lane p of wave 0 polls peer p; bounded like RingCtx::spin_ge.
 __device__ __forceinline__ bool direct_wait(const DirectWork& w, const char* myFlags, int phase,
-                                            int b, uint32_t e, int* shFail) {
+                                            int parity, int b, uint32_t e, int* shFail) {
   const int t = threadIdx.x;
   if (t < w.nRanks && t != w.rank) {
-    const uint32_t* f = (const uint32_t*)(myFlags + direct_flag_off(phase, t, b));
+    const uint32_t* f = (const uint32_t*)(myFlags + direct_flag_off(phase, parity, t, b));
     const DevComm* comm = w.comm;
     uint64_t spins = 0, start = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
@@ -268,48 +268,94 @@ __device__ __forceinline__ bool direct_wait(const DirectWork& w, const char* myF
   return *shFail == 0;
 }
 
-// Every storing wave drains, then lane k of wave 0 raises flag (phase, me, b)
-// at peer (me + k) mod n.
+// Every storing wave drains, then lane k of wave 0 raises flag (phase,
+// parity, me, b) at peer (me + k) mod n.
 __device__ __forceinline__ void direct_post(const DirectWork& w, const DirectPeers& P, int phase,
-                                            int b, uint32_t e) {
+                                            int parity, int b, uint32_t e) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int k = threadIdx.x;
   if (k >= 1 && k < w.nRanks) {
     const int p = w.rank + k < w.nRanks ? w.rank + k : w.rank + k - w.nRanks;
-    __hip_atomic_store((uint32_t*)(P.flags[p] + direct_flag_off(phase, w.rank, b)), e,
+    __hip_atomic_store((uint32_t*)(P.flags[p] + direct_flag_off(phase, parity, w.rank, b)), e,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
+// ---------------------------------------------------------------- all-reduce
+// One call (one part of a batch).  `e` carries the epoch across chunks and
+// parts: chunk c raises the (c+1)-th successor of the value it enters with
+// (epoch_after: never 0, the never-written flag value); the batch's last
+// workgroup stores the final one back (epoch_retire: graph-replay safe).
+//
+// Chunks are double-buffered by parity c & 1 (inbox regions and flags), and
+// chunk c+1's scatter is issued right after chunk c's fold, before chunk c's
+// gather: the gather (local inbox -> output copies) overlaps the next chunk's
+// outgoing traffic.  Reuse of parity p = (c+1) & 1 is safe: region (0, me)
+// at peer q held chunk c-1, which q folded before raising flag (1, *, c-1)
+// — awaited by this workgroup in the previous iteration; region (1, o) of
+// parity p at a reader is rewritten by o for chunk c+2 only after o received
+// the reader's scatter of chunk c+2, which the reader issues after its gather
+// of chunk c.  Per-parity flags: a flag of parity p is raised again (chunk
+// c+2) only after its reader awaited chunk c's value (same chains).
 template <class Fn>
-__device__ void direct_allreduce(const DirectWork& w) {
+__device__ void direct_allreduce_part(const DirectWork& w, uint32_t& e, int& shFail) {
   using T = typename Fn::EltType;
-  __shared__ int shFail;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
-  // Flag values: chunk c of this call raises the (c+1)-th successor of the
-  // stored epoch (epoch_after: never 0, the never-written flag value); the
-  // last workgroup stores the final one back (graph-replay safe, epoch_next).
-  uint32_t e = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const DirectPeers& P = *w.peers;
   const int n = w.nRanks, me = w.rank, b = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
+  constexpr int64_t esz = (int64_t)sizeof(T);
   char* myBuf = P.buf[me];
   const char* myFlags = P.flags[me];
-  if (tid == 0) shFail = 0;
-  __syncthreads();
+  const int64_t inOff = (int64_t)b * w.blkElts * esz;  // block offset in a region
 
+  auto chunk_geom = [&](int c, int64_t* c0, int64_t* cc, int64_t* shardElts) {
+    *c0 = (int64_t)c * w.chunkElts;
+    const int64_t rest = (int64_t)w.count - *c0;
+    *cc = rest < w.chunkElts ? rest : w.chunkElts;
+    *shardElts = direct_shard_elts(*cc, n, eltAlign);
+  };
+  auto block_of = [&](int64_t cc, int64_t shardElts, int o, int64_t* off, int64_t* len) {
+    int64_t shardEnd = (int64_t)(o + 1) * shardElts;
+    shardEnd = shardEnd < cc ? shardEnd : cc;
+    const int64_t lo = (int64_t)o * shardElts + (int64_t)b * w.blkElts;
+    const int64_t hi = lo + w.blkElts < shardEnd ? lo + w.blkElts : shardEnd;
+    *off = lo;
+    *len = hi > lo ? hi - lo : 0;
+  };
+  // Phase 1: scatter my blocks of chunk c's foreign shards into their
+  // owners' inboxes (parity c & 1).  Workgroup b starts at peer offset
+  // 1 + b mod (n-1), so a rank's workgroups feed all n-1 outgoing links.
+  auto scatter = [&](int c) {
+    int64_t c0, cc, shardElts;
+    chunk_geom(c, &c0, &cc, &shardElts);
+    const char* in = (const char*)w.sendbuff + c0 * esz;
+    for (int i = 0; i < n - 1; i++) {
+      const int k = 1 + (b + i) % (n - 1);
+      const int p = me + k < n ? me + k : me + k - n;
+      int64_t off, len;
+      block_of(cc, shardElts, p, &off, &len);
+      const char* s[kDirectMaxRanks] = {in + off * esz};
+      char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, c & 1, me, n, w.regionBytes) + inOff};
+      direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
+    }
+  };
+
+  if (w.nChunks <= 0) return;
+  uint32_t eCur = epoch_after(e);
+  if (!shFail) {
+    scatter(0);
+    direct_post(w, P, 0, 0, b, eCur);
+  }
   for (int c = 0; c < w.nChunks; c++) {
-    e = epoch_after(e);
-    if (shFail) continue;  // keep stepping e: every workgroup retires the same value
-    const int64_t c0 = (int64_t)c * w.chunkElts;
-    const int64_t rest = (int64_t)w.count - c0;
-    const int64_t cc = rest < w.chunkElts ? rest : w.chunkElts;
-    const int64_t shardElts = direct_shard_elts(cc, n, eltAlign);
-    const char* in = (const char*)w.sendbuff + c0 * (int64_t)sizeof(T);
-    char* out = (char*)w.recvbuff + c0 * (int64_t)sizeof(T);
-    const int64_t inOff = (int64_t)b * w.blkElts * (int64_t)sizeof(T);  // block offset in a region
+    const int par = c & 1;
+    const uint32_t eNext = epoch_after(eCur);
+    int64_t c0, cc, shardElts;
+    chunk_geom(c, &c0, &cc, &shardElts);
+    const char* in = (const char*)w.sendbuff + c0 * esz;
+    char* out = (char*)w.recvbuff + c0 * esz;
     // Block offsets are 16-byte multiples, so every block of `out` shares the
     // chunk base's misalignment (the inbox regions are 16-byte aligned).
 #ifdef VCCL_DIRECT_MIS_ELEMENTS
@@ -317,37 +363,13 @@ __device__ void direct_allreduce(const DirectWork& w) {
 #else
     const bool outMis = ((uintptr_t)out & 15) != 0;
 #endif
-    auto block_of = [&](int o, int64_t* off, int64_t* len) {
-      int64_t shardEnd = (int64_t)(o + 1) * shardElts;
-      shardEnd = shardEnd < cc ? shardEnd : cc;
-      int64_t lo = (int64_t)o * shardElts + (int64_t)b * w.blkElts;
-      int64_t hi = lo + w.blkElts < shardEnd ? lo + w.blkElts : shardEnd;
-      *off = lo;
-      *len = hi > lo ? hi - lo : 0;
-    };
-
-    // Phase 1: scatter my blocks of the foreign shards into their owners'
-    // inboxes.  Workgroup b starts at peer offset 1 + b mod (n-1), so at any
-    // moment the workgroups of a rank feed all n-1 outgoing links, not one.
-    for (int i = 0; i < n - 1; i++) {
-      int k = 1 + (b + i) % (n - 1);
-      const int p = me + k < n ? me + k : me + k - n;
-      int64_t off, len;
-      block_of(p, &off, &len);
-      const char* s[kDirectMaxRanks] = {in + off * (int64_t)sizeof(T)};
-      char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + inOff};
-      direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
-    }
-    direct_post(w, P, 0, b, e);
-
     // Phase 2: fold my shard's block b in the ring's order; send it out.
-    if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
+    if (!shFail && direct_wait(w, myFlags, 0, par, b, eCur, &shFail)) {
       int64_t off, len;
-      block_of(me, &off, &len);
+      block_of(cc, shardElts, me, &off, &len);
       // Each wave takes a contiguous span of the block (whole 16-byte packs)
       // and walks it ring chunk by ring chunk: a chunk boundary splits one
       // wave's pass, not the workgroup's.
-      constexpr int64_t esz = (int64_t)sizeof(T);
       // wave index made provably wave-uniform: everything derived from it
       // (span, chunk lookup, operand pointers) stays in SGPRs
       const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
@@ -365,7 +387,7 @@ __device__ void direct_allreduce(const DirectWork& w) {
         // input where the position is mine, else my inbox region of that
         // rank) -> my output (staged in my own aligned region (1, me) when
         // the output is off 16-byte alignment, copied out in phase 3).
-        char* res = outMis ? myBuf + direct_region_off(1, me, n, w.regionBytes) + inOff + cur * esz
+        char* res = outMis ? myBuf + direct_region_off(1, par, me, n, w.regionBytes) + inOff + cur * esz
                            : out + (off + cur) * esz;
         {
           const char* s[kDirectMaxRanks];
@@ -377,7 +399,7 @@ __device__ void direct_allreduce(const DirectWork& w) {
             pos = pos >= n ? pos - n : pos;
             const int q = j < n ? __builtin_amdgcn_readfirstlane(R[pos]) : me;
             s[j] = q == me ? in + (off + cur) * esz
-                           : myBuf + direct_region_off(0, q, n, w.regionBytes) + inOff + cur * esz;
+                           : myBuf + direct_region_off(0, par, q, n, w.regionBytes) + inOff + cur * esz;
           }
           direct_rc<Fn, kDirectUnroll, kSys, kPlain, kPlain>(fn, s, n, w.preOp ? n : 0, true, d, 1,
                                                              end - cur, lane, 64);
@@ -391,30 +413,36 @@ __device__ void direct_allreduce(const DirectWork& w) {
 #pragma unroll
           for (int j = 0; j < kDirectMaxRanks; j++) {
             const int dst = me + j + 1 < n ? me + j + 1 : me + j + 1 - n;
-            d[j] = j < n - 1 ? P.buf[dst] + direct_region_off(1, me, n, w.regionBytes) + inOff + cur * esz
-                             : nullptr;
+            d[j] = j < n - 1
+                       ? P.buf[dst] + direct_region_off(1, par, me, n, w.regionBytes) + inOff + cur * esz
+                       : nullptr;
           }
           direct_bcast<kDirectCopyUnroll>(s[0], d, n - 1, (end - cur) * esz, lane, 64);
         }
         cur = end;
       }
     }
-    direct_post(w, P, 1, b, e);
-
+    if (!shFail) direct_post(w, P, 1, par, b, eCur);
+    // Chunk c+1's scatter before chunk c's gather (see above).
+    if (c + 1 < w.nChunks && !shFail) {
+      scatter(c + 1);
+      direct_post(w, P, 0, par ^ 1, b, eNext);
+    }
     // Phase 3: gather the other owners' reduced blocks (and my own, if staged).
-    if (direct_wait(w, myFlags, 1, b, e, &shFail)) {
+    if (!shFail && direct_wait(w, myFlags, 1, par, b, eCur, &shFail)) {
       for (int k = outMis ? 0 : 1; k < n; k++) {
         const int o = me + k < n ? me + k : me + k - n;
         int64_t off, len;
-        block_of(o, &off, &len);
-        const char* s[kDirectMaxRanks] = {myBuf + direct_region_off(1, o, n, w.regionBytes) + inOff};
-        char* d[kDirectMaxRanks] = {out + off * (int64_t)sizeof(T)};
+        block_of(cc, shardElts, o, &off, &len);
+        const char* s[kDirectMaxRanks] = {myBuf + direct_region_off(1, par, o, n, w.regionBytes) + inOff};
+        char* d[kDirectMaxRanks] = {out + off * esz};
         direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
       }
     }
-    __syncthreads();  // the region reads of this chunk precede the next chunk's posts
+    __syncthreads();  // this chunk's region reads precede later posts
+    e = eCur;
+    eCur = eNext;
   }
-  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
 }
 
 // ------------------------------------------------------------ reduce-scatter
@@ -432,13 +460,12 @@ __device__ void direct_allreduce(const DirectWork& w) {
 //            has consumed what I wrote into it, so the next chunk (or call)
 //            may overwrite region (0, me) there.
 // count = recvcount; shards are the n blocks of the input (stride count).
+// Regions and flags of parity 0 only.
 template <class Fn>
-__device__ void direct_reducescatter(const DirectWork& w) {
+__device__ void direct_reducescatter_part(const DirectWork& w, uint32_t& e, int& shFail) {
   using T = typename Fn::EltType;
   constexpr int64_t esz = (int64_t)sizeof(T);
-  __shared__ int shFail;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
-  uint32_t e = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const DirectPeers& P = *w.peers;
   const int n = w.nRanks, me = w.rank, b = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -447,8 +474,6 @@ __device__ void direct_reducescatter(const DirectWork& w) {
   const char* myFlags = P.flags[me];
   const char* in = (const char*)w.sendbuff;
   char* out = (char*)w.recvbuff;
-  if (tid == 0) shFail = 0;
-  __syncthreads();
   for (int c = 0; c < w.nChunks; c++) {
     e = epoch_after(e);
     if (shFail) continue;
@@ -463,12 +488,12 @@ __device__ void direct_reducescatter(const DirectWork& w) {
       const int k = 1 + (b + i) % (n - 1);
       const int p = me + k < n ? me + k : me + k - n;
       const char* s[kDirectMaxRanks] = {in + ((int64_t)p * count + lo) * esz};
-      char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + rOff};
+      char* d[kDirectMaxRanks] = {P.buf[p] + direct_region_off(0, 0, me, n, w.regionBytes) + rOff};
       direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
     }
-    direct_post(w, P, 0, b, e);
+    direct_post(w, P, 0, 0, b, e);
     // Phase 2: fold per channel part in its ring's order.
-    if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
+    if (direct_wait(w, myFlags, 0, 0, b, e, &shFail)) {
       for (int64_t cur = lo; cur < hi;) {
         int64_t end;
         const int ch = cbd_channel_of(w.cbd, cur, &end);
@@ -481,18 +506,17 @@ __device__ void direct_reducescatter(const DirectWork& w) {
         for (int j = 0; j < kDirectMaxRanks; j++) {
           const int q = j < n ? order[j] : me;
           s[j] = q == me ? in + ((int64_t)me * count + cur) * esz
-                         : myBuf + direct_region_off(0, q, n, w.regionBytes) + ro;
+                         : myBuf + direct_region_off(0, 0, q, n, w.regionBytes) + ro;
         }
         direct_rc<Fn, kDirectUnroll, kSys, kSys, kSys>(fn, s, n, w.preOp ? n : 0, true, d, 1,
-                                                           end - cur, tid, nt);
+                                                       end - cur, tid, nt);
         cur = end;
       }
     }
-    direct_post(w, P, 1, b, e);
+    direct_post(w, P, 1, 0, b, e);
     // Phase 3: the peers' acknowledgements for this chunk.
-    (void)direct_wait(w, myFlags, 1, b, e, &shFail);
+    (void)direct_wait(w, myFlags, 1, 0, b, e, &shFail);
   }
-  epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
 }
 
 // ---------------------------------------------------------------- all-gather
@@ -509,12 +533,10 @@ __device__ void direct_reducescatter(const DirectWork& w) {
 // a peer that finished the previous call may start this one while I still
 // read (1, *) regions of a direct all-reduce's phase 3, never (0, *) ones
 // (its all-reduce could only finish after my phase-2 post, i.e. after my
-// last read of (0, *)).
-__device__ __forceinline__ void direct_allgather(const DirectWork& w) {
+// last read of (0, *)).  Regions and flags of parity 0 only.
+__device__ __forceinline__ void direct_allgather_part(const DirectWork& w, uint32_t& e, int& shFail) {
   using Fn = FnCopy<uint8_t>;
   const Fn fn(0);
-  __shared__ int shFail;
-  uint32_t e = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const DirectPeers& P = *w.peers;
   const int n = w.nRanks, me = w.rank, b = blockIdx.x;
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -523,8 +545,6 @@ __device__ __forceinline__ void direct_allgather(const DirectWork& w) {
   const char* myFlags = P.flags[me];
   const char* in = (const char*)w.sendbuff;
   char* out = (char*)w.recvbuff;
-  if (tid == 0) shFail = 0;
-  __syncthreads();
   for (int c = 0; c < w.nChunks; c++) {
     e = epoch_after(e);
     if (shFail) continue;
@@ -541,25 +561,40 @@ __device__ __forceinline__ void direct_allgather(const DirectWork& w) {
 #pragma unroll
       for (int j = 0; j < kDirectMaxRanks; j++) {
         const int p = me + 1 + j < n ? me + 1 + j : me + 1 + j - n;
-        d[j] = j < n - 1 ? P.buf[p] + direct_region_off(0, me, n, w.regionBytes) + rOff : nullptr;
+        d[j] = j < n - 1 ? P.buf[p] + direct_region_off(0, 0, me, n, w.regionBytes) + rOff : nullptr;
       }
       direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, n - 1, len, tid, nt);
     }
-    direct_post(w, P, 0, b, e);
+    direct_post(w, P, 0, 0, b, e);
     // Phase 2: gather every rank's block b into the output.
-    if (direct_wait(w, myFlags, 0, b, e, &shFail)) {
+    if (direct_wait(w, myFlags, 0, 0, b, e, &shFail)) {
       for (int k = 0; k < n; k++) {
         const int o = me + k < n ? me + k : me + k - n;
         const char* s[kDirectMaxRanks] = {o == me ? in + lo
-                                                  : myBuf + direct_region_off(0, o, n, w.regionBytes) + rOff};
+                                                  : myBuf + direct_region_off(0, 0, o, n, w.regionBytes) + rOff};
         char* d[kDirectMaxRanks] = {out + (int64_t)o * count + lo};
         if (o == me && s[0] == d[0]) continue;  // in place: my block is already there
         direct_rc<Fn, kDirectCopyUnroll, kSys, kSys, kSys>(fn, s, 1, 0, false, d, 1, len, tid, nt);
       }
     }
-    direct_post(w, P, 1, b, e);
-    (void)direct_wait(w, myFlags, 1, b, e, &shFail);
+    direct_post(w, P, 1, 0, b, e);
+    (void)direct_wait(w, myFlags, 1, 0, b, e, &shFail);
   }
+}
+
+// A batch (group aggregation, DirectBatch): the parts in order, one epoch
+// sequence, retired once by the last workgroup.  Every rank launches the
+// same grid (the largest part's block count); a workgroup past a part's
+// blocks moves nothing but still raises and awaits its namesakes' flags.
+template <class Body>
+__device__ __forceinline__ void direct_batch(const DirectBatch& bt, Body body) {
+  __shared__ int shFail;
+  const DirectWork& w = bt.w;
+  uint32_t e = __hip_atomic_load(&w.comm->dEpoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) shFail = 0;
+  __syncthreads();
+  body(w, e, shFail);
+  for (int i = 1; i < bt.nParts; i++) body(direct_work_with(w, bt.more[i - 1]), e, shFail);
   epoch_retire(&w.comm->dEpoch, &w.comm->dDone, e);
 }
 

@@ -36,7 +36,18 @@ template <class Fn>
 constexpr int ring_unroll() { return IsF8<typename Fn::EltType>::value ? 2 : kRingUnroll; }
 
 template <int COLL, class Fn, int UNROLL>
-__global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingWork w) {
+__device__ __forceinline__ void ring_run(RingCtx& r, const Fn& fn, const RingWork& w) {
+  if constexpr (COLL == kCollAllReduce) ring_allreduce<Fn, UNROLL>(r, fn, w, blockIdx.x);
+  else if constexpr (COLL == kCollReduceScatter) ring_reducescatter<Fn, UNROLL>(r, fn, w, blockIdx.x);
+  else ring_allgather<UNROLL>(r, w, blockIdx.x);
+}
+
+// One launch = 1 .. kRingMaxWorks calls (RingBatch, group aggregation): the
+// channel workgroup runs them in order.  The kernel argument is read through
+// scalar loads at any part index (no private copy).
+template <int COLL, class Fn, int UNROLL>
+__global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
+  const RingWork& w = b.w;
   __shared__ int shAbort;
   if (threadIdx.x == 0) shAbort = 0;
   __syncthreads();
@@ -51,9 +62,8 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingWork w) {
   r.slotBytes = w.slotBytes;
   r.shAbort = &shAbort;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
-  if constexpr (COLL == kCollAllReduce) ring_allreduce<Fn, UNROLL>(r, fn, w, blockIdx.x);
-  else if constexpr (COLL == kCollReduceScatter) ring_reducescatter<Fn, UNROLL>(r, fn, w, blockIdx.x);
-  else ring_allgather<UNROLL>(r, w, blockIdx.x);
+  ring_run<COLL, Fn, UNROLL>(r, fn, w);
+  for (int i = 1; i < b.nParts; i++) ring_run<COLL, Fn, UNROLL>(r, fn, ring_work_with(w, b.more[i - 1]));
   __syncthreads();
   if (threadIdx.x == 0) {
     ch->recvStep = r.recvStep;
@@ -62,11 +72,11 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingWork w) {
 }
 
 template <>
-hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingWork& w, int nthreads,
+hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingBatch& w, int nthreads,
                                 hipStream_t stream) {
   using T = typename KTypeOf<VCCL_KT>::T;
   hipError_t err = hipErrorInvalidValue;
-  dim3 grid(w.nChannels), block(nthreads);
+  dim3 grid(w.w.nChannels), block(nthreads);
   if (coll == kCollAllGather) {
     if constexpr (VCCL_KT == K_U8) {
       hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, kRingUnroll>), grid, block, 0,
@@ -126,24 +136,25 @@ hipError_t ll_launch<VCCL_KT>(int coll, int devOp, const LLWork& w, int grid, hi
 
 #elif VCCL_PART == 2
 template <class Fn>
-__global__ __launch_bounds__(kDirectThreads) void k_direct_allreduce(DirectWork w) {
-  direct_allreduce<Fn>(w);
+__global__ __launch_bounds__(kDirectThreads) void k_direct_allreduce(DirectBatch b) {
+  direct_batch(b, [](const DirectWork& w, uint32_t& e, int& f) { direct_allreduce_part<Fn>(w, e, f); });
 }
 template <class Fn>
-__global__ __launch_bounds__(kDirectThreads) void k_direct_reducescatter(DirectWork w) {
-  direct_reducescatter<Fn>(w);
+__global__ __launch_bounds__(kDirectThreads) void k_direct_reducescatter(DirectBatch b) {
+  direct_batch(b, [](const DirectWork& w, uint32_t& e, int& f) { direct_reducescatter_part<Fn>(w, e, f); });
 }
 template <int K>  // instantiated in the K_U8 unit only (byte copies)
-__global__ __launch_bounds__(kDirectThreads) void k_direct_allgather(DirectWork w) {
-  direct_allgather(w);
+__global__ __launch_bounds__(kDirectThreads) void k_direct_allgather(DirectBatch b) {
+  direct_batch(b, [](const DirectWork& w, uint32_t& e, int& f) { direct_allgather_part(w, e, f); });
 }
 
 template <>
-hipError_t direct_launch<VCCL_KT>(int coll, int devOp, const DirectWork& w, hipStream_t stream) {
+hipError_t direct_launch<VCCL_KT>(int coll, int devOp, const DirectBatch& b, hipStream_t stream) {
   using T = typename KTypeOf<VCCL_KT>::T;
+  const dim3 grid(b.w.nBlocks), block(kDirectThreads);
   if (coll == kCollAllGather) {
     if constexpr (VCCL_KT == K_U8) {
-      hipLaunchKernelGGL(k_direct_allgather<K_U8>, dim3(w.nBlocks), dim3(kDirectThreads), 0, stream, w);
+      hipLaunchKernelGGL(k_direct_allgather<K_U8>, grid, block, 0, stream, b);
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
@@ -152,10 +163,9 @@ hipError_t direct_launch<VCCL_KT>(int coll, int devOp, const DirectWork& w, hipS
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
       if (coll == kCollAllReduce)
-        hipLaunchKernelGGL((k_direct_allreduce<Fn>), dim3(w.nBlocks), dim3(kDirectThreads), 0, stream, w);
+        hipLaunchKernelGGL((k_direct_allreduce<Fn>), grid, block, 0, stream, b);
       else
-        hipLaunchKernelGGL((k_direct_reducescatter<Fn>), dim3(w.nBlocks), dim3(kDirectThreads), 0,
-                           stream, w);
+        hipLaunchKernelGGL((k_direct_reducescatter<Fn>), grid, block, 0, stream, b);
       err = hipGetLastError();
     }
   });

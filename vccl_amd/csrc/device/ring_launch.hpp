@@ -20,8 +20,9 @@ enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2 };
 constexpr int kRingUnroll = VCCL_RING_UNROLL;
 constexpr int kRingMaxThreads = 512;  // k_ring launch bound (ring_kernels.hip)
 
+// w.w.nChannels workgroups (the largest part's channelHi + 1).
 template <int K>
-hipError_t ring_launch(int coll, int devOp, const RingWork& w, int nthreads, hipStream_t stream);
+hipError_t ring_launch(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream);
 
 // One-hop LL collectives (ll.hpp): 256-thread workgroups, `grid` of them.
 // All-gather only in the K_U8 unit (byte copies).
@@ -29,9 +30,10 @@ template <int K>
 hipError_t ll_launch(int coll, int devOp, const LLWork& w, int grid, hipStream_t stream);
 
 // Direct collectives over the full mesh (direct.hpp): two-shot all-reduce,
-// one-hop reduce-scatter / all-gather; w.nBlocks workgroups of
-// kDirectThreads threads.  All-gather only in the K_U8 unit.
+// one-hop reduce-scatter / all-gather, 1 .. kDirectMaxWorks calls per launch;
+// b.w.nBlocks workgroups (the largest part's) of kDirectThreads threads.
+// All-gather only in the K_U8 unit.
 template <int K>
-hipError_t direct_launch(int coll, int devOp, const DirectWork& w, hipStream_t stream);
+hipError_t direct_launch(int coll, int devOp, const DirectBatch& b, hipStream_t stream);
 
 }  // namespace vccl

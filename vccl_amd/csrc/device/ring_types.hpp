@@ -160,4 +160,44 @@ struct RingWork {
   int64_t chunkLo, chunkMid, chunkHi;
 };
 
+// Group aggregation (the reference's planner packing a group's collectives
+// into one plan, enqueue.cc:352-508 / :518-769, run by one kernel over its
+// work batch, common.h:260-293): one ring launch carries up to kRingMaxWorks
+// calls of one comm with the same collective, type and op — part 0 in `w`,
+// the others as RingPart (what differs per call).  Every channel workgroup
+// runs the parts in order on its ring, so the FIFO step sequence is the same
+// on every rank; a channel outside a part's [channelLo, channelHi] skips it.
+constexpr int kRingMaxWorks = 16;
+struct RingPart {
+  const void* sendbuff;
+  void* recvbuff;
+  uint64_t count;
+  int channelLo, channelHi;
+  int64_t countLo, countMid, countHi;
+  int64_t chunkLo, chunkMid, chunkHi;
+};
+struct RingBatch {
+  RingWork w;                        // part 0 and everything the parts share
+  int nParts;                        // 1 .. kRingMaxWorks
+  RingPart more[kRingMaxWorks - 1];  // parts 1 .. nParts-1
+};
+__host__ __device__ inline RingPart ring_part_of(const RingWork& w) {
+  return RingPart{w.sendbuff, w.recvbuff, w.count, w.channelLo, w.channelHi, w.countLo,
+                  w.countMid, w.countHi, w.chunkLo, w.chunkMid, w.chunkHi};
+}
+__host__ __device__ inline RingWork ring_work_with(RingWork w, const RingPart& p) {
+  w.sendbuff = p.sendbuff;
+  w.recvbuff = p.recvbuff;
+  w.count = p.count;
+  w.channelLo = p.channelLo;
+  w.channelHi = p.channelHi;
+  w.countLo = p.countLo;
+  w.countMid = p.countMid;
+  w.countHi = p.countHi;
+  w.chunkLo = p.chunkLo;
+  w.chunkMid = p.chunkMid;
+  w.chunkHi = p.chunkHi;
+  return w;
+}
+
 }  // namespace vccl

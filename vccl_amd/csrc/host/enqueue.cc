@@ -368,7 +368,8 @@ static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks
   return p;
 }
 
-static ncclResult_t launch_ring(const Task& t) {
+// The ring work of one call (its kernel element type and device op too).
+static ncclResult_t ring_work_of(const Task& t, RingWork* out, int* ktOut, int* devOpOut) {
   ncclComm* comm = t.comm;
   RingWork w{};
   w.comm = comm->devComm;
@@ -392,35 +393,57 @@ static ncclResult_t launch_ring(const Task& t) {
   }
   w.redArgPtr = t.argPtr;  // ncclScalarDevice: dereferenced by the kernel (nccl.h.in:255-262)
   w.redArgBytes = type_size(t.datatype);
-  {
-    const int64_t esz = t.coll == kAllGather ? 1 : type_size(t.datatype);
-    const CbdPlan p = cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
-                                   comm->slotBytes, comm->nThreads);
-    if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
-      return ncclInternalError;
-    w.channelLo = p.channelLo;
-    w.channelHi = p.channelHi;
-    w.countLo = p.countLo;
-    w.countMid = p.countMid;
-    w.countHi = p.countHi;
-    w.chunkLo = p.chunkLo;
-    w.chunkMid = p.chunkMid;
-    w.chunkHi = p.chunkHi;
-    w.nChannels = p.channelHi + 1;  // idle channels above channelHi are not launched
+  const int64_t esz = t.coll == kAllGather ? 1 : type_size(t.datatype);
+  const CbdPlan p = cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
+                                 comm->slotBytes, comm->nThreads);
+  if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
+    return ncclInternalError;
+  w.channelLo = p.channelLo;
+  w.channelHi = p.channelHi;
+  w.countLo = p.countLo;
+  w.countMid = p.countMid;
+  w.countHi = p.countHi;
+  w.chunkLo = p.chunkLo;
+  w.chunkMid = p.chunkMid;
+  w.chunkHi = p.chunkHi;
+  w.nChannels = p.channelHi + 1;  // idle channels above channelHi are not launched
+  *out = w;
+  *ktOut = kt;
+  *devOpOut = devOp;
+  return ncclSuccess;
+}
+
+// 1 .. kRingMaxWorks ring calls of one comm with the same collective, kernel
+// type and op (ring_fusable) in one launch on ts[0].stream.
+static ncclResult_t launch_ring(const Task* ts, int nTasks) {
+  const Task& t = ts[0];
+  ncclComm* comm = t.comm;
+  if (nTasks < 1 || nTasks > kRingMaxWorks) return ncclInternalError;
+  RingBatch b{};
+  int kt = -1, devOp = -1;
+  NCCLCHECK(ring_work_of(t, &b.w, &kt, &devOp));
+  for (int i = 1; i < nTasks; i++) {
+    RingWork wi;
+    int kti, opi;
+    NCCLCHECK(ring_work_of(ts[i], &wi, &kti, &opi));
+    if (kti != kt || opi != devOp) return ncclInternalError;
+    b.more[i - 1] = ring_part_of(wi);
+    b.w.nChannels = std::max(b.w.nChannels, wi.nChannels);
   }
+  b.nParts = nTasks;
   const int coll = t.coll == kAllReduce ? kCollAllReduce
                    : t.coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
-    case K_U8: e = ring_launch<K_U8>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_U32: e = ring_launch<K_U32>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_U64: e = ring_launch<K_U64>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_F16: e = ring_launch<K_F16>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_F32: e = ring_launch<K_F32>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_F64: e = ring_launch<K_F64>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_BF16: e = ring_launch<K_BF16>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_F8E4M3: e = ring_launch<K_F8E4M3>(coll, devOp, w, comm->nThreads, t.stream); break;
-    case K_F8E5M2: e = ring_launch<K_F8E5M2>(coll, devOp, w, comm->nThreads, t.stream); break;
+    case K_U8: e = ring_launch<K_U8>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_U32: e = ring_launch<K_U32>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_U64: e = ring_launch<K_U64>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F16: e = ring_launch<K_F16>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F32: e = ring_launch<K_F32>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F64: e = ring_launch<K_F64>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_BF16: e = ring_launch<K_BF16>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F8E4M3: e = ring_launch<K_F8E4M3>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F8E5M2: e = ring_launch<K_F8E5M2>(coll, devOp, b, comm->nThreads, t.stream); break;
   }
   if (e != hipSuccess) {
     VWARN("ring kernel launch failed: %s", hipGetErrorString(e));
@@ -459,7 +482,7 @@ static CbdLite rs_cbd(const ncclComm* comm, const Task& t) {
 }
 
 // One-hop LL collectives.  All-reduce: `ts` holds 1 .. kLLMaxParts calls of
-// one comm with the same type and op (ll_fusable) whose lines fit one slot;
+// one comm with the same type and op (fusable) whose lines fit one slot;
 // they run as one launch on ts[0].stream (the caller orders the other
 // streams around it).  Reduce-scatter / all-gather: one call; a slot holds
 // one rank's block.
@@ -515,9 +538,9 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   return ncclSuccess;
 }
 
-// Direct collectives over the full mesh (direct.hpp): two-shot all-reduce,
-// one-hop reduce-scatter / all-gather.
-static ncclResult_t launch_direct(const Task& t) {
+// The direct work of one call (direct.hpp): two-shot all-reduce, one-hop
+// reduce-scatter / all-gather.
+static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, int* devOpOut) {
   ncclComm* comm = t.comm;
   const int n = comm->nRanks;
   const bool ag = t.coll == kAllGather;
@@ -573,8 +596,31 @@ static ncclResult_t launch_direct(const Task& t) {
     return ncclInternalError;
   const int kt = ag ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
-  const int coll = dev_coll(t.coll), devOp = ag ? OP_COPY : t.devOp;
-  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return direct_launch<K>(coll, devOp, w, t.stream); });
+  *out = w;
+  *ktOut = kt;
+  *devOpOut = ag ? OP_COPY : t.devOp;
+  return ncclSuccess;
+}
+
+// 1 .. kDirectMaxWorks direct calls of one comm with the same collective,
+// kernel type and op in one launch on ts[0].stream (the largest part's grid).
+static ncclResult_t launch_direct(const Task* ts, int nTasks) {
+  const Task& t = ts[0];
+  if (nTasks < 1 || nTasks > kDirectMaxWorks) return ncclInternalError;
+  DirectBatch b{};
+  int kt = -1, devOp = -1;
+  NCCLCHECK(direct_work_of(t, &b.w, &kt, &devOp));
+  for (int i = 1; i < nTasks; i++) {
+    DirectWork wi;
+    int kti, opi;
+    NCCLCHECK(direct_work_of(ts[i], &wi, &kti, &opi));
+    if (kti != kt || opi != devOp) return ncclInternalError;
+    b.more[i - 1] = direct_part_of(wi);
+    b.w.nBlocks = std::max(b.w.nBlocks, wi.nBlocks);
+  }
+  b.nParts = nTasks;
+  const int coll = dev_coll(t.coll);
+  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return direct_launch<K>(coll, devOp, b, t.stream); });
   if (e != hipSuccess) {
     VWARN("direct kernel launch failed: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
@@ -643,7 +689,7 @@ static ncclResult_t launch_task(const Task& t) {
   ncclResult_t r = stream_order(t.comm, t.stream, &cs);
   if (r == ncclSuccess) {
     const int algo = choose_algo(t);
-    r = algo == kAlgoLL ? launch_ll(&t, 1) : algo == kAlgoDirect ? launch_direct(t) : launch_ring(t);
+    r = algo == kAlgoLL ? launch_ll(&t, 1) : algo == kAlgoDirect ? launch_direct(&t, 1) : launch_ring(&t, 1);
   }
   if (r == ncclSuccess) r = stream_mark(t.comm, t.stream, cs);
   t.comm->opCount++;
@@ -652,21 +698,26 @@ static ncclResult_t launch_task(const Task& t) {
 }
 
 // Group aggregation (enqueue.cc:352-508 ncclPrepareTasks / :518-769
-// scheduleCollTasksToPlan pack a group's collectives into one kernel plan):
-// here a run of consecutive LL all-reduces of one comm with the same type and
-// op becomes one LL launch (up to kLLMaxParts, lines within one slot).  The
-// decision depends only on the call sequence, never on streams, so every rank
-// fuses identically.  The fused launch runs on the first task's stream; the
-// other tasks' streams are joined before it and wait for it after.
-static bool ll_eligible(const Task& t) {
-  return t.coll == kAllReduce && t.comm->nRanks > 1 && choose_algo(t) == kAlgoLL;
+// scheduleCollTasksToPlan pack a group's collectives into one kernel plan,
+// common.h:260-293 RunWorkBatch runs a plan's works in order): a run of
+// consecutive calls of one comm that take the same algorithm — LL, direct or
+// ring — with the same collective, kernel type and op becomes ONE launch
+// carrying up to 16 works (LL all-reduces: lines within one slot).  A ZeRO
+// loop's bucketed reduce-scatters launch once per group.  The decision
+// depends only on the call sequence, never on streams, so every rank fuses
+// identically.  The fused launch runs on the first task's stream; the other
+// tasks' streams are joined before it and wait for it after.
+static int fuse_key_algo(const Task& t) { return t.comm->nRanks > 1 ? choose_algo(t) : -1; }
+static bool fusable(const Task& a, const Task& b, int algo) {
+  if (a.comm != b.comm || a.coll != b.coll || fuse_key_algo(b) != algo) return false;
+  if (a.coll == kAllGather) return true;  // byte copies: any type
+  return a.datatype == b.datatype && a.devOp == b.devOp && a.arg == b.arg && a.argPtr == b.argPtr;
 }
-static bool ll_fusable(const Task& a, const Task& b) {
-  return a.comm == b.comm && a.datatype == b.datatype && a.devOp == b.devOp && a.arg == b.arg &&
-         a.argPtr == b.argPtr;
+static int max_parts(int algo) {
+  return algo == kAlgoLL ? kLLMaxParts : algo == kAlgoDirect ? kDirectMaxWorks : kRingMaxWorks;
 }
 
-static ncclResult_t launch_ll_batch(const std::vector<Task>& ts) {
+static ncclResult_t launch_fused(const std::vector<Task>& ts, int algo) {
   ncclComm* comm = ts[0].comm;
   const hipStream_t s0 = ts[0].stream;
   int old = -1;
@@ -684,7 +735,11 @@ static ncclResult_t launch_ll_batch(const std::vector<Task>& ts) {
         hipStreamWaitEvent(s0, comm->joinEvent, 0) != hipSuccess)
       r = ncclUnhandledCudaError;
   }
-  if (r == ncclSuccess) r = launch_ll(ts.data(), (int)ts.size());
+  if (r == ncclSuccess) {
+    const int n = (int)ts.size();
+    r = algo == kAlgoLL ? launch_ll(ts.data(), n)
+        : algo == kAlgoDirect ? launch_direct(ts.data(), n) : launch_ring(ts.data(), n);
+  }
   if (r == ncclSuccess) r = stream_mark(comm, s0, cs);
   const hipEvent_t done = stream_last_event(comm, cs);
   for (hipStream_t s : others)
@@ -703,18 +758,21 @@ static ncclResult_t launch_group(std::vector<Task>& tasks) {
   for (size_t i = 0; i < tasks.size(); i++) {
     if (done[i]) continue;
     ncclResult_t r;
-    if (fuse && ll_eligible(tasks[i])) {
+    const int algo = fuse ? fuse_key_algo(tasks[i]) : -1;
+    if (algo >= 0 && (algo != kAlgoLL || tasks[i].coll == kAllReduce)) {
       std::vector<Task> batch{tasks[i]};
       int64_t lines = ll_lines_of(tasks[i]);
-      for (size_t j = i + 1; j < tasks.size() && batch.size() < (size_t)kLLMaxParts; j++) {
+      for (size_t j = i + 1; j < tasks.size() && batch.size() < (size_t)max_parts(algo); j++) {
         if (done[j] || tasks[j].comm != tasks[i].comm) continue;
-        if (!ll_eligible(tasks[j]) || !ll_fusable(tasks[i], tasks[j])) break;
-        if (lines + ll_lines_of(tasks[j]) > tasks[i].comm->llLines) break;
-        lines += ll_lines_of(tasks[j]);
+        if (!fusable(tasks[i], tasks[j], algo)) break;
+        if (algo == kAlgoLL) {
+          if (lines + ll_lines_of(tasks[j]) > tasks[i].comm->llLines) break;
+          lines += ll_lines_of(tasks[j]);
+        }
         batch.push_back(tasks[j]);
         done[j] = 1;
       }
-      r = batch.size() == 1 ? launch_task(tasks[i]) : launch_ll_batch(batch);
+      r = batch.size() == 1 ? launch_task(tasks[i]) : launch_fused(batch, algo);
     } else {
       r = launch_task(tasks[i]);
     }

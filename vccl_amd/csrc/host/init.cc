@@ -264,7 +264,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     if (n <= kDirectMaxRanks) {
       const int64_t chunk = std::max<int64_t>(param_int("DIRECT_CHUNK_BYTES", 16 << 20), 64 << 10);
       c->dRegionBytes = (chunk + n - 1) / n / 256 * 256 + 256;
-      const size_t bytes = (size_t)2 * n * c->dRegionBytes;
+      const size_t bytes = (size_t)kDirectInboxRegions * n * c->dRegionBytes;
       NCCLCHECK(alloc_uncached((void**)&c->dBuf, bytes));
       NCCLCHECK(alloc_uncached((void**)&c->dFlags, kDirectFlagBytes));
       HIPCHECK(hipMemset(c->dFlags, 0, kDirectFlagBytes));
