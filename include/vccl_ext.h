@@ -46,6 +46,8 @@
  *                     = channelLo, channelHi, countLo, countMid, countHi,
  *                     chunkLo, chunkMid, chunkHi (elements; bytes for
  *                     all-gather, which the reference runs as int8).
+ *   vcclRingOrders     the arc-balanced ring set for n ranks (SURVEY.md
+ *                     Appendix D; Walecki's decomposition for odd n).
  *   vcclRingChunkOf    for element i of an all-reduce on that partition:
  *                     out[0] = its channel, out[1] = the ring chunk c of its
  *                     loop (the chunk that finishes at ring position c,
@@ -84,6 +86,9 @@ ncclResult_t vcclRingPartition(int coll, size_t count, ncclDataType_t datatype, 
                                int nChannels, size_t slotBytes, int nThreads, int64_t* out);
 ncclResult_t vcclRingChunkOf(size_t count, ncclDataType_t datatype, int nRanks, int nChannels,
                              size_t slotBytes, int nThreads, size_t i, int64_t* out);
+/* The ring set of an nRanks communicator: orders[k * nRanks + i] = the rank
+ * at position i of ring k (channel c runs on ring c mod nRings). */
+ncclResult_t vcclRingOrders(int nRanks, int maxRings, int* orders, int* nRings);
 
 #ifdef __cplusplus
 }

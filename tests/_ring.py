@@ -24,15 +24,43 @@ RINGS = {
 }
 
 
+# 6 GPUs: two edge-disjoint Hamiltonian cycles of K6, both directions.
+RINGS[6] = [[0, 1, 2, 3, 4, 5], [0, 5, 4, 3, 2, 1], [0, 2, 4, 1, 5, 3], [0, 3, 5, 1, 4, 2]]
+
+
+def walecki(n):
+    """Odd n = 2m+1: Walecki's m edge-disjoint Hamiltonian cycles of K_n (hub
+    n-1, then k, k+1, k-1, k+2, ... mod 2m), each in both directions, rotated
+    to start at 0 — an independent restatement of host/init.cc."""
+    m, h = (n - 1) // 2, n - 1
+    out = []
+    for k in range(m):
+        cyc = [n - 1, k]
+        j = 1
+        while len(cyc) < n:
+            cyc.append((k + j) % h)
+            if len(cyc) < n:
+                cyc.append((k - j) % h)
+            j += 1
+        for c in (cyc, [cyc[0]] + cyc[1:][::-1]):
+            i = c.index(0)
+            out.append(c[i:] + c[:i])
+    return out
+
+
 def ring_orders(n):
-    return RINGS.get(n, [list(range(n))])
+    if n in RINGS:
+        return RINGS[n]
+    if n >= 3 and n % 2 == 1 and n - 1 <= 8:
+        return walecki(n)
+    return [list(range(n))]
 
 
 def n_channels(n, per_ring=None, nch=None):
     """Library default channel count (host/init.cc) unless overridden."""
     rings = ring_orders(n)
     if per_ring is None:
-        per_ring = 8 if n >= 4 else 48
+        per_ring = 8 if n >= 4 else 24 if n == 3 else 48
     c = nch if nch is not None else per_ring * len(rings)
     return max(1, min(c, 64))
 

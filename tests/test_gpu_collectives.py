@@ -163,9 +163,10 @@ def test_single_process_ranks(n, monkeypatch):
             c.destroy()
 
 
-@pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (8, "test"),
-                                    (2, "ring_only"), (4, "ring_only"), (8, "ring_only"),
-                                    (4, "direct_only"), (8, "default8"), (2, "net"), (3, "net")])
+@pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (6, "test"), (8, "test"),
+                                    (2, "ring_only"), (4, "ring_only"), (7, "ring_only"),
+                                    (8, "ring_only"), (4, "direct_only"), (8, "default8"), (2, "net"),
+                                    (3, "net")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()

@@ -102,7 +102,7 @@ def _simulate_allreduce(op, dt, inputs, nch, slot_bytes):
     return outs
 
 
-@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("dt,op", [(7, 0), (9, 0), (6, 4), (2, 4), (7, 1)])
 def test_simulated_schedule_matches_owner_map(n, dt, op):
     rng = np.random.default_rng(n * 10 + dt)
@@ -122,7 +122,9 @@ def test_simulated_schedule_matches_owner_map(n, dt, op):
 
 
 def test_ring_sets_are_arc_balanced():
-    for n, mult in ((8, 1), (4, 2)):
+    # every n-1 rings arc-disjoint (8; odd n by Walecki's construction) or every
+    # arc in exactly 2 rings (4)
+    for n, mult in ((8, 1), (4, 2), (3, 1), (5, 1), (7, 1)):
         arcs = {}
         for ring in _ring.ring_orders(n):
             assert sorted(ring) == list(range(n))
@@ -137,3 +139,24 @@ def test_ring_sets_are_arc_balanced():
     disjoint3 = [(a, b, d) for a in range(6) for b in range(a + 1, 6) for d in range(b + 1, 6)
                  if not (arcsets[a] & arcsets[b] or arcsets[a] & arcsets[d] or arcsets[b] & arcsets[d])]
     assert disjoint3 == []
+
+
+def test_six_rank_rings_edge_disjoint():
+    """6 GPUs (no directed Hamiltonian decomposition of K6 exists): two
+    edge-disjoint Hamiltonian cycles in both directions — every used arc
+    once, 4 of each rank's 5 outgoing links."""
+    arcs = {}
+    for ring in _ring.ring_orders(6):
+        assert sorted(ring) == list(range(6))
+        for i in range(6):
+            a = (ring[i], ring[(i + 1) % 6])
+            arcs[a] = arcs.get(a, 0) + 1
+    assert set(arcs.values()) == {1} and len(arcs) == 24
+    assert all(sum(1 for a in arcs if a[0] == r) == 4 for r in range(6))
+
+
+def test_library_ring_sets_equal_restatement():
+    """vcclRingOrders (host/init.cc) == tests/_ring.py for every n."""
+    from vccl_amd import nccl
+    for n in range(1, 9):
+        assert nccl.ring_orders(n) == _ring.ring_orders(n), n

@@ -33,10 +33,40 @@ ncclResult_t comm_check(const ncclComm* comm, const char* api) {
   return ncclSuccess;
 }
 
-// SURVEY.md Appendix D (exhaustive search, verified by tests/test_rings.py):
-// 8 GPUs: 7 arc-disjoint directed Hamiltonian cycles (every xGMI link used by
-// exactly one ring per direction); 4 GPUs: all 6 directed Hamiltonian cycles
-// (every arc in exactly 2); 2 GPUs: the single ring.
+// Walecki's decomposition of the complete graph on an odd number of vertices
+// n = 2m + 1 into m edge-disjoint Hamiltonian cycles: vertex n-1 (the hub)
+// followed by the zigzag k, k+1, k-1, k+2, k-2, ... over 0..2m-1 (mod 2m),
+// k = 0..m-1.  Each cycle run in both directions gives n-1 arc-disjoint
+// directed rings that use every xGMI link once per direction.
+static std::vector<std::vector<int>> walecki_rings(int n) {
+  const int m = (n - 1) / 2, h = 2 * m;
+  std::vector<std::vector<int>> out;
+  for (int k = 0; k < m; k++) {
+    std::vector<int> cyc{n - 1, k};
+    for (int j = 1; (int)cyc.size() < n; j++) {
+      cyc.push_back(((k + j) % h + h) % h);
+      if ((int)cyc.size() < n) cyc.push_back(((k - j) % h + h) % h);
+    }
+    out.push_back(cyc);
+    std::vector<int> rev{cyc[0]};
+    for (int i = n - 1; i >= 1; i--) rev.push_back(cyc[i]);
+    out.push_back(rev);
+  }
+  // rotate each ring to start at rank 0 (cosmetic: a ring is a cycle)
+  for (auto& r : out) std::rotate(r.begin(), std::find(r.begin(), r.end(), 0), r.end());
+  return out;
+}
+
+// Ring sets over the fully connected xGMI mesh (SURVEY.md Appendix D,
+// verified by tests/test_ring_schedule.py):
+//   8 GPUs: 7 arc-disjoint directed Hamiltonian cycles (every link carries
+//           one ring per direction);
+//   4 GPUs: all 6 directed Hamiltonian cycles (every arc in exactly 2: no
+//           arc-disjoint decomposition exists);
+//   odd n (3, 5, 7): Walecki's n-1 arc-disjoint directed rings;
+//   6 GPUs: two edge-disjoint Hamiltonian cycles, both directions (4 of each
+//           rank's 5 links; K6 has no directed Hamiltonian decomposition);
+//   2 GPUs: the single ring.
 std::vector<std::vector<int>> ring_orders(int n) {
   if (n == 8)
     return {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 2, 1, 3, 5, 4, 7, 6}, {0, 3, 1, 4, 6, 2, 7, 5},
@@ -44,6 +74,9 @@ std::vector<std::vector<int>> ring_orders(int n) {
             {0, 7, 3, 2, 5, 1, 6, 4}};
   if (n == 4)
     return {{0, 1, 2, 3}, {0, 1, 3, 2}, {0, 2, 1, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {0, 3, 2, 1}};
+  if (n == 6)
+    return {{0, 1, 2, 3, 4, 5}, {0, 5, 4, 3, 2, 1}, {0, 2, 4, 1, 5, 3}, {0, 3, 5, 1, 4, 2}};
+  if (n >= 3 && n % 2 == 1 && n - 1 <= kOrderMaxRings) return walecki_rings(n);
   std::vector<int> id(n);
   for (int i = 0; i < n; i++) id[i] = i;
   return {id};
@@ -147,7 +180,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   // 8- and 4-GPU ring sets (56 / 48 workgroups), 48 for 2 GPUs
   // (profiles/r02g/sweep_ring_1g.log: 16 / 32 / 48 channels -> 199 / 299 /
   // 436 GB/s busbw at 1 GiB, 2 ranks on one GPU).
-  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : 48);
+  // (3 ranks: 2 rings x 24 = the 48 workgroups of the 2-rank default)
+  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : n == 3 ? 24 : 48);
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
   // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490)
   nch = std::max(c->minCTAs, std::min(nch, c->maxCTAs));
@@ -547,6 +581,17 @@ using namespace vccl;
 
 #define VCCL_EXPORT extern "C" __attribute__((visibility("default")))
 #define VCCL_ALIAS(name) __attribute__((alias(#name), visibility("default")))
+
+// vccl_ext.h: the ring set the library uses for nRanks ranks.
+VCCL_EXPORT ncclResult_t vcclRingOrders(int nRanks, int maxRings, int* orders, int* nRings) {
+  if (nRanks < 1 || nRanks > kMaxRanks || maxRings < 1 || !orders || !nRings) return ncclInvalidArgument;
+  const auto rings = ring_orders(nRanks);
+  *nRings = (int)rings.size();
+  if ((int)rings.size() > maxRings) return ncclInvalidArgument;
+  for (size_t k = 0; k < rings.size(); k++)
+    for (int i = 0; i < nRanks; i++) orders[k * nRanks + i] = rings[k][i];
+  return ncclSuccess;
+}
 
 VCCL_EXPORT ncclResult_t ncclGetVersion(int* version) {
   if (!version) return ncclInvalidArgument;

@@ -40,7 +40,7 @@ EXPORTED = [
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
-    "vcclRingPartition", "vcclRingChunkOf",
+    "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
 ]
@@ -109,6 +109,7 @@ def lib() -> ctypes.CDLL:
         "vcclCommDebugSetEpochs": [vp, ctypes.c_uint32, ctypes.c_uint32],
         "vcclRingChunkOf": [c_size, c_int, c_int, c_int, c_size, c_int, c_size,
                             ctypes.POINTER(ctypes.c_int64)],
+        "vcclRingOrders": [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -180,6 +181,14 @@ def ring_partition(coll: int, count: int, dtype: int, nranks: int, nchannels: in
     check(lib().vcclRingPartition(coll, count, dtype, nranks, nchannels, slot_bytes, nthreads, out),
           "vcclRingPartition")
     return tuple(out)
+
+
+def ring_orders(nranks: int) -> list[list[int]]:
+    """vcclRingOrders: the library's ring set for nranks ranks."""
+    out = (ctypes.c_int * (16 * nranks))()
+    nr = ctypes.c_int()
+    check(lib().vcclRingOrders(nranks, 16, out, ctypes.byref(nr)), "vcclRingOrders")
+    return [list(out[k * nranks:(k + 1) * nranks]) for k in range(nr.value)]
 
 
 def ring_chunk_of(count: int, dtype: int, nranks: int, nchannels: int, slot_bytes: int,
