@@ -38,8 +38,9 @@
  *   vcclRingPartition  the channel partition the ring algorithm uses for a
  *                     call (host only): VCCL's cbd split and chunking
  *                     (scheduleCollTasksToPlan, src/enqueue.cc:518-644, for a
- *                     plan of one collective) for `nChannels` channels and a
- *                     FIFO slot of `slotBytes` (NCCL_BUFFSIZE / 8) and
+ *                     plan of one collective) for `nChannels` channels,
+ *                     protocol `proto` (2 SIMPLE, 1 LL128) with a FIFO step
+ *                     of `stepBytes` (that protocol's buffer size / 8) and
  *                     `nThreads` ring threads (NCCL_NTHREADS: the channel
  *                     tuning's maxThreads[RING][SIMPLE], tuning.cc:198-200).
  *                     out[0..7]
@@ -70,7 +71,8 @@ typedef enum {
   vcclAlgoRing = 0,     /* SIMPLE ring over arc-balanced ring sets */
   vcclAlgoLL = 1,       /* one-shot LL all-reduce, chain-tree fold */
   vcclAlgoDirect = 2,   /* two-shot direct all-reduce over the full mesh */
-  vcclAlgoOneRank = 3   /* nRanks == 1: copy / PreMulSum kernel */
+  vcclAlgoOneRank = 3,  /* nRanks == 1: copy / PreMulSum kernel */
+  vcclAlgoLL128 = 4     /* ring over LL128 FIFOs (64-byte lines, in-line flags) */
 } vcclAlgo_t;
 
 ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count, ncclDataType_t datatype,
@@ -83,7 +85,8 @@ ncclResult_t vcclCommNetStats(ncclComm_t comm, uint64_t* bytesSent, uint64_t* by
 ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences);
 ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoch, uint32_t directEpoch);
 ncclResult_t vcclRingPartition(int coll, size_t count, ncclDataType_t datatype, int nRanks,
-                               int nChannels, size_t slotBytes, int nThreads, int64_t* out);
+                               int nChannels, int proto, size_t stepBytes, int nThreads,
+                               int64_t* out);
 ncclResult_t vcclRingChunkOf(size_t count, ncclDataType_t datatype, int nRanks, int nChannels,
                              size_t slotBytes, int nThreads, size_t i, int64_t* out);
 /* The ring set of an nRanks communicator: orders[k * nRanks + i] = the rank

@@ -73,7 +73,17 @@ def _div_up(x, a):
     return (x + a - 1) // a
 
 
-def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=512):
+def _sched(coll, count, esz, n, nch, slot_bytes, nthreads, proto):
+    """The ring's partition: SIMPLE with the comm's slot and NCCL_NTHREADS, or
+    LL128 with VCCL's default LL128 buffer and NCCL_LL128_NTHREADS (640)."""
+    if proto == S.PROTO_LL128:
+        return S.cbd_schedule(coll, count, esz, n, nch, proto=S.PROTO_LL128)
+    return S.cbd_schedule(coll, count, esz, n, nch, buff_size=slot_bytes * S.NCCL_STEPS,
+                          nthreads=nthreads)
+
+
+def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=512,
+                       proto=S.PROTO_SIMPLE):
     """Exact expected ring all-reduce output (identical on every rank): the
     oracle's restatement of VCCL's channel partition and chunking
     (oracle/vccl_sched.py) decides channel and finishing ring index per
@@ -84,8 +94,7 @@ def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size
     esz = inputs[0].dtype.itemsize
-    work = S.cbd_schedule("ar", count, esz, n, nch, buff_size=slot_bytes * S.NCCL_STEPS,
-                          nthreads=nthreads)
+    work = _sched("ar", count, esz, n, nch, slot_bytes, nthreads, proto)
     chan, owner = S.allreduce_owner(work, count, n)
     out = np.empty_like(inputs[0])
     for c in range(work.channel_lo, work.channel_hi + 1):
@@ -98,7 +107,8 @@ def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=
     return out
 
 
-def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=None, nthreads=512):
+def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=None, nthreads=512,
+                           proto=S.PROTO_SIMPLE):
     """Per-rank expected outputs; inputs[r] has n*recvcount elements.  Rank
     r's block is folded on the ring of each element's channel (VCCL's cbd
     partition of the recvcount block), finishing at r."""
@@ -107,8 +117,7 @@ def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=N
     dev_op, arg = O.host_to_dev_redop(op, dtype, n)
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size // n
-    work = S.cbd_schedule("rs", count, inputs[0].dtype.itemsize, n, nch,
-                          buff_size=slot_bytes * S.NCCL_STEPS, nthreads=nthreads)
+    work = _sched("rs", count, inputs[0].dtype.itemsize, n, nch, slot_bytes, nthreads, proto)
     chan = S.channel_of(work, count)
     outs = [np.empty(count, inputs[0].dtype) for _ in range(n)]
     for c in range(work.channel_lo, work.channel_hi + 1):

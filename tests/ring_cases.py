@@ -149,15 +149,15 @@ def gen_group_input(gi, rank):
 
 
 def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
-                   nthreads=512):
+                   nthreads=512, proto=2):
     name, op, dt, count = GROUP_CASES[gi]
     ins = [gen_group_input(gi, r) for r in range(n_ranks)]
     return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                       nthreads)
+                       nthreads, proto)
 
 
 def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                nthreads=512):
+                nthreads=512, proto=2):
     """All-reduce result: LL chain fold up to ll_max bytes, the ring's
     owner-map fold (VCCL's ring schedule on these channels) above — for the
     two-shot direct path too, which folds every element in the ring's order
@@ -168,11 +168,12 @@ def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direc
     if count * ins[0].dtype.itemsize <= ll_max:
         dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
         return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
-    return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes, nthreads=nthreads)
+    return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes, nthreads=nthreads, proto=proto)
 
 
 def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
-             nthreads=512):
+             nthreads=512, proto=2):
+    """proto: the ring's protocol (2 SIMPLE, 1 LL128 — VCCL's LL128 partition)."""
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
     (oracle ref_chain_fold); larger ones the two-shot direct path (up to
@@ -181,10 +182,10 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace", "ar_mis"):
         e = expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                        nthreads)
+                        nthreads, proto)
         return [e] * n_ranks
     if coll == "rs":
-        return _ring.expected_reducescatter(op, dt, ins, nch, nthreads=nthreads)
+        return _ring.expected_reducescatter(op, dt, ins, nch, nthreads=nthreads, proto=proto)
     full = np.concatenate(ins)
     return [full] * n_ranks
 

@@ -45,13 +45,13 @@ DIRECT_TEST = 4 << 20
 DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in chunks
 
 
-def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST, nthreads=512):
+def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST, nthreads=512, proto=2):
     """Bit-exact against the path's own fold order (the ring's IS VCCL's
     schedule on our rings and channels); for fp sum / prod additionally
     within the §8c tolerance of the exact value and of VCCL's result on its
     reference geometry (RC.vccl_reference)."""
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk, nthreads)
+    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
     vref = RC.vccl_reference(ci, n)
@@ -166,15 +166,23 @@ def test_single_process_ranks(n, monkeypatch):
 @pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (6, "test"), (8, "test"),
                                     (2, "ring_only"), (4, "ring_only"), (7, "ring_only"),
                                     (8, "ring_only"), (4, "direct_only"), (8, "default8"), (2, "net"),
-                                    (3, "net")])
+                                    (3, "net"), (2, "ll128"), (4, "ll128"), (8, "ll128")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
     ll_max, direct_max, chunk = LL_DEFAULT, DIRECT_TEST, DIRECT_CHUNK_TEST
-    nthreads = 512
-    if geom in ("test", "ring_only", "direct_only"):
+    nthreads, proto = 512, 2
+    if geom == "ll128":
+        # NCCL_PROTO=LL128: every collective on the LL128 ring (ring.hpp
+        # prim_ll128), on VCCL's LL128 partition and chunking
+        env.update(TEST_GEOM)
+        env["NCCL_PROTO"] = "LL128"
+        nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+        ll_max = direct_max = 0
+        proto = 1
+    elif geom in ("test", "ring_only", "direct_only"):
         env.update(TEST_GEOM)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
         if geom == "ring_only":  # NCCL_ALGO forces the ring for every size
@@ -226,9 +234,9 @@ def test_multi_process_ranks(n, geom):
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
             _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk,
-                   nthreads)
+                   nthreads, proto)
         _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot, ll_max,
-                     direct_max, chunk, nthreads)
+                     direct_max, chunk, nthreads, proto)
         # every geometry fuses the group's runs (LL, direct or ring batches)
         fused = int(res[0]["launch_stats"][1])
         assert fused > 0, f"fused group launches: {fused}"
@@ -271,9 +279,9 @@ def test_beyond_2gib_two_ranks():
     assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
 
 
-def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512):
+def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512, proto=2):
     for gi, (name, op, dt, count) in enumerate(RC.GROUP_CASES):
-        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads)
+        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto)
         for r in range(n):
             assert_bitexact(dt, outs[r][name], exp, minmax=op in (2, 3),
                             what=f"group {name} n={n} rank {r}")

@@ -77,6 +77,27 @@ def test_partition_properties(coll):
                         assert all(ln * e * tpb >= S.MIN_TRAFFIC_PER_CHANNEL for ln in ends[:-1])
 
 
+@pytest.mark.parametrize("coll", ["ar", "rs", "ag"])
+def test_library_ll128_partition_equals_oracle(coll):
+    """The LL128 ring's partition (VCCL's LL128 cells, 1,920 B grain, 576,000 B
+    chunk of the 614,400 B step, 640-thread channel tuning, enqueue.cc:
+    1902-1925, 2027-2032) from the library vs the oracle."""
+    for n in (2, 4, 8):
+        for nch in (1, 14, 56):
+            for dt in (7, 9, 0):
+                for count in _sizes():
+                    lib = nccl.ring_partition(COLLS[coll], count, dt, n, nch, 614_400, 640,
+                                              proto=nccl.PROTO_LL128)
+                    w = S.cbd_schedule(coll, count, ESZ[dt], n, nch, proto=S.PROTO_LL128)
+                    per = S.grain_size(w.proto) // w.elt_size
+                    ref = (w.channel_lo, w.channel_hi, w.count_lo, w.count_mid, w.count_hi,
+                           w.chunk_grains_lo * per, w.chunk_grains_mid * per, w.chunk_grains_hi * per)
+                    assert lib[:5] == ref[:5], (coll, n, nch, dt, count, lib, ref)
+                    for i, cnt in ((5, w.count_lo), (6, w.count_mid), (7, w.count_hi)):
+                        if cnt:
+                            assert lib[i] == ref[i] == 576_000 // w.elt_size, (coll, n, nch, dt, count, i)
+
+
 def test_hand_derived_cases():
     # 1 GiB f32 all-reduce, 56 channels (8 GPUs x 7 rings x 8): traffic 2 GiB,
     # 38,347,922 B per channel; 8 KiB cells (16 KiB traffic), 131,072 cells;

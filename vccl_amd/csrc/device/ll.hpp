@@ -67,7 +67,7 @@ __device__ __forceinline__ uint64_t ll_apply(const Fn& fn, uint64_t acc, uint64_
 // Poll one LL line until both halves carry `epoch`; returns the 8 data bytes.
 __device__ __forceinline__ bool ll_read_line(const char* line, uint32_t epoch, const DevComm* comm,
                                              uint64_t* out) {
-  const SysAddr s = sys_addr(line);
+  const SysAddr s = sys_addr_window(line);  // lanes may poll different ranks' slots
   uint64_t spins = 0, start = 0;
   for (;;) {
     u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(s.r, s.voff, 0, kSysAux);
@@ -251,7 +251,8 @@ __device__ void ll_reducescatter(const LLWork& w) {
     for (int j = 0; j < kOrderMaxRanks; j++) {  // every peer line of l in flight at once
       const int q = j < n ? order[j] : me;
       if (q != me) {
-        const SysAddr a = sys_addr(w.localBuf + ll_slot_off(parity, q, n, w.linesPerSlot) + l * 16);
+        // q differs between lanes whose lines sit in different channel parts
+        const SysAddr a = sys_addr_window(w.localBuf + ll_slot_off(parity, q, n, w.linesPerSlot) + l * 16);
         v[j] = __builtin_amdgcn_raw_buffer_load_b128(a.r, a.voff, 0, kSysAux);
       }
     }

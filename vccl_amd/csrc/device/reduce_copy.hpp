@@ -67,6 +67,21 @@ __device__ __forceinline__ SysAddr sys_addr(const char* a) {
           (int)(x - x0)};
 }
 
+// The same for lanes whose addresses need NOT grow with the lane index (the
+// LL reduce-scatter's fold reads, where lanes of one wave may sit in
+// different channel parts and so read different ranks' slots): the
+// descriptor base is 1 GiB below the first active lane's address, so every
+// lane within +-1 GiB of it gets a valid non-negative voffset.  Callers keep
+// all of a wave's addresses inside one buffer far smaller than that.
+__device__ __forceinline__ SysAddr sys_addr_window(const char* a) {
+  const uint64_t x = (uint64_t)(uintptr_t)a;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  const uint64_t x0 = (((uint64_t)hi << 32) | lo) - (1ull << 30);
+  return {__builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)x0, 0, 0x7fffffff, 0x00020000),
+          (int)(x - x0)};
+}
+
 template <int P>
 __device__ __forceinline__ u32x4 ld16(const char* base, int64_t off) {
   if constexpr (P == kNT) return __builtin_nontemporal_load((const u32x4*)(base + off));

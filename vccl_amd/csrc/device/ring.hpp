@@ -35,6 +35,7 @@ struct RingCtx {
   uint64_t recvStep, sendStep;
   int tid, nthreads;
   int slotBytes;
+  int64_t ll128Slot;  // bytes per LL128 FIFO slot (LL128 ring only)
   int* shAbort;  // LDS
 
   // Bounded spin on `flag` until pred(value); returns false on abort/timeout.
@@ -133,6 +134,176 @@ struct RingCtx {
   }
 };
 
+// ---------------------------------------------------------------- LL128
+// LL128 protocol (prims_ll128.h:176-324, recvReduceSendCopy / GenericOp),
+// gfx950 wire format.  A step's data travels as 64-byte lines: lanes 4i..4i+2
+// carry 16-byte data pieces, lane 4i+3 an 8-byte data piece and the 8-byte
+// flag (step + 1, as recvFlag / sendFlag).  One wave instruction moves 16
+// lines = 1 KiB ("a round") carrying 896 data bytes: lane l's piece is bytes
+// [16 (3 (l/4) + l%4), +16) of the round, or for a flag lane the half
+// [16 (48 + l/8) + 8 ((l/4) & 1), +8).  The receiver polls its round's lines
+// (one 16-byte sc0 sc1 load per lane) until every flag lane shows the step,
+// and uses the data of that same load: a line is one 64-byte write request
+// of the sender's wave store (sc0 sc1 write-through), the granule the flag
+// covers.  The reference puts one 8-byte flag in each 128-byte NVLink line
+// (15/16 efficiency, atomic on NVLink); here a flag per 64-byte request
+// (7/8).  No tail flag and no drain per step: the sender waits for the
+// credit (head) like SIMPLE, the receiver posts the head after the step.
+// Steps and credits are the channel's SIMPLE ones (ring_types.hpp).
+template <class T>
+__device__ __forceinline__ void ll128_put(uint64_t& lo, uint64_t& hi, int q, T x) {
+  uint64_t v;
+  if constexpr (sizeof(T) == 1) v = __builtin_bit_cast(uint8_t, x);
+  else if constexpr (sizeof(T) == 2) v = __builtin_bit_cast(uint16_t, x);
+  else if constexpr (sizeof(T) == 4) v = __builtin_bit_cast(uint32_t, x);
+  else v = __builtin_bit_cast(uint64_t, x);
+  if (q < 8) lo |= v << (8 * q);
+  else hi |= v << (8 * (q - 8));
+}
+template <class T>
+__device__ __forceinline__ T ll128_get(uint64_t lo, uint64_t hi, int q) {
+  const uint64_t w = q < 8 ? lo >> (8 * q) : hi >> (8 * (q - 8));
+  if constexpr (sizeof(T) == 1) return __builtin_bit_cast(T, (uint8_t)w);
+  else if constexpr (sizeof(T) == 2) return __builtin_bit_cast(T, (uint16_t)w);
+  else if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, (uint32_t)w);
+  else return __builtin_bit_cast(T, w);
+}
+// `len` (16 or 8) bytes at byte offset b0 of `p`, zero past `nbytes`;
+// `al`: p is 16-byte aligned (whole-piece access), else element by element.
+template <class T, int P>
+__device__ __forceinline__ u32x4 ll128_ld_piece(const char* p, int64_t b0, int len, int64_t nbytes,
+                                               bool al) {
+  u32x4 v = {0, 0, 0, 0};
+  if (b0 >= nbytes) return v;
+  if (al && b0 + len <= nbytes) {
+    if (len == 16) return ld16<P>(p, b0);
+    const uint64_t x = *(const uint64_t*)(p + b0);
+    v.x = (uint32_t)x;
+    v.y = (uint32_t)(x >> 32);
+    return v;
+  }
+  uint64_t lo = 0, hi = 0;
+#pragma unroll
+  for (int q = 0; q < 16; q += (int)sizeof(T))
+    if (q < len && b0 + q < nbytes) ll128_put<T>(lo, hi, q, *(const T*)(p + b0 + q));
+  v.x = (uint32_t)lo;
+  v.y = (uint32_t)(lo >> 32);
+  v.z = (uint32_t)hi;
+  v.w = (uint32_t)(hi >> 32);
+  return v;
+}
+template <class T, int P>
+__device__ __forceinline__ void ll128_st_piece(char* p, int64_t b0, int len, int64_t nbytes, bool al,
+                                               u32x4 v) {
+  if (b0 >= nbytes) return;
+  if (al && b0 + len <= nbytes) {
+    if (len == 16) st16<P>(p, b0, v);
+    else *(uint64_t*)(p + b0) = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    return;
+  }
+  const uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32), hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+#pragma unroll
+  for (int q = 0; q < 16; q += (int)sizeof(T))
+    if (q < len && b0 + q < nbytes) *(T*)(p + b0 + q) = ll128_get<T>(lo, hi, q);
+}
+
+constexpr int kLL128Unroll = 2;  // rounds in flight per wave
+
+// One LL128 primitive call: a whole ring chunk (<= one LL128 slot).
+//   src = own input (SRC), dst = own output (DST); recv / send = the slots.
+template <class Fn, bool RECV, bool SEND, bool SRC, bool DST>
+__device__ void ll128_prim(RingCtx& R, const Fn& fn, const void* srcv, void* dstv, int64_t nelem,
+                           bool preOp, bool postOp) {
+  using T = typename Fn::EltType;
+  if (R.aborted()) return;
+  if (R.tid == 0) {
+    bool ok = true;
+    if (SEND && R.sendStep + 1 > (uint64_t)kSteps) ok = R.spin_ge(R.ch->sendHead, R.sendStep + 1 - kSteps);
+    if (!ok) *R.shAbort = 1;
+  }
+  __syncthreads();
+  if (R.aborted()) return;
+  const char* src = (const char*)srcv;
+  char* dst = (char*)dstv;
+  const int64_t nbytes = nelem > 0 ? nelem * (int64_t)sizeof(T) : 0;
+  const int64_t nRounds = (nbytes + kLL128RoundData - 1) / kLL128RoundData;
+  const uint64_t rflag = R.recvStep + 1, sflag = R.sendStep + 1;
+  const char* rslot = RECV ? R.ch->ll128Recv + (int64_t)(R.recvStep % kSteps) * R.ll128Slot : nullptr;
+  char* sslot = SEND ? R.ch->ll128Send + (int64_t)(R.sendStep % kSteps) * R.ll128Slot : nullptr;
+  const int lane = R.tid & 63, wave = R.tid >> 6, nw = R.nthreads >> 6;
+  const int line = lane >> 2;
+  const bool flagLane = (lane & 3) == 3;
+  const int dOff = flagLane ? (48 + (line >> 1)) * 16 + (line & 1) * 8 : (line * 3 + (lane & 3)) * 16;
+  const int dLen = flagLane ? 8 : 16;
+  const bool srcAl = SRC && (((uintptr_t)src & 15) == 0);
+  const bool dstAl = DST && (((uintptr_t)dst & 15) == 0);
+  bool fail = false;
+  for (int64_t r0 = wave; r0 < nRounds && !fail; r0 += (int64_t)nw * kLL128Unroll) {
+    u32x4 own[kLL128Unroll], rv[kLL128Unroll];
+#pragma unroll
+    for (int u = 0; u < kLL128Unroll; u++) {
+      const int64_t r = r0 + (int64_t)u * nw;
+      if (SRC && r < nRounds) own[u] = ll128_ld_piece<T, VCCL_RING_SRC_POL>(src, r * kLL128RoundData + dOff, dLen, nbytes, srcAl);
+      if (RECV && r < nRounds) rv[u] = ld16<kSys>(rslot, r * kLL128RoundWire + lane * 16);
+    }
+    if (RECV) {
+#pragma unroll
+      for (int u = 0; u < kLL128Unroll; u++) {
+        const int64_t r = r0 + (int64_t)u * nw;
+        if (r >= nRounds) break;
+        uint64_t spins = 0, start = 0;
+        for (;;) {
+          const bool ok = !flagLane || ((uint64_t)rv[u].z | ((uint64_t)rv[u].w << 32)) == rflag;
+          if (__all(ok)) break;
+          if ((++spins & 255) == 0) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (start == 0) start = now;
+            if (*R.comm->abortFlag ||
+                __hip_atomic_load(R.comm->errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                now - start > R.comm->spinTimeoutTicks) {
+              __hip_atomic_store(R.comm->errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              fail = true;
+              break;
+            }
+          }
+          __builtin_amdgcn_s_sleep(1);
+          rv[u] = ld16<kSys>(rslot, r * kLL128RoundWire + lane * 16);
+        }
+        if (fail) break;
+      }
+      if (fail) break;
+    }
+#pragma unroll
+    for (int u = 0; u < kLL128Unroll; u++) {
+      const int64_t r = r0 + (int64_t)u * nw;
+      if (r >= nRounds) break;
+      u32x4 acc;
+      if constexpr (SRC) {
+        acc = own[u];
+        if (Fn::kPreOp && preOp) acc = pack_preop(fn, acc);
+        if constexpr (RECV) acc = pack_reduce(fn, acc, rv[u]);  // own (+) recv, as the SIMPLE ring
+      } else {
+        acc = rv[u];
+      }
+      if (Fn::kPostOp && postOp) acc = pack_postop(fn, acc);
+      if constexpr (SEND) {
+        u32x4 o = acc;
+        if (flagLane) {
+          o.z = (uint32_t)sflag;
+          o.w = (uint32_t)(sflag >> 32);
+        }
+        st16<kSys>(sslot, r * kLL128RoundWire + lane * 16, o);
+      }
+      if constexpr (DST) ll128_st_piece<T, kNT>(dst, r * kLL128RoundData + dOff, dLen, nbytes, dstAl, acc);
+    }
+  }
+  if (fail) *R.shAbort = 1;
+  __syncthreads();  // every lane's reads of the receive slot are done
+  if (R.tid == 0 && RECV && !R.aborted()) st_sys(R.ch->prevSendHead, R.recvStep + 1);
+  if (SEND) R.sendStep++;
+  if (RECV) R.recvStep++;
+}
+
 __device__ __forceinline__ int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 __device__ __forceinline__ int64_t div_up(int64_t x, int64_t a) { return (x + a - 1) / a; }
 
@@ -163,11 +334,17 @@ __device__ __forceinline__ bool cbd_part(const RingWork& w, int c, int64_t* off,
 // 193-194); an empty step still hands over one (empty) slot, as the
 // reference's nelem <= 0 primitive calls do.  Sender and receiver of a chunk
 // always agree on its length, so they agree on the slice count.
-template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
+template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL, int PROTO = kProtoSimple>
 __device__ __forceinline__ void ring_step(RingCtx& r, const Fn& fn, const void* src, void* dst,
                                           int64_t nelem, bool postOp, int recvOff = 0,
                                           int sendOff = 0) {
   using T = typename Fn::EltType;
+  if constexpr (PROTO == kProtoLL128) {  // a whole chunk is one LL128 step
+    (void)recvOff;
+    (void)sendOff;
+    ll128_prim<Fn, RECV, SEND, SRC, DST>(r, fn, src, dst, nelem > 0 ? nelem : 0, SRC, postOp);
+    return;
+  }
   const int64_t slotElts = (int64_t)r.slotBytes / (int64_t)sizeof(T);
   const int64_t nSlices = nelem > 0 ? div_up(nelem, slotElts) : 1;
   for (int64_t s = 0; s < nSlices; s++) {
@@ -182,7 +359,7 @@ __device__ __forceinline__ void ring_step(RingCtx& r, const Fn& fn, const void* 
 // ----------------------------------------------------------------- AllReduce
 // all_reduce.h:12-83 (runRing): RS then AG within one kernel, chunk c of each
 // round finishing at ring position c.
-template <class Fn, int UNROLL>
+template <class Fn, int UNROLL, int PROTO = kProtoSimple>
 __device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
   using T = typename Fn::EltType;
   const int n = w.nRanks;
@@ -203,22 +380,22 @@ __device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int 
       return l < chunkCount ? (l < 0 ? 0 : l) : chunkCount;
     };
     int chunk = modRanks(ringIx + n - 1);  // step 0: send own chunk
-    ring_step<Fn, false, true, true, false, UNROLL>(r, fn, in + off_of(chunk), nullptr, len_of(chunk), false);
+    ring_step<Fn, false, true, true, false, UNROLL, PROTO>(r, fn, in + off_of(chunk), nullptr, len_of(chunk), false);
     for (int j = 2; j < n; ++j) {          // n-2 recv-reduce-send
       chunk = modRanks(ringIx + n - j);
-      ring_step<Fn, true, true, true, false, UNROLL>(r, fn, in + off_of(chunk), nullptr, len_of(chunk),
+      ring_step<Fn, true, true, true, false, UNROLL, PROTO>(r, fn, in + off_of(chunk), nullptr, len_of(chunk),
                                                      false);
     }
     chunk = ringIx;                         // final reduce: output + send
-    ring_step<Fn, true, true, true, true, UNROLL>(r, fn, in + off_of(chunk), out + off_of(chunk),
+    ring_step<Fn, true, true, true, true, UNROLL, PROTO>(r, fn, in + off_of(chunk), out + off_of(chunk),
                                                   len_of(chunk), true);
     for (int j = 1; j < n - 1; ++j) {      // n-2 recv-copy-send
       chunk = modRanks(ringIx + n - j);
-      ring_step<Fn, true, true, false, true, UNROLL>(r, fn, nullptr, out + off_of(chunk), len_of(chunk),
+      ring_step<Fn, true, true, false, true, UNROLL, PROTO>(r, fn, nullptr, out + off_of(chunk), len_of(chunk),
                                                      false);
     }
     chunk = modRanks(ringIx + 1);          // final recv
-    ring_step<Fn, true, false, false, true, UNROLL>(r, fn, nullptr, out + off_of(chunk), len_of(chunk),
+    ring_step<Fn, true, false, false, true, UNROLL, PROTO>(r, fn, nullptr, out + off_of(chunk), len_of(chunk),
                                                     false);
   }
 }
@@ -226,7 +403,7 @@ __device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int 
 // ------------------------------------------------------------- ReduceScatter
 // reduce_scatter.h:12-55: the chunk owned by rank ringRanks[k] starts at its
 // ring successor; the owner writes output[off] with postOp.
-template <class Fn, int UNROLL>
+template <class Fn, int UNROLL, int PROTO = kProtoSimple>
 __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
   using T = typename Fn::EltType;
   const int n = w.nRanks;
@@ -244,22 +421,22 @@ __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, 
     const int64_t nelem = chCount - eo < chunkCount ? chCount - eo : chunkCount;
     const int64_t dataOff = gridOff + eo;
     int rankDest = ringRanks[n - 1];
-    ring_step<Fn, false, true, true, false, UNROLL>(r, fn, in + dataOff + rankDest * count, nullptr, nelem,
+    ring_step<Fn, false, true, true, false, UNROLL, PROTO>(r, fn, in + dataOff + rankDest * count, nullptr, nelem,
                                                     false, 0, mis(rankDest));
     for (int j = 2; j < n; ++j) {
       rankDest = ringRanks[n - j];
-      ring_step<Fn, true, true, true, false, UNROLL>(r, fn, in + dataOff + rankDest * count, nullptr,
+      ring_step<Fn, true, true, true, false, UNROLL, PROTO>(r, fn, in + dataOff + rankDest * count, nullptr,
                                                      nelem, false, mis(rankDest), mis(rankDest));
     }
     rankDest = ringRanks[0];
-    ring_step<Fn, true, false, true, true, UNROLL>(r, fn, in + dataOff + rankDest * count, out + dataOff,
+    ring_step<Fn, true, false, true, true, UNROLL, PROTO>(r, fn, in + dataOff + rankDest * count, out + dataOff,
                                                    nelem, true, mis(rankDest), 0);
   }
 }
 
 // ----------------------------------------------------------------- AllGather
 // all_gather.h:12-83: byte copies (enqueue.cc:2400-2404 rewrites AG as int8).
-template <int UNROLL>
+template <int UNROLL, int PROTO = kProtoSimple>
 __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
   using Fn = FnCopy<uint8_t>;
   const Fn fn(0);
@@ -279,20 +456,20 @@ __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
     int rankDest = ringRanks[0];
     int64_t off = dataOff + rankDest * count;
     if (in + dataOff == out + off)
-      ring_step<Fn, false, true, true, false, UNROLL>(r, fn, in + dataOff, nullptr, nelem, false, 0,
+      ring_step<Fn, false, true, true, false, UNROLL, PROTO>(r, fn, in + dataOff, nullptr, nelem, false, 0,
                                                       mis(rankDest));
     else
-      ring_step<Fn, false, true, true, true, UNROLL>(r, fn, in + dataOff, out + off, nelem, false, 0,
+      ring_step<Fn, false, true, true, true, UNROLL, PROTO>(r, fn, in + dataOff, out + off, nelem, false, 0,
                                                      mis(rankDest));
     for (int j = 1; j < n - 1; ++j) {
       rankDest = ringRanks[n - j];
       off = dataOff + rankDest * count;
-      ring_step<Fn, true, true, false, true, UNROLL>(r, fn, nullptr, out + off, nelem, false, mis(rankDest),
+      ring_step<Fn, true, true, false, true, UNROLL, PROTO>(r, fn, nullptr, out + off, nelem, false, mis(rankDest),
                                                      mis(rankDest));
     }
     rankDest = ringRanks[1];
     off = dataOff + rankDest * count;
-    ring_step<Fn, true, false, false, true, UNROLL>(r, fn, nullptr, out + off, nelem, false, mis(rankDest),
+    ring_step<Fn, true, false, false, true, UNROLL, PROTO>(r, fn, nullptr, out + off, nelem, false, mis(rankDest),
                                                     0);
   }
 }

@@ -8,7 +8,7 @@
 
 #include "dispatch.hpp"
 #include "ring_launch.hpp"
-#if VCCL_PART == 0
+#if VCCL_PART == 0 || VCCL_PART == 3
 #include "ring.hpp"
 #elif VCCL_PART == 1
 #include "ll.hpp"
@@ -20,12 +20,19 @@
 #error "compile with -DVCCL_KT=<kernel element type>"
 #endif
 #ifndef VCCL_PART
-#error "compile with -DVCCL_PART=<0 ring | 1 LL | 2 direct>"
+#error "compile with -DVCCL_PART=<0 ring | 1 LL | 2 direct | 3 LL128 ring>"
 #endif
 
 namespace vccl {
 
-#if VCCL_PART == 0
+#if VCCL_PART == 0 || VCCL_PART == 3
+// PART 0: the SIMPLE ring; PART 3: the same schedules over LL128 FIFOs.
+constexpr int kPartProto = VCCL_PART == 3 ? kProtoLL128 : kProtoSimple;
+#if VCCL_PART == 3
+#define VCCL_RING_LAUNCH ring_launch_ll128
+#else
+#define VCCL_RING_LAUNCH ring_launch
+#endif
 
 // 512 threads per channel: the ring primitive (pipelined aligned copy +
 // realigning misaligned path, inlined per (recv, send, src, dst) shape) needs
@@ -35,17 +42,20 @@ namespace vccl {
 template <class Fn>
 constexpr int ring_unroll() { return IsF8<typename Fn::EltType>::value ? 2 : kRingUnroll; }
 
-template <int COLL, class Fn, int UNROLL>
+// PROTO is a template parameter of every function below, so the SIMPLE and
+// LL128 objects never define the same symbol differently.
+template <int COLL, class Fn, int UNROLL, int PROTO>
 __device__ __forceinline__ void ring_run(RingCtx& r, const Fn& fn, const RingWork& w) {
-  if constexpr (COLL == kCollAllReduce) ring_allreduce<Fn, UNROLL>(r, fn, w, blockIdx.x);
-  else if constexpr (COLL == kCollReduceScatter) ring_reducescatter<Fn, UNROLL>(r, fn, w, blockIdx.x);
-  else ring_allgather<UNROLL>(r, w, blockIdx.x);
+  if constexpr (COLL == kCollAllReduce) ring_allreduce<Fn, UNROLL, PROTO>(r, fn, w, blockIdx.x);
+  else if constexpr (COLL == kCollReduceScatter)
+    ring_reducescatter<Fn, UNROLL, PROTO>(r, fn, w, blockIdx.x);
+  else ring_allgather<UNROLL, PROTO>(r, w, blockIdx.x);
 }
 
 // One launch = 1 .. kRingMaxWorks calls (RingBatch, group aggregation): the
 // channel workgroup runs them in order.  The kernel argument is read through
 // scalar loads at any part index (no private copy).
-template <int COLL, class Fn, int UNROLL>
+template <int COLL, class Fn, int UNROLL, int PROTO>
 __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
   const RingWork& w = b.w;
   __shared__ int shAbort;
@@ -60,10 +70,12 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
   r.tid = threadIdx.x;
   r.nthreads = blockDim.x;
   r.slotBytes = w.slotBytes;
+  r.ll128Slot = w.ll128SlotBytes;
   r.shAbort = &shAbort;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
-  ring_run<COLL, Fn, UNROLL>(r, fn, w);
-  for (int i = 1; i < b.nParts; i++) ring_run<COLL, Fn, UNROLL>(r, fn, ring_work_with(w, b.more[i - 1]));
+  ring_run<COLL, Fn, UNROLL, PROTO>(r, fn, w);
+  for (int i = 1; i < b.nParts; i++)
+    ring_run<COLL, Fn, UNROLL, PROTO>(r, fn, ring_work_with(w, b.more[i - 1]));
   __syncthreads();
   if (threadIdx.x == 0) {
     ch->recvStep = r.recvStep;
@@ -72,14 +84,14 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
 }
 
 template <>
-hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingBatch& w, int nthreads,
-                                hipStream_t stream) {
+hipError_t VCCL_RING_LAUNCH<VCCL_KT>(int coll, int devOp, const RingBatch& w, int nthreads,
+                                     hipStream_t stream) {
   using T = typename KTypeOf<VCCL_KT>::T;
   hipError_t err = hipErrorInvalidValue;
   dim3 grid(w.w.nChannels), block(nthreads);
   if (coll == kCollAllGather) {
     if constexpr (VCCL_KT == K_U8) {
-      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, kRingUnroll>), grid, block, 0,
+      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, kRingUnroll, kPartProto>), grid, block, 0,
                          stream, w);
       return hipGetLastError();
     }
@@ -89,10 +101,10 @@ hipError_t ring_launch<VCCL_KT>(int coll, int devOp, const RingBatch& w, int nth
     if constexpr (std::is_same<Fn, FnCopy<T>>::value) {
       err = hipErrorInvalidValue;
     } else if (coll == kCollAllReduce) {
-      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, ring_unroll<Fn>()>), grid, block, 0, stream, w);
+      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, ring_unroll<Fn>(), kPartProto>), grid, block, 0, stream, w);
       err = hipGetLastError();
     } else if (coll == kCollReduceScatter) {
-      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, ring_unroll<Fn>()>), grid, block, 0, stream, w);
+      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, ring_unroll<Fn>(), kPartProto>), grid, block, 0, stream, w);
       err = hipGetLastError();
     }
   });

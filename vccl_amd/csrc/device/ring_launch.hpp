@@ -20,9 +20,18 @@ enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2 };
 constexpr int kRingUnroll = VCCL_RING_UNROLL;
 constexpr int kRingMaxThreads = 512;  // k_ring launch bound (ring_kernels.hip)
 
-// w.w.nChannels workgroups (the largest part's channelHi + 1).
+// w.w.nChannels workgroups (the largest part's channelHi + 1); the SIMPLE
+// ring, or the same schedules over LL128 FIFOs (separate objects).
 template <int K>
 hipError_t ring_launch(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream);
+template <int K>
+hipError_t ring_launch_ll128(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream);
+template <int K>
+inline hipError_t ring_launch_any(bool ll128, int coll, int devOp, const RingBatch& w, int nthreads,
+                                  hipStream_t stream) {
+  return ll128 ? ring_launch_ll128<K>(coll, devOp, w, nthreads, stream)
+               : ring_launch<K>(coll, devOp, w, nthreads, stream);
+}
 
 // One-hop LL collectives (ll.hpp): 256-thread workgroups, `grid` of them.
 // All-gather only in the K_U8 unit (byte copies).

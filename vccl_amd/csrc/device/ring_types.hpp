@@ -45,6 +45,12 @@ struct DevChannel {
   // Net connection only (null over xGMI): bytes of each posted slot, stored
   // before the tail so the proxy sends only what the step filled.
   uint32_t* sendSizes;
+  // LL128 FIFOs (ring.hpp prim_ll128): kSteps slots of 64-byte lines, local
+  // (receive) and next's (send); null when the comm has no LL128 buffers.
+  // Steps, credits (sendHead / prevSendHead) and the slot index are shared
+  // with the SIMPLE FIFO: a step is one slot of either protocol.
+  char* ll128Recv;
+  char* ll128Send;
   // persistent step counters (kernel reads at start, writes at end)
   uint64_t recvStep;
   uint64_t sendStep;
@@ -158,7 +164,18 @@ struct RingWork {
   int channelLo, channelHi;
   int64_t countLo, countMid, countHi;
   int64_t chunkLo, chunkMid, chunkHi;
+  // LL128 ring (proto = kProtoLL128): bytes per LL128 FIFO slot
+  int64_t ll128SlotBytes;
 };
+
+// Protocols of the ring kernels (nccl_common.h ids).
+enum : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2 };
+// LL128 wire format on gfx950 (ring.hpp prim_ll128): 64-byte lines of three
+// 16-byte data pieces + one {8-byte data, 8-byte flag} piece, one line per 4
+// lanes, 16 lines (1 KiB) per wave instruction carrying 896 data bytes.
+constexpr int kLL128LineBytes = 64;
+constexpr int kLL128RoundWire = 1024;
+constexpr int kLL128RoundData = 896;
 
 // Group aggregation (the reference's planner packing a group's collectives
 // into one plan, enqueue.cc:352-508 / :518-769, run by one kernel over its

@@ -87,11 +87,13 @@ struct PeerMap {               // what one rank published about itself
   hipIpcMemHandle_t llHandle;
   hipIpcMemHandle_t dBufHandle;
   hipIpcMemHandle_t dFlagHandle;
+  hipIpcMemHandle_t ll128Handle;
   char* fifoPtr;               // raw pointers (valid only in the owner process)
   char* flagPtr;
   char* llPtr;
   char* dBufPtr;
   char* dFlagPtr;
+  char* ll128Ptr;
 };
 
 struct UserRedOp {             // ncclRedOpCreatePreMulSum state (enqueue.cc:2528-2567)
@@ -117,6 +119,15 @@ struct ncclComm {
   int llLines = 0;             // lines per (parity, source) slot = llMaxBytes / 8
   size_t llMaxBytes = 0;       // largest all-reduce carried by LL
   std::vector<char*> llPeer;   // every rank's LL buffer mapped into this process
+  // LL128 ring (ring.hpp prim_ll128): nChannels x kSteps slots of
+  // ll128SlotBytes, uncached; VCCL's LL128 partition and chunk
+  // (ll128ChunkBytes of data per step, enqueue.cc:2027-2032) and thread count
+  // (NCCL_LL128_NTHREADS, tuning.cc:198-211) for the channel tuning.
+  char* ll128Buf = nullptr;
+  int64_t ll128SlotBytes = 0;
+  int64_t ll128StepBytes = 0;  // NCCL_LL128_BUFFSIZE / NCCL_STEPS (init.cc:617-633)
+  int ll128Threads = 640;
+  size_t ll128MinBytes = 0, ll128MaxBytes = 0;  // automatic LL128 window (0 = off)
   // two-shot direct all-reduce (direct.hpp): inbox [2 phases][nRanks][dRegionBytes]
   char* dBuf = nullptr;
   char* dFlags = nullptr;      // kDirectFlagBytes of epoch flags

@@ -309,13 +309,18 @@ struct CbdPlan {
   int64_t countLo, countMid, countHi;
   int64_t chunkLo, chunkMid, chunkHi;  // elements
 };
-// nThreads: maxThreads[RING][SIMPLE], i.e. NCCL_NTHREADS (tuning.cc:198-200;
-// the ring kernel's own block size here, comm->nThreads).
+// proto: kProtoSimple or kProtoLL128.  stepBytes: that protocol's FIFO step
+// (buffSize / NCCL_STEPS).  nThreads: maxThreads[RING][proto] — NCCL_NTHREADS
+// for SIMPLE (the ring kernel's own block size here, comm->nThreads),
+// NCCL_LL128_NTHREADS (640) for LL128 (tuning.cc:198-211).
 static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
-                            int64_t slotBytes, int64_t nThreads) {
+                            int proto, int64_t stepBytes, int64_t nThreads) {
   constexpr int64_t kMinTraffic = 16 << 10;         // enqueue.cc:528
-  constexpr int64_t kSimpleThreshold = 64;         // NCCL_SIMPLE_THREAD_THRESHOLD (comm.h:40)
-  constexpr int64_t kGrain = 512;                  // ncclProtoGrainSize(SIMPLE) (device.h:290-295)
+  // thread thresholds (comm.h:38-40): SIMPLE 64, LL128 8; grains
+  // ncclProtoGrainSize (device.h:290-295): SIMPLE 512, LL128 1920
+  const bool ll128 = proto == kProtoLL128;
+  const int64_t kSimpleThreshold = ll128 ? 8 : 64;
+  const int64_t kGrain = ll128 ? 1920 : 512;
   auto divUp = [](int64_t a, int64_t b) { return (a + b - 1) / b; };
   const int64_t tpb = coll == kAllReduce ? 2 : nRanks;  // ncclFuncTrafficPerByte (enqueue.cc:67-74)
   const int64_t nBytes = eltSize * (coll == kAllReduce ? count : (int64_t)nRanks * count);
@@ -361,15 +366,18 @@ static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks
   nCh = (p.countLo ? 1 : 0) + nMid + (cellsHi ? 1 : 0);
   p.channelLo = (int)channelId;
   p.channelHi = (int)(channelId + nCh - 1);
-  // RING / SIMPLE chunk: chunkSteps (4) FIFO steps of buffSize / NCCL_STEPS
-  // (= one slot here), rounded down to the 512 B grain; independent of size.
-  const int64_t chunkElts = (4 * slotBytes) / kGrain * kGrain / eltSize;
+  // RING chunk (calcCollChunking, enqueue.cc:2027-2032, 2093): SIMPLE =
+  // chunkSteps (4) FIFO steps of buffSize / NCCL_STEPS (= one slot here);
+  // LL128 = one step, 15/16 of it data; rounded down to the protocol grain;
+  // independent of size.
+  const int64_t chunkBytes = ll128 ? stepBytes / 16 * 15 : 4 * stepBytes;
+  const int64_t chunkElts = chunkBytes / kGrain * kGrain / eltSize;
   p.chunkLo = p.chunkMid = p.chunkHi = chunkElts;
   return p;
 }
 
 // The ring work of one call (its kernel element type and device op too).
-static ncclResult_t ring_work_of(const Task& t, RingWork* out, int* ktOut, int* devOpOut) {
+static ncclResult_t ring_work_of(const Task& t, bool ll128, RingWork* out, int* ktOut, int* devOpOut) {
   ncclComm* comm = t.comm;
   RingWork w{};
   w.comm = comm->devComm;
@@ -394,8 +402,10 @@ static ncclResult_t ring_work_of(const Task& t, RingWork* out, int* ktOut, int* 
   w.redArgPtr = t.argPtr;  // ncclScalarDevice: dereferenced by the kernel (nccl.h.in:255-262)
   w.redArgBytes = type_size(t.datatype);
   const int64_t esz = t.coll == kAllGather ? 1 : type_size(t.datatype);
-  const CbdPlan p = cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
-                                 comm->slotBytes, comm->nThreads);
+  const CbdPlan p = ll128 ? cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
+                                          kProtoLL128, comm->ll128StepBytes, comm->ll128Threads)
+                         : cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
+                                        kProtoSimple, comm->slotBytes, comm->nThreads);
   if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
     return ncclInternalError;
   w.channelLo = p.channelLo;
@@ -407,6 +417,7 @@ static ncclResult_t ring_work_of(const Task& t, RingWork* out, int* ktOut, int* 
   w.chunkMid = p.chunkMid;
   w.chunkHi = p.chunkHi;
   w.nChannels = p.channelHi + 1;  // idle channels above channelHi are not launched
+  w.ll128SlotBytes = ll128 ? comm->ll128SlotBytes : 0;
   *out = w;
   *ktOut = kt;
   *devOpOut = devOp;
@@ -414,18 +425,19 @@ static ncclResult_t ring_work_of(const Task& t, RingWork* out, int* ktOut, int* 
 }
 
 // 1 .. kRingMaxWorks ring calls of one comm with the same collective, kernel
-// type and op (ring_fusable) in one launch on ts[0].stream.
-static ncclResult_t launch_ring(const Task* ts, int nTasks) {
+// type and op (fusable) in one launch on ts[0].stream; SIMPLE or LL128.
+static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128) {
   const Task& t = ts[0];
   ncclComm* comm = t.comm;
   if (nTasks < 1 || nTasks > kRingMaxWorks) return ncclInternalError;
+  if (ll128 && !comm->ll128Buf) return ncclInternalError;
   RingBatch b{};
   int kt = -1, devOp = -1;
-  NCCLCHECK(ring_work_of(t, &b.w, &kt, &devOp));
+  NCCLCHECK(ring_work_of(t, ll128, &b.w, &kt, &devOp));
   for (int i = 1; i < nTasks; i++) {
     RingWork wi;
     int kti, opi;
-    NCCLCHECK(ring_work_of(ts[i], &wi, &kti, &opi));
+    NCCLCHECK(ring_work_of(ts[i], ll128, &wi, &kti, &opi));
     if (kti != kt || opi != devOp) return ncclInternalError;
     b.more[i - 1] = ring_part_of(wi);
     b.w.nChannels = std::max(b.w.nChannels, wi.nChannels);
@@ -435,15 +447,15 @@ static ncclResult_t launch_ring(const Task* ts, int nTasks) {
                    : t.coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
-    case K_U8: e = ring_launch<K_U8>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_U32: e = ring_launch<K_U32>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_U64: e = ring_launch<K_U64>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F16: e = ring_launch<K_F16>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F32: e = ring_launch<K_F32>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F64: e = ring_launch<K_F64>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_BF16: e = ring_launch<K_BF16>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F8E4M3: e = ring_launch<K_F8E4M3>(coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F8E5M2: e = ring_launch<K_F8E5M2>(coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_U8: e = ring_launch_any<K_U8>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_U32: e = ring_launch_any<K_U32>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_U64: e = ring_launch_any<K_U64>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F16: e = ring_launch_any<K_F16>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F32: e = ring_launch_any<K_F32>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F64: e = ring_launch_any<K_F64>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_BF16: e = ring_launch_any<K_BF16>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F8E4M3: e = ring_launch_any<K_F8E4M3>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_F8E5M2: e = ring_launch_any<K_F8E5M2>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
   }
   if (e != hipSuccess) {
     VWARN("ring kernel launch failed: %s", hipGetErrorString(e));
@@ -477,7 +489,7 @@ static int dev_coll(int coll) {
 // reduce-scatters' per-channel fold order (the ring's own, cbd_schedule).
 static CbdLite rs_cbd(const ncclComm* comm, const Task& t) {
   const CbdPlan p = cbd_schedule(kReduceScatter, (int64_t)t.count, type_size(t.datatype), comm->nRanks,
-                                 comm->nChannels, comm->slotBytes, comm->nThreads);
+                                 comm->nChannels, kProtoSimple, comm->slotBytes, comm->nThreads);
   return CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)t.count};
 }
 
@@ -570,8 +582,8 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
     shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
     // the ring's partition of this bucket: phase 2 folds every element in the
     // order VCCL's ring all-reduce gives it on these channels (ar_chunk_of)
-    const CbdPlan p = cbd_schedule(kAllReduce, count, esz, n, comm->nChannels, comm->slotBytes,
-                                   comm->nThreads);
+    const CbdPlan p = cbd_schedule(kAllReduce, count, esz, n, comm->nChannels, kProtoSimple,
+                                   comm->slotBytes, comm->nThreads);
     w.cbd = CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, count};
     w.arChunk = p.chunkLo;
   } else {
@@ -635,10 +647,12 @@ static ncclResult_t launch_direct(const Task* ts, int nTasks) {
 // larger ones the SIMPLE ring.  NCCL_ALGO / NCCL_PROTO force one: Ring/SIMPLE
 // -> ring; Tree/LL -> LL where it fits; LL128/Direct -> direct where it
 // fits; anything that does not fit falls through to the ring.
-enum { kAlgoRing = 0, kAlgoLL = 1, kAlgoDirect = 2 };
+enum { kAlgoRing = 0, kAlgoLL = 1, kAlgoDirect = 2, kAlgoRingLL128 = 3 };
 static int choose_algo(const Task& t) {
   const ncclComm* c = t.comm;
   if (c->nRanks < 2 || c->algoForce == 1) return kAlgoRing;
+  // NCCL_PROTO=LL128 (or vcclCommSetAlgo): the LL128 ring for every size
+  if (c->algoForce == 4) return c->ll128Buf ? kAlgoRingLL128 : kAlgoRing;
   const size_t esz = (size_t)type_size(t.datatype);
   bool llFits, directFits;
   if (t.coll == kAllReduce) {
@@ -660,6 +674,13 @@ static int choose_algo(const Task& t) {
   // peers)
   if (c->algoForce == 3) return c->dPeers && c->nRanks <= kDirectMaxRanks ? kAlgoDirect : kAlgoRing;
   if (llFits) return kAlgoLL;
+  // VCCL_LL128=1: the LL128 ring over its window (the bucket, as the tuner
+  // sizes it), ahead of the direct path
+  {
+    const size_t bytes = t.count * esz * (t.coll == kAllReduce ? 1 : (size_t)c->nRanks);
+    if (c->ll128Buf && c->ll128MaxBytes && bytes >= c->ll128MinBytes && bytes <= c->ll128MaxBytes)
+      return kAlgoRingLL128;
+  }
   if (directFits) return kAlgoDirect;
   return kAlgoRing;
 }
@@ -689,7 +710,8 @@ static ncclResult_t launch_task(const Task& t) {
   ncclResult_t r = stream_order(t.comm, t.stream, &cs);
   if (r == ncclSuccess) {
     const int algo = choose_algo(t);
-    r = algo == kAlgoLL ? launch_ll(&t, 1) : algo == kAlgoDirect ? launch_direct(&t, 1) : launch_ring(&t, 1);
+    r = algo == kAlgoLL ? launch_ll(&t, 1)
+        : algo == kAlgoDirect ? launch_direct(&t, 1) : launch_ring(&t, 1, algo == kAlgoRingLL128);
   }
   if (r == ncclSuccess) r = stream_mark(t.comm, t.stream, cs);
   t.comm->opCount++;
@@ -738,7 +760,8 @@ static ncclResult_t launch_fused(const std::vector<Task>& ts, int algo) {
   if (r == ncclSuccess) {
     const int n = (int)ts.size();
     r = algo == kAlgoLL ? launch_ll(ts.data(), n)
-        : algo == kAlgoDirect ? launch_direct(ts.data(), n) : launch_ring(ts.data(), n);
+        : algo == kAlgoDirect ? launch_direct(ts.data(), n)
+                              : launch_ring(ts.data(), n, algo == kAlgoRingLL128);
   }
   if (r == ncclSuccess) r = stream_mark(comm, s0, cs);
   const hipEvent_t done = stream_last_event(comm, cs);
@@ -1015,20 +1038,22 @@ extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count
   t.count = count;
   t.datatype = datatype;
   const int a = choose_algo(t);
-  *algo = a == kAlgoLL ? vcclAlgoLL : a == kAlgoDirect ? vcclAlgoDirect : vcclAlgoRing;
+  *algo = a == kAlgoLL ? vcclAlgoLL
+          : a == kAlgoDirect ? vcclAlgoDirect : a == kAlgoRingLL128 ? vcclAlgoLL128 : vcclAlgoRing;
   return ncclSuccess;
 }
 
 extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition(
-    int coll, size_t count, ncclDataType_t datatype, int nRanks, int nChannels, size_t slotBytes,
-    int nThreads, int64_t* out) {
+    int coll, size_t count, ncclDataType_t datatype, int nRanks, int nChannels, int proto,
+    size_t stepBytes, int nThreads, int64_t* out) {
   if (!out || coll < 0 || coll > 2 || type_size(datatype) < 1 || nRanks < 1 ||
-      nChannels < 1 || nChannels > kMaxChannels || count == 0 || slotBytes < 4096 || nThreads < 64)
+      nChannels < 1 || nChannels > kMaxChannels || count == 0 || stepBytes < 4096 || nThreads < 64 ||
+      (proto != kProtoSimple && proto != kProtoLL128))
     return ncclInvalidArgument;
   const int c = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : kAllGather;
   const int64_t esz = c == kAllGather ? 1 : type_size(datatype);
   const int64_t cnt = c == kAllGather ? (int64_t)count * type_size(datatype) : (int64_t)count;
-  const CbdPlan p = cbd_schedule(c, cnt, esz, nRanks, nChannels, (int64_t)slotBytes, nThreads);
+  const CbdPlan p = cbd_schedule(c, cnt, esz, nRanks, nChannels, proto, (int64_t)stepBytes, nThreads);
   const int64_t v[8] = {p.channelLo, p.channelHi, p.countLo, p.countMid,
                         p.countHi,   p.chunkLo,   p.chunkMid, p.chunkHi};
   memcpy(out, v, sizeof(v));
@@ -1042,8 +1067,8 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingChunkOf(
       count == 0 || i >= count || slotBytes < 4096 || nThreads < 64)
     return ncclInvalidArgument;
   const int64_t esz = type_size(datatype);
-  const CbdPlan p = cbd_schedule(kAllReduce, (int64_t)count, esz, nRanks, nChannels, (int64_t)slotBytes,
-                                 nThreads);
+  const CbdPlan p = cbd_schedule(kAllReduce, (int64_t)count, esz, nRanks, nChannels, kProtoSimple,
+                                 (int64_t)slotBytes, nThreads);
   const CbdLite cbd{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)count};
   int k;
   int64_t end;
@@ -1060,6 +1085,7 @@ extern "C" ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo) {
     case vcclAlgoRing: comm->algoForce = 1; return ncclSuccess;
     case vcclAlgoLL: comm->algoForce = 2; return ncclSuccess;
     case vcclAlgoDirect: comm->algoForce = 3; return ncclSuccess;
+    case vcclAlgoLL128: comm->algoForce = 4; return ncclSuccess;  // SIMPLE ring without LL128 buffers
   }
   return ncclInvalidArgument;
 }

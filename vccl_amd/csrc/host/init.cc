@@ -111,6 +111,8 @@ static void free_resources(ncclComm* c) {
   if (c->flagBuf) (void)hipFree(c->flagBuf);
   if (c->llBuf) (void)hipFree(c->llBuf);
   c->llBuf = nullptr;
+  if (c->ll128Buf) (void)hipFree(c->ll128Buf);
+  c->ll128Buf = nullptr;
   if (c->dBuf) (void)hipFree(c->dBuf);
   if (c->dFlags) (void)hipFree(c->dFlags);
   if (c->dPeers) (void)hipFree(c->dPeers);
@@ -135,12 +137,12 @@ static void free_resources(ncclComm* c) {
 }
 
 // Map a peer's buffer into this process/device.
-enum { kMapFifo = 0, kMapFlag = 1, kMapLL = 2, kMapDirect = 3, kMapDirectFlag = 4 };
+enum { kMapFifo = 0, kMapFlag = 1, kMapLL = 2, kMapDirect = 3, kMapDirectFlag = 4, kMapLL128 = 5 };
 static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, int which,
                              char** out) {
-  char* const raws[] = {p.fifoPtr, p.flagPtr, p.llPtr, p.dBufPtr, p.dFlagPtr};
+  char* const raws[] = {p.fifoPtr, p.flagPtr, p.llPtr, p.dBufPtr, p.dFlagPtr, p.ll128Ptr};
   const hipIpcMemHandle_t* const handles[] = {&p.fifoHandle, &p.flagHandle, &p.llHandle,
-                                              &p.dBufHandle, &p.dFlagHandle};
+                                              &p.dBufHandle, &p.dFlagHandle, &p.ll128Handle};
   char* raw = raws[which];
   const hipIpcMemHandle_t& handle = *handles[which];
   if (p.pid == me.pid && p.hostHash == me.hostHash) {
@@ -201,8 +203,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     const char* proto = getenv("NCCL_PROTO");
     auto has = [](const char* s, const char* w) { return s && strcasestr(s, w) != nullptr; };
     if (has(proto, "LL") || has(algo, "tree")) c->algoForce = 2;
-    // LL128's slot (the mid-range protocol) is the two-shot direct path here
-    if (has(proto, "LL128") || has(algo, "direct")) c->algoForce = 3;
+    if (has(algo, "direct")) c->algoForce = 3;
+    if (has(proto, "LL128")) c->algoForce = 4;  // the LL128 ring (ring.hpp prim_ll128)
     if (has(proto, "simple") || (has(algo, "ring") && !has(algo, "tree"))) c->algoForce = 1;
   }
   // Threads per ring channel (NCCL_NTHREADS, tuning.cc:198-200): 256 or 512
@@ -310,6 +312,30 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       c->directMaxBytes = c->directRsAgMaxBytes = 0;
     }
   }
+  if (n > 1) {
+    // LL128 ring buffers: with NCCL_PROTO=LL128, or VCCL_LL128=1 (the
+    // automatic window VCCL_LL128_MIN..MAX, default 64 KiB - 8 MiB: the range
+    // VCCL's tuner gives LL128, enqueue.cc:2032).  VCCL's LL128 step
+    // (NCCL_LL128_BUFFSIZE / 8, default 120 x 640 x 8 x 8 B / 8 = 614,400 B)
+    // carries 15/16 of it as data, rounded to the 1,920 B grain: 576,000 B per
+    // chunk; the slot holds that many data bytes in 64-byte lines of 56.
+    const bool want = c->algoForce == 4 || param_int("LL128", 0) != 0;
+    if (want) {
+      c->ll128StepBytes = std::max<int64_t>(param_int("LL128_BUFFSIZE", 120 * 640 * kSteps * 8) / kSteps, 1920 * 16);
+      c->ll128Threads = (int)std::max<int64_t>(param_int("LL128_NTHREADS", 640), 64);
+      const int64_t chunk = c->ll128StepBytes / 16 * 15 / 1920 * 1920;
+      c->ll128SlotBytes = (chunk + kLL128RoundData - 1) / kLL128RoundData * kLL128RoundWire;
+      const size_t bytes = (size_t)c->nChannels * kSteps * c->ll128SlotBytes;
+      NCCLCHECK(alloc_uncached((void**)&c->ll128Buf, bytes));
+      HIPCHECK(hipMemset(c->ll128Buf, 0, bytes));
+      HIPCHECK(hipIpcGetMemHandle(&me.ll128Handle, c->ll128Buf));
+      me.ll128Ptr = c->ll128Buf;
+      if (param_int("LL128", 0) != 0) {
+        c->ll128MinBytes = (size_t)param_int("LL128_MIN", 64 << 10);
+        c->ll128MaxBytes = (size_t)param_int("LL128_MAX", 8 << 20);
+      }
+    }
+  }
   if (n > 1) NCCLCHECK(net_listen(c, &me));
   VINFO("rank %d: exchange peer info", c->rank);
   c->peers.assign(n, PeerMap{});
@@ -333,6 +359,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // through the proxy, a few are enough (NCCL's net defaults use 2-4).
     c->llMaxBytes = c->llRsAgMaxBytes = 0;
     c->directMaxBytes = c->directRsAgMaxBytes = 0;
+    c->ll128MinBytes = c->ll128MaxBytes = 0;
+    if (c->algoForce == 4) c->algoForce = 1;  // LL128 lines need the xGMI mesh: SIMPLE
     c->nChannels = std::max(1, std::min(c->nChannels, (int)param_int("NET_NCHANNELS", 8)));
     VINFO("rank %d: inter-node ring through the net proxy, %d channels", c->rank, c->nChannels);
   }
@@ -436,8 +464,16 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
         else NCCLCHECK(map_peer(c, me, c->peers[r], kMapLL, &c->llPeer[r]));
       }
     }
+    std::vector<char*> ll128Of(n, nullptr);
+    if (c->ll128Buf && !anyNet) {
+      for (int r = 0; r < n; r++) {
+        if (r == c->rank) ll128Of[r] = c->ll128Buf;
+        else NCCLCHECK(map_peer(c, me, c->peers[r], kMapLL128, &ll128Of[r]));
+      }
+    }
     std::vector<DevChannel> chans(c->nChannels);
     const size_t fifoPerCh = (size_t)kSteps * slot_stride(c->slotBytes);
+    const size_t ll128PerCh = (size_t)kSteps * c->ll128SlotBytes;
     for (int ch = 0; ch < c->nChannels; ch++) {
       const auto& ring = rings[ch % nRings];
       int pos = (int)(std::find(ring.begin(), ring.end(), c->rank) - ring.begin());
@@ -457,6 +493,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       d.sendHead = flag(c->rank, 1);
       d.recvStep = d.sendStep = 0;
       d.sendSizes = nullptr;
+      d.ll128Recv = ll128Of[c->rank] ? ll128Of[c->rank] + ch * ll128PerCh : nullptr;
+      d.ll128Send = ll128Of[next] ? ll128Of[next] + ch * ll128PerCh : nullptr;
       // a net end's pointers are set by net_connect below
       if (netPeer[prev]) {
         d.recvFifo = nullptr;

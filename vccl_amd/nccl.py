@@ -44,7 +44,7 @@ EXPORTED = [
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
 ]
-ALGO_NAMES = {0: "ring", 1: "ll", 2: "direct", 3: "one_rank"}
+ALGO_NAMES = {0: "ring", 1: "ll", 2: "direct", 3: "one_rank", 4: "ll128"}
 
 
 class VcclError(RuntimeError):
@@ -104,7 +104,7 @@ def lib() -> ctypes.CDLL:
         "vcclKernelTypeOf": [c_int, c_int],
         "vcclBootstrapAllGather": [ctypes.POINTER(ncclUniqueId), c_int, c_int, vp, c_size],
         "vcclCommSetFences": [vp, c_int],
-        "vcclRingPartition": [c_int, c_size, c_int, c_int, c_int, c_size, c_int,
+        "vcclRingPartition": [c_int, c_size, c_int, c_int, c_int, c_int, c_size, c_int,
                               ctypes.POINTER(ctypes.c_int64)],
         "vcclCommDebugSetEpochs": [vp, ctypes.c_uint32, ctypes.c_uint32],
         "vcclRingChunkOf": [c_size, c_int, c_int, c_int, c_size, c_int, c_size,
@@ -172,13 +172,18 @@ def kernel_type_of(dev_op: int, dtype: int) -> int:
     return lib().vcclKernelTypeOf(dev_op, dtype)
 
 
+PROTO_LL128, PROTO_SIMPLE = 1, 2
+
+
 def ring_partition(coll: int, count: int, dtype: int, nranks: int, nchannels: int,
-                   slot_bytes: int, nthreads: int = 512) -> tuple[int, ...]:
+                   slot_bytes: int, nthreads: int = 512, proto: int = PROTO_SIMPLE) -> tuple[int, ...]:
     """vcclRingPartition: (channelLo, channelHi, countLo, countMid, countHi,
     chunkLo, chunkMid, chunkHi) of the ring's cbd partition (host only);
-    nthreads = NCCL_NTHREADS (the ring kernel's block size)."""
+    slot_bytes = the protocol's FIFO step, nthreads = NCCL_NTHREADS (SIMPLE)
+    or NCCL_LL128_NTHREADS (LL128)."""
     out = (ctypes.c_int64 * 8)()
-    check(lib().vcclRingPartition(coll, count, dtype, nranks, nchannels, slot_bytes, nthreads, out),
+    check(lib().vcclRingPartition(coll, count, dtype, nranks, nchannels, proto, slot_bytes, nthreads,
+                                  out),
           "vcclRingPartition")
     return tuple(out)
 
@@ -275,7 +280,7 @@ class Comm:
         return ALGO_NAMES[a.value]
 
     def set_algo(self, algo: str | None):
-        """vcclCommSetAlgo: force "ring" | "ll" | "direct" for later calls; None = automatic."""
+        """vcclCommSetAlgo: force "ring" | "ll" | "direct" | "ll128" for later calls; None = automatic."""
         code = -1 if algo is None else {v: k for k, v in ALGO_NAMES.items()}[algo]
         check(lib().vcclCommSetAlgo(self.handle, code), "vcclCommSetAlgo")
 
