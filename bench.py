@@ -126,7 +126,7 @@ def bench_reduce_copy(args):
     achieved = bytes_per / avg_kern_s / 1e9
     value = bytes_per * args.steps / wall / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("reduce_copy", bytes_per),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": "k_reduce_copy<FnSum<float>,2,1>", "algorithmic_bytes_per_launch": bytes_per,
             "avg_launch_us": round(avg_kern_s * 1e6, 2), "event_span_launches": ev_launches,
             "single_launch_us_median": round(float(np.median(kern_ms)) * 1e3, 2)}
@@ -139,6 +139,17 @@ def bench_reduce_copy(args):
                       "bytes_per_buffer": n * 4, "n_srcs": 2, "n_dsts": 1,
                       "launch": cfg or "library default"},
            "roofline": roof, "preroll": preroll}
+    # HBM traffic of the same kernel measured live on this box (PMC passes in
+    # child processes); the committed summary only when that is impossible
+    if not args.no_pmc_live:
+        live, why = _pmc_live(bytes_per)
+        if live is not None:
+            roof["traffic"] = live["hbm_bytes_per_launch"]
+            roof["traffic_detail"] = live
+        else:
+            roof["traffic"] = _pmc_traffic("reduce_copy", bytes_per)
+            roof["traffic_detail"] = {"source": "committed profiles/pmc_traffic.json",
+                                      "live_error": why}
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(n)
     if not args.no_extras:
@@ -232,6 +243,54 @@ def bench_one_rank_latency(iters=1000):
     res["bitwise_equal"] = bool(torch.equal(x.view(torch.int32), y.view(torch.int32)))
     comm.destroy()
     return res
+
+
+PMC_KERNEL = "k_reduce_copy<vccl::FnSum<float>, 2, 1,"
+
+
+def _pmc_live(algo_bytes, timeout_s=120):
+    """HBM bytes per launch of the headline kernel measured on THIS box: two
+    rocprofv3 `--pmc` passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one
+    pass on gfx950), kernel trace only, each over a short child run of this
+    same benchmark (5 launches after 2, no CPU leg / extras / pre-roll) under
+    its own hard time limit; FETCH_SIZE doubled and both KiB x 1024 as
+    MI355X_MICROARCH.md §HBM prescribes.  Returns a dict, or None with the
+    reason when the profiler is unavailable or a pass fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("rocprofv3") is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="vccl_pmc_")
+        cmd = ["timeout", "-s", "KILL", str(timeout_s), "rocprofv3", "--pmc", counter,
+               "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+               os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2", "--no-cpu",
+               "--no-extras", "--no-pmc-live", "--preroll-s", "0"]
+        try:
+            p = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp",
+                               env={**os.environ, "TMPDIR": "/tmp"}, timeout=timeout_s + 30)
+        except subprocess.TimeoutExpired:
+            return None, f"{counter} pass timed out"
+        if p.returncode != 0:
+            return None, f"{counter} pass rc {p.returncode}: {(p.stderr or '')[-300:]}"
+        got = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if PMC_KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    got.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not got:
+            return None, f"no {counter} samples for {PMC_KERNEL}"
+        vals[counter] = sum(got) / len(got)
+    hbm = int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024)
+    return {"hbm_bytes_per_launch": hbm, "traffic_over_algorithmic": round(hbm / algo_bytes, 4),
+            "fetch_kib_raw": vals["FETCH_SIZE"], "write_kib": vals["WRITE_SIZE"],
+            "method": "live rocprofv3 --pmc, separate FETCH_SIZE / WRITE_SIZE passes on this box; "
+                      "FETCH_SIZE x2 (gfx950), KiB x1024"}, None
 
 
 def _pmc_traffic(workload, algo_bytes):
@@ -400,6 +459,9 @@ def _dist_setup():
         os.close(saved)
     obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
+    # LL128 ring buffers for the mid-range rows (the automatic choice is
+    # unchanged: VCCL_LL128_ALLOC only allocates them)
+    os.environ.setdefault("VCCL_LL128_ALLOC", "1")
     comm = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank)
     return dist, rank, world, comm
 
@@ -771,6 +833,9 @@ def bench_allreduce(args):
         for algo in ("ring", "direct"):
             for S in (64 << 20, head):
                 plan[f"ar_{algo}_{S}"] = ("ar", {"nbytes": S, "algo": algo})
+        for algo in MID_ALGOS:
+            for S in MID_SIZES:
+                plan[f"ar_mid_{algo}_{S}"] = ("ar", {"nbytes": S, "algo": algo})
         for S in EXTRA_GROUP_SIZES:
             plan[f"group16_{S}"] = ("group", {"nbytes": S, "k": 16})
         plan[f"rs_ag_bf16_{args.rs_ag_bytes}"] = ("rs_ag", {"nbytes": args.rs_ag_bytes})
@@ -833,6 +898,9 @@ EXTRA_F32_SIZES = (8, 1 << 10, 8 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20)
 EXTRA_F16_SIZES = (8, 1 << 10, 16 << 10, 128 << 10)
 EXTRA_GROUP_SIZES = (4 << 10, 32 << 10)
 EXTRA_RSAG_SIZES = (64 << 10, 1 << 20, 8 << 20)  # whole bucket (n blocks), f32
+# the mid range VCCL's tuner gives LL128 (enqueue.cc:2032): every path forced
+MID_SIZES = (256 << 10, 1 << 20, 8 << 20)
+MID_ALGOS = ("ring", "direct", "ll128")
 
 
 def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
@@ -903,6 +971,16 @@ def bench_extras(dist, comm, rank, world, args):
                 for S, st in ((64 << 20, 10), (args.bytes or (1 << 30), 5))]
     except Exception as e:  # noqa: BLE001
         ex["by_algo_error"] = repr(e)
+    finally:
+        comm.set_algo(None)
+    try:  # the mid range (64 KiB - 8 MiB: LL128's slot in VCCL's tuner), each path forced
+        ex["allreduce_f32_mid_by_algo"] = {}
+        for algo in MID_ALGOS:
+            comm.set_algo(algo)
+            ex["allreduce_f32_mid_by_algo"][algo] = [
+                _ar_size_row(dist, comm, rank, world, S, "f32", 20, 3) for S in MID_SIZES]
+    except Exception as e:  # noqa: BLE001
+        ex["mid_by_algo_error"] = repr(e)
     finally:
         comm.set_algo(None)
     try:
@@ -989,6 +1067,7 @@ def main():
     ap.add_argument("--no-peer", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-initall", action="store_true")
+    ap.add_argument("--no-pmc-live", action="store_true")
     ap.add_argument("--rs-ag-bytes", type=int, default=4 << 30)
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)

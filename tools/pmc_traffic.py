@@ -20,7 +20,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
-KERNEL = "k_reduce_copy<vccl::FnSum<float>, 2, 1"
+KERNEL = "k_reduce_copy<vccl::FnSum<float>, 2, 1,"
 
 
 def run_pass(counter):

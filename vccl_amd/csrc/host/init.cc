@@ -319,7 +319,9 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // (NCCL_LL128_BUFFSIZE / 8, default 120 x 640 x 8 x 8 B / 8 = 614,400 B)
     // carries 15/16 of it as data, rounded to the 1,920 B grain: 576,000 B per
     // chunk; the slot holds that many data bytes in 64-byte lines of 56.
-    const bool want = c->algoForce == 4 || param_int("LL128", 0) != 0;
+    // (VCCL_LL128_ALLOC=1: the buffers only — vcclCommSetAlgo may pick the
+    // LL128 ring per call, the automatic choice is unchanged)
+    const bool want = c->algoForce == 4 || param_int("LL128", 0) != 0 || param_int("LL128_ALLOC", 0) != 0;
     if (want) {
       c->ll128StepBytes = std::max<int64_t>(param_int("LL128_BUFFSIZE", 120 * 640 * kSteps * 8) / kSteps, 1920 * 16);
       c->ll128Threads = (int)std::max<int64_t>(param_int("LL128_NTHREADS", 640), 64);
