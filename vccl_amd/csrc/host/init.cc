@@ -517,6 +517,10 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   NCCLCHECK(bootstrap_barrier(c->bootstrap));
   VINFO("comm %p rank %d/%d dev %d: %d channels x %d threads, slot %d B", (void*)c, c->rank, n,
         c->device, c->nChannels, c->nThreads, c->slotBytes);
+  VINFO("rank %d: thresholds LL %zu, LL RS/AG %zu, direct %zu, direct RS/AG %zu, LL128 [%zu, %zu]%s, "
+        "algo force %d", c->rank, c->llMaxBytes, c->llRsAgMaxBytes, c->directMaxBytes,
+        c->directRsAgMaxBytes, c->ll128MinBytes, c->ll128MaxBytes, c->ll128Buf ? " (buffers)" : "",
+        c->algoForce);
   return ncclSuccess;
 }
 
