@@ -918,6 +918,40 @@ def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
             "busbw": round(algbw * 2 * (world - 1) / world, 3), "algo": comm.coll_algo(0, n, code)}
 
 
+def _ar_graph_row(dist, comm, rank, world, S, dtype="f16", calls=50, replays=10):
+    """Config 5 in graph mode (nccl-tests ``-G``): ``calls`` all-reduces of S
+    bytes captured into one HIP graph, replayed ``replays`` times; us per call
+    = replay time / calls (no per-call launch cost).  The replayed output is
+    compared bitwise with an eager call of the same algorithm."""
+    tdt, code = {"f32": (torch.float32, nccl.ncclFloat32), "f16": (torch.float16, nccl.ncclFloat16)}[dtype]
+    esz = torch.tensor([], dtype=tdt).element_size()
+    n = max(1, S // esz)
+    g = torch.Generator(device="cuda").manual_seed(3000 + rank)
+    x = (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt)
+    y, ref = torch.empty_like(x), torch.empty_like(x)
+    cs = torch.cuda.Stream()
+    cs.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(cs):
+        graph.capture_begin(capture_error_mode="relaxed")
+        for _ in range(calls):
+            comm.all_reduce(x.data_ptr(), y.data_ptr(), n, code, nccl.ncclSum, cs.cuda_stream)
+        graph.capture_end()
+    torch.cuda.synchronize()
+    dt = _time_coll(dist, graph.replay, replays, 2)
+    sp = torch.cuda.current_stream().cuda_stream
+    comm.all_reduce(x.data_ptr(), ref.data_ptr(), n, code, nccl.ncclSum, sp)
+    torch.cuda.synchronize()
+    ok = _all_ok(dist, bool(torch.equal(y.view(torch.int16 if esz == 2 else torch.int32),
+                                        ref.view(torch.int16 if esz == 2 else torch.int32))))
+    del graph
+    us = dt / (replays * calls) * 1e6
+    return {"bytes": n * esz, "us": round(us, 2), "calls_per_graph": calls,
+            "busbw": round(n * esz / us / 1e3 * 2 * (world - 1) / world, 3),
+            "algo": comm.coll_algo(0, n, code), "matches_eager": ok}
+
+
 def _group_row(dist, comm, rank, world, S, k, steps=20, warmup=3):
     """k all-reduces of S bytes (fp32 sum): issued one by one vs inside one
     ncclGroupStart/End, where runs of small buckets are fused into one launch."""
@@ -957,6 +991,10 @@ def bench_extras(dist, comm, rank, world, args):
                                   for S in EXTRA_F16_SIZES]
     except Exception as e:  # noqa: BLE001 - reported, not fatal to the headline
         ex["allreduce_error"] = repr(e)
+    try:  # config 5 without per-call launch cost (nccl-tests -G: HIP graph replay)
+        ex["allreduce_f16_ll_graph"] = [_ar_graph_row(dist, comm, rank, world, S) for S in EXTRA_F16_SIZES]
+    except Exception as e:  # noqa: BLE001
+        ex["graph_error"] = repr(e)
     try:
         ex["group_fusion_f32"] = [_group_row(dist, comm, rank, world, S, 16) for S in EXTRA_GROUP_SIZES]
     except Exception as e:  # noqa: BLE001

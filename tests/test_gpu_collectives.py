@@ -206,7 +206,7 @@ def test_multi_process_ranks(n, geom):
         env.update(VCCL_ALLOW_SHARED_DEVICE="1", VCCL_LL_MAX_BLOCKS="32",
                    VCCL_DIRECT_MAX_BLOCKS="16", VCCL_NTHREADS="256", VCCL_CHANNELS_PER_RING="2")
         nch, slot = _ring.n_channels(n, per_ring=2), 512 << 10
-        ll_max, direct_max, chunk = 128 << 10, 64 << 20, 16 << 20
+        ll_max, direct_max, chunk = 128 << 10, 8 << 20, 16 << 20
         nthreads = 256  # NCCL_NTHREADS steers VCCL's channel tuning too
     else:  # library defaults (2 ranks x 32 channels x 1024 threads fit on one GPU)
         for k in TEST_GEOM:
@@ -214,7 +214,7 @@ def test_multi_process_ranks(n, geom):
         env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         nch, slot = _ring.n_channels(n), 512 << 10
         ll_max = (64 << 10) if n <= 2 else (128 << 10)
-        direct_max, chunk = (64 << 20) if n >= 4 else 0, 16 << 20
+        direct_max, chunk = (8 << 20) if n >= 4 else 0, 16 << 20
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
                                    str(r), str(n), "0", hexid, d], env=env,

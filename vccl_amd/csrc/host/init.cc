@@ -269,15 +269,17 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // Inbox of the direct collectives (direct.hpp): 2 phases x n regions of
     // one shard of a VCCL_DIRECT_CHUNK_BYTES chunk each, plus the epoch
     // flags.  Larger buckets stream through the inbox chunk by chunk.
-    // Two-shot direct all-reduce up to VCCL_DIRECT_THRESHOLD (64 MiB from 4
+    // Two-shot direct all-reduce up to VCCL_DIRECT_THRESHOLD (8 MiB from 4
     // ranks), the SIMPLE ring above: the ring, with VCCL's own partition, is
     // the north-star path and keeps VCCL's fold order for large buckets; the
     // direct path's two hops (vs 2(n-1)) matter where the per-hop latency
     // does, i.e. small and mid buckets at n >= 4 (profiles/r02e/lat_n4.log,
-    // lat_n8.log).  At n = 2 the ring IS two hops and its 48 channels beat
-    // the direct path at every size above LL (profiles/r02/lat_n2.log).
+    // lat_n8.log).  Above 8 MiB the ring's continuous pipeline wins (4 ranks:
+    // 16 MiB 111 vs 121 us, 64 MiB 330 vs 504 us, profiles/r03g/lat_n4.log).
+    // At n = 2 the ring IS two hops and its 48 channels beat the direct path
+    // at every size above LL (profiles/r02/lat_n2.log).
     c->directMaxBytes = n <= kDirectMaxRanks
-                            ? (size_t)param_int("DIRECT_THRESHOLD", n >= 4 ? (int64_t)64 << 20 : 0)
+                            ? (size_t)param_int("DIRECT_THRESHOLD", n >= 4 ? (int64_t)8 << 20 : 0)
                             : 0;
     c->directMaxBlocks = (int)std::max<int64_t>(
         1, std::min<int64_t>(param_int("DIRECT_MAX_BLOCKS", 64), kDirectMaxBlocks));
@@ -294,7 +296,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // n = 8 the one-hop paths lead at <= 1 MiB, profiles/r02e/lat_n8.log.)
     c->directRsAgMaxBytes =
         n <= kDirectMaxRanks
-            ? (size_t)param_int("DIRECT_RSAG_THRESHOLD", n >= 4 ? (int64_t)64 << 20 : 0) : 0;
+            ? (size_t)param_int("DIRECT_RSAG_THRESHOLD", n >= 4 ? (int64_t)8 << 20 : 0) : 0;
     // The inbox exists whenever the mesh allows the direct path, so that
     // NCCL_ALGO=Direct can take any bucket even where no size defaults to it.
     if (n <= kDirectMaxRanks) {
