@@ -26,6 +26,7 @@ def main():
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count())
     if world > torch.cuda.device_count():
         os.environ["VCCL_ALLOW_SHARED_DEVICE"] = "1"
+    os.environ.setdefault("VCCL_LL128_ALLOC", "1")  # so LAT_ALGOS may force ll128
     dist.init_process_group("gloo")
     obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)

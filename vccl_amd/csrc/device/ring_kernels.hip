@@ -41,6 +41,9 @@ constexpr int kPartProto = VCCL_PART == 3 ? kProtoLL128 : kProtoSimple;
 // bandwidth.
 template <class Fn>
 constexpr int ring_unroll() { return IsF8<typename Fn::EltType>::value ? 2 : kRingUnroll; }
+#ifndef VCCL_AG_UNROLL
+#define VCCL_AG_UNROLL kRingUnroll
+#endif
 
 // PROTO is a template parameter of every function below, so the SIMPLE and
 // LL128 objects never define the same symbol differently.
@@ -91,7 +94,7 @@ hipError_t VCCL_RING_LAUNCH<VCCL_KT>(int coll, int devOp, const RingBatch& w, in
   dim3 grid(w.w.nChannels), block(nthreads);
   if (coll == kCollAllGather) {
     if constexpr (VCCL_KT == K_U8) {
-      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, kRingUnroll, kPartProto>), grid, block, 0,
+      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, VCCL_AG_UNROLL, kPartProto>), grid, block, 0,
                          stream, w);
       return hipGetLastError();
     }
