@@ -215,7 +215,9 @@ __device__ __forceinline__ void ll128_st_piece(char* p, int64_t b0, int len, int
 }
 
 #ifndef VCCL_LL128_UNROLL
-#define VCCL_LL128_UNROLL 2
+// 4 rounds per wave in flight: RS 1 / 4 MiB 6-7 % faster than 2, AR 4 MiB 3 %,
+// AR 256 KiB ~1 us slower (2 ranks, 3 interleaved reps, profiles/r03k)
+#define VCCL_LL128_UNROLL 4
 #endif
 constexpr int kLL128Unroll = VCCL_LL128_UNROLL;  // rounds in flight per wave
 
