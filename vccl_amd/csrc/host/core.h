@@ -110,6 +110,7 @@ struct ncclComm {
   uint64_t magic;
   int rank = 0, nRanks = 1, device = 0;
   int nChannels = 0, slotBytes = 0, nThreads = 0;
+  int stepBytes = 0;  // VCCL's FIFO step: the partition / chunk unit (slotBytes = the FIFO slot)
   vccl::Bootstrap* bootstrap = nullptr;
   // device resources
   char* fifoBuf = nullptr;     // nChannels * kSteps * slotBytes, uncached

@@ -405,7 +405,7 @@ static ncclResult_t ring_work_of(const Task& t, bool ll128, RingWork* out, int* 
   const CbdPlan p = ll128 ? cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
                                           kProtoLL128, comm->ll128StepBytes, comm->ll128Threads)
                          : cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
-                                        kProtoSimple, comm->slotBytes, comm->nThreads);
+                                        kProtoSimple, comm->stepBytes, comm->nThreads);
   if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
     return ncclInternalError;
   w.channelLo = p.channelLo;
@@ -489,7 +489,7 @@ static int dev_coll(int coll) {
 // reduce-scatters' per-channel fold order (the ring's own, cbd_schedule).
 static CbdLite rs_cbd(const ncclComm* comm, const Task& t) {
   const CbdPlan p = cbd_schedule(kReduceScatter, (int64_t)t.count, type_size(t.datatype), comm->nRanks,
-                                 comm->nChannels, kProtoSimple, comm->slotBytes, comm->nThreads);
+                                 comm->nChannels, kProtoSimple, comm->stepBytes, comm->nThreads);
   return CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)t.count};
 }
 
@@ -583,7 +583,7 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
     // the ring's partition of this bucket: phase 2 folds every element in the
     // order VCCL's ring all-reduce gives it on these channels (ar_chunk_of)
     const CbdPlan p = cbd_schedule(kAllReduce, count, esz, n, comm->nChannels, kProtoSimple,
-                                   comm->slotBytes, comm->nThreads);
+                                   comm->stepBytes, comm->nThreads);
     w.cbd = CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, count};
     w.arChunk = p.chunkLo;
   } else {

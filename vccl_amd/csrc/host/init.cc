@@ -178,25 +178,41 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   // Channel count: NCCL_NCHANNELS total, else VCCL_CHANNELS_PER_RING x rings.
   // Defaults from tools/sweep_ring.py (profiles/r01_sweep_ring*.log): a
   // channel is one workgroup whose throughput is bounded by the per-slot
-  // credit round trip, so bandwidth scales with channels: 8 per ring for the
-  // 8- and 4-GPU ring sets (56 / 48 workgroups), 48 for 2 GPUs
+  // credit round trip and its CU's memory rate (tools/step_probe.py), so
+  // bandwidth scales with channels: 8 per ring for the 8- and 4-GPU ring
+  // sets (56 / 48 workgroups), 64 (MAXCHANNELS) for 2 GPUs
   // (profiles/r02g/sweep_ring_1g.log: 16 / 32 / 48 channels -> 199 / 299 /
-  // 436 GB/s busbw at 1 GiB, 2 ranks on one GPU).
-  // (3 ranks: 2 rings x 24 = the 48 workgroups of the 2-rank default)
-  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : n == 3 ? 24 : 48);
+  // 436 GB/s busbw at 1 GiB; profiles/r03m: 48 -> 64 channels, 512 MiB RS
+  // 733 -> 586 us, AR 1289 -> 1036 us; 2 ranks on one GPU).
+  // (3 ranks: 2 rings x 32 = the 64 workgroups of the 2-rank default)
+  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : n == 3 ? 32 : 64);
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
   // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490)
   nch = std::max(c->minCTAs, std::min(nch, c->maxCTAs));
   nch = std::max(1, std::min(nch, kMaxChannels));
   c->nChannels = n > 1 ? nch : 0;
-  // Slot = one FIFO step: NCCL_BUFFSIZE / NCCL_STEPS (init.cc:619-633, 4 MiB
-  // -> 512 KiB), or VCCL_SLOT_BYTES directly.
+  // Step = VCCL's FIFO step: NCCL_BUFFSIZE / NCCL_STEPS (init.cc:619-633,
+  // 4 MiB -> 512 KiB), or VCCL_SLOT_BYTES directly.  It sets VCCL's
+  // partition and ring chunk (4 steps, cbd_schedule), hence the fold order.
+  // The FIFO slot (the unit a chunk crosses the FIFO in, one flag hand-off
+  // each) is the step unless VCCL_SLICE_BYTES sets it apart without touching
+  // the fold order.  A chunk may span at most kSteps / 2 slots: a recv-send
+  // step needs free slots while its successor still holds the previous
+  // step's (the reference's chunkSteps 4 of NCCL_STEPS 8); 8 slots of 256 KiB
+  // for a 2 MiB chunk deadlock the n = 2 all-reduce (profiles/r03n).
   const int64_t buffSize = param_int("BUFFSIZE", -2);
-  c->slotBytes = (int)param_int("SLOT_BYTES", buffSize > 0 ? buffSize / kSteps : 512 << 10);
-  if (c->slotBytes < 4096 || c->slotBytes % 4096 || c->slotBytes > (64 << 20)) {
+  c->stepBytes = (int)param_int("SLOT_BYTES", buffSize > 0 ? buffSize / kSteps : 512 << 10);
+  if (c->stepBytes < 4096 || c->stepBytes % 4096 || c->stepBytes > (64 << 20)) {
     VWARN("slot size (NCCL_BUFFSIZE / 8 or VCCL_SLOT_BYTES) must be a multiple of 4096 up to "
           "64 MiB, using 524288");
-    c->slotBytes = 512 << 10;
+    c->stepBytes = 512 << 10;
+  }
+  c->slotBytes = (int)param_int("SLICE_BYTES", c->stepBytes);
+  if (c->slotBytes < 4096 || c->slotBytes % 4096 || c->slotBytes > (64 << 20) ||
+      (int64_t)c->slotBytes * (kSteps / 2) < (int64_t)c->stepBytes * 4) {
+    VWARN("VCCL_SLICE_BYTES must be a multiple of 4096 up to 64 MiB and hold a ring chunk (4 steps of %d B) "
+          "in %d slots, using the step", c->stepBytes, kSteps / 2);
+    c->slotBytes = c->stepBytes;
   }
   {
     const char* algo = getenv("NCCL_ALGO");
@@ -517,8 +533,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   }
   VINFO("rank %d: final barrier", c->rank);
   NCCLCHECK(bootstrap_barrier(c->bootstrap));
-  VINFO("comm %p rank %d/%d dev %d: %d channels x %d threads, slot %d B", (void*)c, c->rank, n,
-        c->device, c->nChannels, c->nThreads, c->slotBytes);
+  VINFO("comm %p rank %d/%d dev %d: %d channels x %d threads, step %d B, FIFO slot %d B", (void*)c, c->rank,
+        n, c->device, c->nChannels, c->nThreads, c->stepBytes, c->slotBytes);
   VINFO("rank %d: thresholds LL %zu, LL RS/AG %zu, direct %zu, direct RS/AG %zu, LL128 [%zu, %zu]%s, "
         "algo force %d", c->rank, c->llMaxBytes, c->llRsAgMaxBytes, c->directMaxBytes,
         c->directRsAgMaxBytes, c->ll128MinBytes, c->ll128MaxBytes, c->ll128Buf ? " (buffers)" : "",
