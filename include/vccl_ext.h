@@ -16,6 +16,14 @@
  *   vcclCommLaunchStats  collectives enqueued on this communicator so far and
  *                     how many launches carried more than one of them (group
  *                     aggregation of small all-reduces into one LL launch).
+ *   vcclCommRingTrace the SIMPLE ring's slot timeline of the last launch
+ *                     (VCCL_RING_TRACE=<records per channel> at init, else
+ *                     ncclInvalidUsage): per channel `cap` records of 56 bytes
+ *                     {t0 entry, t1 credits seen, t2 released, t3 payload
+ *                     drained, t4 flags stored (s_memrealtime, 100 MHz);
+ *                     uint32 shape = RECV | SEND<<1 | SRC<<2 | DST<<3; uint32
+ *                     payload bytes; uint64 step}, unused records zero.  A
+ *                     measurement hook (no reference counterpart).
  *   vcclCommNetStats  payload bytes this rank's net proxy has sent / received
  *                     and its connection count (0 when every peer is reached
  *                     over xGMI).  The net transport carries ring connections
@@ -80,6 +88,7 @@ ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count, ncclDataT
 ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo);
 ncclResult_t vcclCommLaunchStats(ncclComm_t comm, unsigned long long* collectives,
                                  unsigned long long* fusedLaunches);
+ncclResult_t vcclCommRingTrace(ncclComm_t comm, void* hostBuf, size_t bytes, int* nChannels, int* cap);
 ncclResult_t vcclCommNetStats(ncclComm_t comm, uint64_t* bytesSent, uint64_t* bytesReceived,
                               int* connections);
 ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences);

@@ -44,6 +44,8 @@ struct RingCtx {
   int slotBytes;
   int64_t ll128Slot;  // bytes per LL128 FIFO slot (LL128 ring only)
   int* shAbort;  // LDS
+  RingTraceRec* trace;  // this channel's timeline (DevComm::trace) or nullptr
+  int traceN;           // records written by this launch
 
   // Bounded spin on `flag` until pred(value); returns false on abort/timeout.
   // The timeout is per wait (no progress for spinTimeoutTicks), not per call.
@@ -85,7 +87,10 @@ struct RingCtx {
   __device__ void prim(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
                        int recvOff = 0, int sendOff = 0) {
     if (aborted()) return;
+    const bool tr = trace != nullptr && traceN < comm->traceCap;
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
     if (tid == 0) {
+      if (tr) t0 = __builtin_amdgcn_s_memrealtime();
       bool ok = true;
       if (RECV) ok = spin_ge(ch->recvTail, recvStep + 1);
       if (SEND && ok && sendStep + 1 > (uint64_t)kSteps) ok = spin_ge(ch->sendHead, sendStep + 1 - kSteps);
@@ -94,9 +99,11 @@ struct RingCtx {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
         drain_vmem();
       }
+      if (tr) t1 = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     if (aborted()) return;
+    if (tid == 0 && tr) t2 = __builtin_amdgcn_s_memrealtime();
     if (nelem > 0) {
       // Operand order and memory policy: own input streamed once (nt), FIFO
       // slots system-coherent write-through (sc0 sc1).  Own output: nt
@@ -125,6 +132,7 @@ struct RingCtx {
     drain_vmem();  // every storing wave: its write-through payload stores are complete
     __syncthreads();
     if (tid == 0) {
+      if (tr) t3 = __builtin_amdgcn_s_memrealtime();
       if (comm->useFences) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system-scope release (L2 writeback)
         drain_vmem();
@@ -135,7 +143,19 @@ struct RingCtx {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (SEND) st_sys(ch->nextRecvTail, sendStep + 1);
       if (RECV) st_sys(ch->prevSendHead, recvStep + 1);
+      if (tr) {
+        RingTraceRec& rec = trace[traceN];
+        rec.t0 = t0;
+        rec.t1 = t1;
+        rec.t2 = t2;
+        rec.t3 = t3;
+        rec.t4 = __builtin_amdgcn_s_memrealtime();
+        rec.shape = (RECV ? 1u : 0u) | (SEND ? 2u : 0u) | (SRC ? 4u : 0u) | (DST ? 8u : 0u);
+        rec.bytes = (uint32_t)(nelem > 0 ? nelem * (int64_t)sizeof(typename Fn::EltType) : 0);
+        rec.step = SEND ? sendStep : recvStep;
+      }
     }
+    if (tr) traceN++;
     if (SEND) sendStep++;
     if (RECV) recvStep++;
   }

@@ -75,6 +75,8 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
   r.slotBytes = w.slotBytes;
   r.ll128Slot = w.ll128SlotBytes;
   r.shAbort = &shAbort;
+  r.trace = w.comm->trace ? (RingTraceRec*)w.comm->trace + (int64_t)blockIdx.x * w.comm->traceCap : nullptr;
+  r.traceN = 0;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
   ring_run<COLL, Fn, UNROLL, PROTO>(r, fn, w);
   for (int i = 1; i < b.nParts; i++)

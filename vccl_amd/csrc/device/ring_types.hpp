@@ -86,7 +86,23 @@ struct DevComm {
   // position c+1 around to c (all_reduce.h:42-64), whichever rank computes
   // it — the direct all-reduce folds in that order too.
   int8_t ringAt[kOrderMaxRings][kOrderMaxRanks];
+  // Opt-in slot timeline of the SIMPLE ring (VCCL_RING_TRACE=<records per
+  // channel>, vcclCommRingTrace): per channel, the first traceCap slot
+  // hand-offs of each launch as RingTraceRec; nullptr = off.
+  uint64_t* trace;
+  int traceCap;
 };
+
+// One SIMPLE-ring slot hand-off, s_memrealtime ticks (100 MHz), taken by
+// thread 0: entry, credits seen, workgroup released, payload drained
+// (every wave's stores complete, second barrier), flags stored; shape =
+// RECV | SEND << 1 | SRC << 2 | DST << 3; bytes of payload.
+struct RingTraceRec {
+  uint64_t t0, t1, t2, t3, t4;
+  uint32_t shape, bytes;
+  uint64_t step;
+};
+static_assert(sizeof(RingTraceRec) == 56, "trace record layout");
 
 // The part of VCCL's cbd partition a reduce-scatter needs to know which
 // channel (hence ring, hence fold order) an element of the block is on.

@@ -111,6 +111,8 @@ struct ncclComm {
   int rank = 0, nRanks = 1, device = 0;
   int nChannels = 0, slotBytes = 0, nThreads = 0;
   int stepBytes = 0;  // VCCL's FIFO step: the partition / chunk unit (slotBytes = the FIFO slot)
+  uint64_t* ringTrace = nullptr;  // VCCL_RING_TRACE: nChannels x ringTraceCap RingTraceRec
+  int ringTraceCap = 0;
   vccl::Bootstrap* bootstrap = nullptr;
   // device resources
   char* fifoBuf = nullptr;     // nChannels * kSteps * slotBytes, uncached

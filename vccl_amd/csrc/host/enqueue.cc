@@ -1090,6 +1090,23 @@ extern "C" ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo) {
   return ncclInvalidArgument;
 }
 
+extern "C" ncclResult_t vcclCommRingTrace(ncclComm_t comm, void* hostBuf, size_t bytes, int* nChannels,
+                                          int* cap) {
+  NCCLCHECK(comm_check(comm, "vcclCommRingTrace"));
+  if (nChannels) *nChannels = comm->nChannels;
+  if (cap) *cap = comm->ringTraceCap;
+  if (!comm->ringTrace) return ncclInvalidUsage;
+  const size_t need = (size_t)comm->nChannels * comm->ringTraceCap * sizeof(RingTraceRec);
+  if (!hostBuf || bytes < need) return ncclInvalidArgument;
+  int old = -1;
+  HIPCHECK(hipGetDevice(&old));
+  if (old != comm->device) HIPCHECK(hipSetDevice(comm->device));
+  const hipError_t e = hipMemcpy(hostBuf, comm->ringTrace, need, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) (void)hipMemset(comm->ringTrace, 0, need);
+  if (old != comm->device) (void)hipSetDevice(old);
+  return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+}
+
 extern "C" ncclResult_t vcclCommLaunchStats(ncclComm_t comm, unsigned long long* collectives,
                                             unsigned long long* fusedLaunches) {
   NCCLCHECK(comm_check(comm, "vcclCommLaunchStats"));

@@ -119,6 +119,8 @@ static void free_resources(ncclComm* c) {
   c->dBuf = c->dFlags = nullptr;
   c->dPeers = nullptr;
   if (c->devComm) (void)hipFree(c->devComm);
+  if (c->ringTrace) (void)hipFree(c->ringTrace);
+  c->ringTrace = nullptr;
   if (c->devChannels) (void)hipFree(c->devChannels);
   if (c->abortFlag) (void)hipHostFree((void*)c->abortFlag);
   if (c->errorFlag) (void)hipHostFree(c->errorFlag);
@@ -439,6 +441,15 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   dc.useFences = (int)param_int("FENCES", 0);
   if (anyNet) dc.useFences = 1;  // slots and flags in host memory: full system-scope fences
   dc.pollMode = (int)param_int("POLL_MODE", 0);
+  // Opt-in slot timeline of the SIMPLE ring (vcclCommRingTrace)
+  c->ringTraceCap = n > 1 ? (int)std::max<int64_t>(0, std::min<int64_t>(param_int("RING_TRACE", 0), 1 << 16)) : 0;
+  if (c->ringTraceCap > 0) {
+    const size_t tb = (size_t)c->nChannels * c->ringTraceCap * sizeof(RingTraceRec);
+    HIPCHECK(hipMalloc((void**)&c->ringTrace, tb));
+    HIPCHECK(hipMemset(c->ringTrace, 0, tb));
+  }
+  dc.trace = c->ringTrace;
+  dc.traceCap = c->ringTraceCap;
   // reduce-scatter fold order of this rank on each ring (ring_types.hpp)
   dc.nRings = std::min(nRings, kOrderMaxRings);
   for (int k = 0; k < dc.nRings && n <= kOrderMaxRanks; k++) {

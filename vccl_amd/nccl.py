@@ -40,6 +40,7 @@ EXPORTED = [
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
+    "vcclCommRingTrace",
     "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
@@ -290,6 +291,19 @@ class Comm:
         check(lib().vcclCommLaunchStats(self.handle, ctypes.byref(a), ctypes.byref(b)),
               "vcclCommLaunchStats")
         return a.value, b.value
+
+    def ring_trace(self):
+        """vcclCommRingTrace: the SIMPLE ring's slot timeline of the last launch
+        as a numpy structured array [nChannels, cap] (VCCL_RING_TRACE at init)."""
+        import numpy as np
+        nch, cap = ctypes.c_int(), ctypes.c_int()
+        lib().vcclCommRingTrace(self.handle, None, 0, ctypes.byref(nch), ctypes.byref(cap))
+        dt = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("t2", "<u8"), ("t3", "<u8"), ("t4", "<u8"),
+                       ("shape", "<u4"), ("bytes", "<u4"), ("step", "<u8")])
+        out = np.zeros((nch.value, cap.value), dtype=dt)
+        check(lib().vcclCommRingTrace(self.handle, out.ctypes.data_as(ctypes.c_void_p),
+                                      ctypes.c_size_t(out.nbytes), None, None), "vcclCommRingTrace")
+        return out
 
     def net_stats(self) -> tuple[int, int, int]:
         """vcclCommNetStats: (bytes sent, bytes received, connections) of the net proxy."""
