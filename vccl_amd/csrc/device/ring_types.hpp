@@ -18,7 +18,10 @@ namespace vccl {
 
 constexpr int kSteps = 8;            // NCCL_STEPS (device.h:24)
 constexpr int kMaxRanks = 64;
-constexpr int kMaxChannels = 64;     // MAXCHANNELS (device.h:62)
+#ifndef VCCL_MAX_CHANNELS
+#define VCCL_MAX_CHANNELS 64
+#endif
+constexpr int kMaxChannels = VCCL_MAX_CHANNELS;  // MAXCHANNELS (device.h:62)
 constexpr int kFlagStride = 128;     // bytes between flags (one line each)
 constexpr int kOrderMaxRings = 8;    // ring sets of SURVEY.md Appendix D: 7 (n=8), 6 (n=4), 1
 constexpr int kOrderMaxRanks = 8;
