@@ -18,10 +18,15 @@ namespace vccl {
 
 constexpr int kSteps = 8;            // NCCL_STEPS (device.h:24)
 constexpr int kMaxRanks = 64;
+// MAXCHANNELS (device.h:62) is 64 in the reference; here 128: a channel is
+// one workgroup on one CU, and a ring channel's rate is bounded by its CU's
+// memory rate (tools/step_probe.py), so wide rings need more of the 256 CUs
+// than an NVLink GPU's SMs (2 ranks on one GPU: 64 -> 96 -> 128 channels,
+// 512 MiB AR 1039 -> 868 -> 845 us, profiles/r03q).
 #ifndef VCCL_MAX_CHANNELS
-#define VCCL_MAX_CHANNELS 64
+#define VCCL_MAX_CHANNELS 128
 #endif
-constexpr int kMaxChannels = VCCL_MAX_CHANNELS;  // MAXCHANNELS (device.h:62)
+constexpr int kMaxChannels = VCCL_MAX_CHANNELS;
 constexpr int kFlagStride = 128;     // bytes between flags (one line each)
 constexpr int kOrderMaxRings = 8;    // ring sets of SURVEY.md Appendix D: 7 (n=8), 6 (n=4), 1
 constexpr int kOrderMaxRanks = 8;

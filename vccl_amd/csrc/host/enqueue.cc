@@ -533,7 +533,7 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   if (kt < 0) return ncclInvalidArgument;
   // A bounded grid (256-thread workgroups, each thread looping over lines):
   // one workgroup per 256 lines, within the comm's CTA bounds (minCTAs /
-  // maxCTAs, default 1 / 64), and never above VCCL_LL_MAX_BLOCKS (256): every
+  // maxCTAs, default 1 / 128), and never above VCCL_LL_MAX_BLOCKS (256): every
   // rank's LL workgroups must be resident at once for the peers' spins to
   // complete, so that co-residency cap is applied LAST (tests that
   // put 8 ranks on ONE GPU lower it).
