@@ -60,7 +60,7 @@ def n_channels(n, per_ring=None, nch=None):
     """Library default channel count (host/init.cc) unless overridden."""
     rings = ring_orders(n)
     if per_ring is None:
-        per_ring = 8 if n >= 4 else 48 if n == 3 else 96
+        per_ring = 16 if n >= 4 else 48 if n == 3 else 96
     c = nch if nch is not None else per_ring * len(rings)
     return max(1, min(c, 128))  # kMaxChannels
 

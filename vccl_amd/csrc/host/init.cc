@@ -182,16 +182,19 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   // channel is one workgroup whose throughput is bounded by the per-slot
   // credit round trip and its CU's memory rate (tools/step_probe.py; the
   // slot timeline, tools/ring_trace.py, shows < 2 us of protocol per 512 KiB
-  // slot: the copy is the bound), so bandwidth scales with channels: 8 per
-  // ring for the 8- and 4-GPU ring sets (56 / 48 workgroups; a channel there
-  // carries ~9.6 GB/s per direction at the xGMI spec, well inside one CU's
-  // rate), 96 for 2 GPUs (profiles/r02g/sweep_ring_1g.log: 16 / 32 / 48
+  // slot: the copy is the bound), so bandwidth scales with channels: 16 per
+  // ring from 4 ranks (112 workgroups for the 8-GPU ring set, 96 for the
+  // 4-GPU one): a channel then carries 7 x 76.8 / 112 = 4.8 GB/s per
+  // direction at the xGMI spec, about a tenth of the slowest ring shape's
+  // per-channel rate on one GPU, as headroom for remote-store latency that
+  // no single-GPU run can show (RCCL's MI300X guidance uses 112 channels
+  // too); 96 for 2 GPUs (profiles/r02g/sweep_ring_1g.log: 16 / 32 / 48
   // channels -> 199 / 299 / 436 GB/s busbw at 1 GiB; profiles/r03m, r03q:
   // 48 / 64 / 96 / 128 channels -> 512 MiB AR 1289 / 1039 / 868 / 845 us,
   // 2 ranks on one GPU; 96 leaves a quarter of the CUs to the peer ranks'
   // other work when two ranks share a GPU).
   // (3 ranks: 2 rings x 48 = the 96 workgroups of the 2-rank default)
-  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 8 : n == 3 ? 48 : 96);
+  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 16 : n == 3 ? 48 : 96);
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
   // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490)
   nch = std::max(c->minCTAs, std::min(nch, c->maxCTAs));
