@@ -81,7 +81,7 @@ struct PeerMap {               // what one rank published about itself
   int64_t busId;               // PCI domain/bus/device: the GPU's identity across processes
   uint32_t netIp;              // net proxy listener (network order), see proxy.cc
   uint16_t netPort;
-  uint16_t pad0;
+  uint16_t cuCount;            // compute units of the device (co-residency cap of shared GPUs)
   hipIpcMemHandle_t fifoHandle;
   hipIpcMemHandle_t flagHandle;
   hipIpcMemHandle_t llHandle;

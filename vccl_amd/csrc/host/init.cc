@@ -260,6 +260,9 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     HIPCHECK(hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device));
     HIPCHECK(hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, c->device));
     me.busId = ((int64_t)dom << 16) | (bus << 8) | dev;
+    int cus = 0;
+    HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    me.cuCount = (uint16_t)std::max(1, std::min(cus, 65535));
   }
   if (n > 1) {
     const size_t fifoBytes = (size_t)c->nChannels * kSteps * slot_stride(c->slotBytes);
@@ -404,6 +407,33 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
                 (long)c->peers[q].busId);
           return ncclInvalidUsage;
         }
+  }
+  {
+    // Ranks sharing a GPU (VCCL_ALLOW_SHARED_DEVICE: rehearsals on fewer GPUs
+    // than ranks) spin on each other, so all their ring workgroups must be
+    // resident at once: one 512-thread ring workgroup fills a CU (176-232
+    // VGPRs), so k ranks on a device get at most 7/8 of its CUs / k channels
+    // (e.g. 4 ranks on 256 CUs: 56), the rest left to the other kernels.
+    // Computed from the shared peer table, so every rank picks the same
+    // count (the partition depends on it); the FIFO was sized for the
+    // uncapped count, its tail stays unused.  Real one-rank-per-GPU runs are
+    // untouched.
+    int share = 1, cus = 1 << 30;
+    for (int q = 0; q < n; q++) {
+      int k = 0;
+      for (int r = 0; r < n; r++)
+        k += c->peers[r].hostHash == c->peers[q].hostHash && c->peers[r].busId == c->peers[q].busId;
+      share = std::max(share, k);
+      cus = std::min(cus, (int)c->peers[q].cuCount);
+    }
+    if (share > 1 && c->nChannels > 0) {
+      const int cap = std::max(1, cus * 7 / 8 / share);
+      if (c->nChannels > cap) {
+        VINFO("rank %d: %d ranks share a GPU of %d CUs: %d -> %d ring channels", c->rank, share, cus,
+              c->nChannels, cap);
+        c->nChannels = cap;
+      }
+    }
   }
   {
     // Ranks of this comm that share ONE device inside ONE process (allowed
