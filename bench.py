@@ -935,9 +935,11 @@ def _ar_graph_row(dist, comm, rank, world, S, dtype="f16", calls=50, replays=10)
     torch.cuda.synchronize()
     with torch.cuda.stream(cs):
         graph.capture_begin(capture_error_mode="relaxed")
-        for _ in range(calls):
-            comm.all_reduce(x.data_ptr(), y.data_ptr(), n, code, nccl.ncclSum, cs.cuda_stream)
-        graph.capture_end()
+        try:
+            for _ in range(calls):
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), n, code, nccl.ncclSum, cs.cuda_stream)
+        finally:  # a failing call must not leave the stream capturing (the process would abort)
+            graph.capture_end()
     torch.cuda.synchronize()
     dt = _time_coll(dist, graph.replay, replays, 2)
     sp = torch.cuda.current_stream().cuda_stream

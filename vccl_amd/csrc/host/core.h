@@ -113,6 +113,7 @@ struct ncclComm {
   int stepBytes = 0;  // VCCL's FIFO step: the partition / chunk unit (slotBytes = the FIFO slot)
   uint64_t* ringTrace = nullptr;  // VCCL_RING_TRACE: nChannels x ringTraceCap RingTraceRec
   int ringTraceCap = 0;
+  int shareBlockCap = 0;  // ranks sharing a GPU: workgroups per launch that stay co-resident (0 = no cap)
   vccl::Bootstrap* bootstrap = nullptr;
   // device resources
   char* fifoBuf = nullptr;     // nChannels * kSteps * slotBytes, uncached

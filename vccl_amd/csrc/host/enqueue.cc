@@ -537,7 +537,8 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   // rank's LL workgroups must be resident at once for the peers' spins to
   // complete, so that co-residency cap is applied LAST (tests that
   // put 8 ranks on ONE GPU lower it).
-  const int maxBlocks = (int)std::max<int64_t>(1, param_int("LL_MAX_BLOCKS", 256));
+  int maxBlocks = (int)std::max<int64_t>(1, param_int("LL_MAX_BLOCKS", 256));
+  if (comm->shareBlockCap > 0) maxBlocks = std::min(maxBlocks, comm->shareBlockCap);
   int grid = (int)std::max<int64_t>(1, (lines + 255) / 256);
   grid = std::max(std::min(grid, comm->maxCTAs), comm->minCTAs);
   grid = std::max(1, std::min(grid, maxBlocks));

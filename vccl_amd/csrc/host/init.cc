@@ -426,8 +426,10 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       share = std::max(share, k);
       cus = std::min(cus, (int)c->peers[q].cuCount);
     }
-    if (share > 1 && c->nChannels > 0) {
+    if (share > 1) {
       const int cap = std::max(1, cus * 7 / 8 / share);
+      c->shareBlockCap = cap;  // the LL and direct grids too (enqueue.cc)
+      c->directMaxBlocks = std::min(c->directMaxBlocks, cap);
       if (c->nChannels > cap) {
         VINFO("rank %d: %d ranks share a GPU of %d CUs: %d -> %d ring channels", c->rank, share, cus,
               c->nChannels, cap);
