@@ -436,3 +436,41 @@ def test_group_zero_pattern(n, geom):
         exp = _ring.expected_allreduce(0, dt, ins, nch, slot)
         for r in range(n):
             assert_bitexact(dt, res[r][name], exp, what=f"{name} n={n} {geom} rank {r}")
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_ring_trace_and_shared_cap(n):
+    """The SIMPLE ring's slot timeline (VCCL_RING_TRACE, vcclCommRingTrace)
+    and the co-residency cap of ranks sharing one GPU: with library defaults,
+    n ranks on one device get min(default, 7/8 CUs / n) ring channels (the
+    peer table gives every rank the same count); every traced slot has
+    ordered stamps, an all-reduce shape and payload, and the output is
+    exact (tests/mp_trace_worker.py)."""
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    for k in TEST_GEOM:
+        env.pop(k, None)
+    env.update(VCCL_ALLOW_SHARED_DEVICE="1", VCCL_RING_TRACE="256", VCCL_SPIN_TIMEOUT_S="20")
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_trace_worker.py"),
+                                   str(r), str(n), hexid, d], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
+    cus = int(res[0]["cus"])
+    want = min(_ring.n_channels(n), max(1, cus * 7 // 8 // n))
+    ar_shapes = {0b0110, 0b0111, 0b1111, 0b1011, 0b1001}  # S->F, S+F->F, S+F->F+O, F->F+O, F->O
+    for r in range(n):
+        assert bool(res[r]["ok"]), f"rank {r}: all-reduce output"
+        assert int(res[r]["nch"]) == want, (int(res[r]["nch"]), want)
+        t, shape, nbytes = res[r]["t"], res[r]["shape"], res[r]["bytes"]
+        used = t[..., 4] > 0
+        assert used.any()
+        ts = t[used]
+        assert (np.diff(ts, axis=-1) >= 0).all(), "stamps out of order"
+        assert set(int(s) for s in shape[used]) <= ar_shapes
+        assert nbytes[used].sum() > 0 and (nbytes[used] % 16 == 0).all()
+        # every traced channel ran at least the 2n-1 steps of one loop
+        assert (used.sum(axis=1)[used.any(axis=1)] >= 2 * n - 1).all()
