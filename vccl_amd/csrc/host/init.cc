@@ -304,8 +304,9 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // does, i.e. small and mid buckets at n >= 4 (profiles/r02e/lat_n4.log,
     // lat_n8.log).  Above 8 MiB the ring's continuous pipeline wins (4 ranks:
     // 16 MiB 111 vs 121 us, 64 MiB 330 vs 504 us, profiles/r03g/lat_n4.log).
-    // At n = 2 the ring IS two hops and its 48 channels beat the direct path
-    // at every size above LL (profiles/r02/lat_n2.log).
+    // At n = 2 the ring IS two hops and its channels beat the direct path at
+    // every size above LL (profiles/r02/lat_n2.log, r03r: 1 GiB ring 655 vs
+    // direct ~220 GB/s).
     c->directMaxBytes = n <= kDirectMaxRanks
                             ? (size_t)param_int("DIRECT_THRESHOLD", n >= 4 ? (int64_t)8 << 20 : 0)
                             : 0;
