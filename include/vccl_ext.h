@@ -62,6 +62,25 @@
  *                     loop (the chunk that finishes at ring position c,
  *                     src/device/all_reduce.h:32-64), out[2] = the end of that
  *                     chunk — the lookup the direct all-reduce folds by.
+ *   vcclGroupPlan      the partition a GROUP of ring / direct calls of one
+ *                     communicator gets (host only): VCCL's multi-task plan —
+ *                     the size sorter and (func, op, type) bins with 4x
+ *                     aggregation of ncclPrepareTasks (src/enqueue.cc:352-437)
+ *                     and scheduleCollTasksToPlan's shared trafficPerChannel,
+ *                     running channelId and currentTraffic, split into kernel
+ *                     plans at the argument budget (:518-769).  Inputs per
+ *                     call: colls[i], counts[i] (AR count, RS recvcount, AG
+ *                     sendcount), datatypes[i], ops[i] (ncclRedOp_t built-in;
+ *                     ignored for all-gather).  Outputs: order[0..n) the calls
+ *                     in plan (execution) order, planOf[i] the kernel plan of
+ *                     call i, cbd[8 i .. 8 i + 8) its partition as in
+ *                     vcclRingPartition.
+ *   vcclAlgoSelection  how NCCL_ALGO / NCCL_PROTO strings select paths (the
+ *                     reference's parseList, graph/tuning.cc:53-116: comma
+ *                     lists, a leading '^' excludes): *force = 0 automatic,
+ *                     1 SIMPLE ring, 2 LL, 3 direct, 4 LL128 ring; *allowed =
+ *                     bit 0 LL, bit 1 LL128, bit 2 SIMPLE, bit 3 direct.
+ *                     ncclInvalidUsage for an unknown name, as at init.
  */
 #ifndef VCCL_EXT_H_
 #define VCCL_EXT_H_
@@ -101,6 +120,10 @@ ncclResult_t vcclRingChunkOf(size_t count, ncclDataType_t datatype, int nRanks, 
 /* The ring set of an nRanks communicator: orders[k * nRanks + i] = the rank
  * at position i of ring k (channel c runs on ring c mod nRings). */
 ncclResult_t vcclRingOrders(int nRanks, int maxRings, int* orders, int* nRings);
+ncclResult_t vcclGroupPlan(int nCalls, const int* colls, const size_t* counts, const int* datatypes,
+                           const int* ops, int nRanks, int nChannels, size_t stepBytes, int nThreads,
+                           int* order, int* planOf, int64_t* cbd);
+ncclResult_t vcclAlgoSelection(const char* algo, const char* proto, int* force, int* allowed);
 
 #ifdef __cplusplus
 }

@@ -8,7 +8,8 @@ with the C oracle's ring_fold (oracle/reduce_ref.c) it gives VCCL's exact
 result for a given (ring set, channel count, buffer size).
 
 Followed, for a plan holding one collective (the ncclAllReduce /
-ncclReduceScatter / ncclAllGather call outside a group):
+ncclReduceScatter / ncclAllGather call outside a group; plan_schedule below
+restates the multi-task plan of a group):
   * taskAppend: AG counted in bytes as int8 (enqueue.cc:2398-2404);
     trafficBytes = count * eltSize * trafficPerByte (enqueue.cc:2405,
     ncclFuncTrafficPerByte enqueue.cc:67-74: AR 2, RS/AG nRanks)
@@ -181,6 +182,176 @@ def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPL
     return CbdWork(channel_id, channel_id + n_channels - 1, count_lo, count_mid, count_hi,
                    grains if count_lo else 0, grains if n_mid else 0, grains if count_hi else 0,
                    proto, elt_size)
+
+
+# ------------------------------------------------------------------ group plan
+# VCCL's plan for a GROUP of ring collectives of one communicator (all taken
+# as RING / SIMPLE):
+#   * taskAppend (enqueue.cc:2398-2413): AG as int8 bytes, trafficBytes =
+#     count * eltSize * trafficPerByte, inserted into ncclTaskCollSorter;
+#   * the sorter (comm.h:294-343): bin = BinCount-1 - u32fpEncode(min(size,
+#     1 GiB) >> 10, 2) (bitops.h:252-262), bins walked in ascending index
+#     (descending size), each bin's tasks newest first;
+#   * ncclPrepareTasks (enqueue.cc:352-437): pushed onto one LIFO per
+#     (func, devOp, type) -> each list size-ascending, lists in order of first
+#     appearance; runs within 4x of the run's first trafficBytes aggregated,
+#     nMaxChannels from the ring tuning on the aggregate's count;
+#   * scheduleCollTasksToPlan (enqueue.cc:518-769): per plan, the tasks that
+#     pass the work-budget estimate give trafficPerChannel = sum(max(16K,
+#     traffic)) / min(sum nMaxChannels, comm channels); every task is split
+#     into cells at the running (channelId, currentTraffic); a task whose
+#     channels would exceed the argument budget (testBudget :278-286, work
+#     batches counted as addWorkBatchToPlan :91-156) ends the plan.
+U32FP_BITS, SORTER_UNIT_LOG2, SORTER_MAX_LOG2 = 2, 10, 30
+SORTER_BINS = 1 + (SORTER_MAX_LOG2 - SORTER_UNIT_LOG2) * (1 << U32FP_BITS)
+WORK_COLL_BYTES, WORK_BATCH_BYTES = 96, 16           # sizeof(ncclDevWorkColl / ncclDevWorkBatch)
+IN_ARGS_BYTES = (4 << 10) - 32                        # workArgsBytes - sizeof(ncclDevKernelArgs)
+OUT_ARGS_BYTES = (1 << 20) // 2                       # NCCL_WORK_FIFO_BYTES default / 2
+MAX_BATCH_BYTES = 1024                                # NCCL_MAX_DEV_WORK_BATCH_BYTES
+
+
+def u32fp_encode(x, bits):
+    """bitops.h:252-262."""
+    log2x = (x | 1).bit_length() - 1
+    mant = (x >> (log2x - bits if log2x >= bits else 0)) & ((1 << bits) - 1)
+    expo = log2x - (bits - 1) if log2x >= bits else 0
+    return (expo << bits) | mant
+
+
+@dataclass
+class GroupCall:
+    """One queued collective: coll "ar"|"rs"|"ag", count (AR count, RS
+    recvcount, AG sendcount) in elements of elt_size; key = (func, devOp,
+    type) of ncclPrepareTasks' bins; func = the device function (batches of a
+    channel merge while it is the same)."""
+    coll: str
+    count: int
+    elt_size: int
+    key: tuple
+    func: tuple
+
+
+def _place(cur, coll, count, elt_size, nranks, proto, buff_size):
+    """One task's cbd split at the plan cursor (enqueue.cc:597-644) and the
+    cursor advanced (:667-681).  cur = dict(tpc, ch, cur, nmax)."""
+    tpb = traffic_per_byte(coll, nranks)
+    cell = _div_up(_div_up(MIN_TRAFFIC_PER_CHANNEL, tpb), 16) * 16
+    epc = cell // elt_size
+    cells = _div_up(count * elt_size, cell)
+    tpe = elt_size * tpb
+    tpcell = cell * tpb
+    tpc, ch, used, nmax = cur["tpc"], cur["ch"], cur["cur"], cur["nmax"]
+    per_ch = min(cells, _div_up(tpc, tpcell))
+    lo = cells if ch + 1 == nmax else min(cells, _div_up(tpc - used, tpcell))
+    n_mid = (cells - lo) // per_ch
+    hi = (cells - lo) % per_ch
+    n_ch = (1 if lo else 0) + n_mid + (1 if hi else 0)
+    if nmax < ch + n_ch:
+        n_mid = nmax - ch - 2
+        per_ch = (cells - lo) // (n_mid + 1)
+        hi = per_ch + (cells - lo) % (n_mid + 1)
+    if hi == 0 and n_mid != 0:
+        hi, n_mid = per_ch, n_mid - 1
+    if lo == 0:
+        ch += 1
+        if n_mid == 0:
+            lo, hi = hi, 0
+        else:
+            lo, n_mid = per_ch, n_mid - 1
+    c_mid = per_ch * epc if n_mid else 0
+    c_lo, c_hi = lo * epc, hi * epc
+    excess = cells * epc - count
+    if c_hi:
+        c_hi -= excess
+    else:
+        c_lo -= excess
+    n_ch = (1 if c_lo else 0) + n_mid + (1 if hi else 0)
+    grains = chunk_size(proto, buff_size) // grain_size(proto)
+    work = CbdWork(ch, ch + n_ch - 1, c_lo, c_mid, c_hi, grains if c_lo else 0, grains if n_mid else 0,
+                   grains if c_hi else 0, proto, elt_size)
+    if c_hi:
+        ch, used = ch + n_ch - 1, hi * epc * tpe
+    elif n_mid:
+        ch, used = ch + n_ch, 0
+    else:
+        used += lo * epc * tpe
+    if used >= tpc and ch + 1 != nmax:
+        ch, used = ch + 1, 0
+    return work, dict(tpc=tpc, ch=ch, cur=used, nmax=nmax)
+
+
+def plan_schedule(calls, nranks, comm_channels, buff_size=None, nthreads=None):
+    """VCCL's plans for a group of ring calls.  Returns (order, plan_of,
+    works): the calls in execution order, the plan (kernel) index of every
+    call, and every call's CbdWork (indexed like `calls`)."""
+    proto = PROTO_SIMPLE
+    calls = [GroupCall(c.coll, c.count * c.elt_size, 1, c.key, c.func) if c.coll == "ag" else c
+             for c in calls]
+    traffic = [c.count * c.elt_size * traffic_per_byte(c.coll, nranks) for c in calls]
+    bins = [[] for _ in range(SORTER_BINS)]
+    for i, t in enumerate(traffic):
+        x = min(t, 1 << SORTER_MAX_LOG2) >> SORTER_UNIT_LOG2
+        bins[SORTER_BINS - 1 - u32fp_encode(x, U32FP_BITS)].append(i)
+    sorted_ = [i for b in bins for i in reversed(b)]
+    by_key = {}
+    for i in sorted_:
+        by_key.setdefault(calls[i].key, []).insert(0, i)   # dicts keep first-appearance order
+    nmax, queue = {}, []
+    for lst in by_key.values():
+        a = 0
+        while a < len(lst):
+            e, agg = a + 1, calls[lst[a]].count
+            while e < len(lst) and traffic[lst[e]] < 4 * traffic[lst[a]]:
+                agg += calls[lst[e]].count
+                e += 1
+            c0 = calls[lst[a]]
+            nc = ring_n_max_channels(c0.coll, agg, c0.elt_size, nranks, comm_channels, proto, nthreads)
+            for j in lst[a:e]:
+                nmax[j] = nc
+            a = e
+        queue += lst
+
+    def budget_ok(n_batches, work_bytes):
+        bb = n_batches * WORK_BATCH_BYTES
+        return bb + work_bytes <= IN_ARGS_BYTES or (bb <= IN_ARGS_BYTES and work_bytes <= OUT_ARGS_BYTES)
+
+    plan_of, works = [None] * len(calls), [None] * len(calls)
+    head, plan = 0, 0
+    while head < len(queue):
+        n_plan, tb, nch, wb = 0, 0, 0, 0
+        for i in queue[head:]:
+            if not budget_ok(_div_up(n_plan, 4), wb + WORK_COLL_BYTES):
+                break
+            n_plan += 1
+            wb += WORK_COLL_BYTES
+            tb += max(MIN_TRAFFIC_PER_CHANNEL, traffic[i])
+            nch = min(nch + nmax[i], comm_channels)
+        cur = dict(tpc=max(MIN_TRAFFIC_PER_CHANNEL, tb // nch), ch=0, cur=0, nmax=comm_channels)
+        batch = {}                        # channel -> [func, offsetBase, wipBytes]
+        n_batches = work_bytes = 0
+        while n_plan and head < len(queue):
+            i = queue[head]
+            c = calls[i]
+            w, nxt = _place(cur, c.coll, c.count, c.elt_size, nranks, proto, buff_size)
+            if not budget_ok(n_batches + w.channel_hi - w.channel_lo + 1, work_bytes + WORK_COLL_BYTES):
+                break
+            cur = nxt
+            for ch in range(w.channel_lo, w.channel_hi + 1):
+                b = batch.get(ch)
+                new = b is None or b[0] != c.func or b[2] + WORK_COLL_BYTES > MAX_BATCH_BYTES
+                off = 0 if new else work_bytes - b[1]
+                if new or 63 * WORK_COLL_BYTES < off:
+                    b = [c.func, work_bytes, 0 if new else b[2]]
+                    n_batches += 1
+                b[0] = c.func
+                b[2] += WORK_COLL_BYTES
+                batch[ch] = b
+            work_bytes += WORK_COLL_BYTES
+            plan_of[i], works[i] = plan, w
+            head += 1
+            n_plan -= 1
+        plan += 1
+    return queue, plan_of, works
 
 
 def allreduce_owner(work: CbdWork, count, nranks):

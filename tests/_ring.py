@@ -56,11 +56,20 @@ def ring_orders(n):
     return [list(range(n))]
 
 
+def default_per_ring(n):
+    """The library's link-bound channel model (host/init.cc):
+    ceil(8 x 76.8 GB/s / (k x 40 GB/s)) channels per ring, k = rings per arc
+    (2 for the 4-GPU set), within VCCL's MAXCHANNELS of 64 in total."""
+    k = 2 if n == 4 else 1
+    model = -(-8 * 768 // (10 * 40 * k))
+    return max(1, min(model, 64 // len(ring_orders(n))))
+
+
 def n_channels(n, per_ring=None, nch=None):
     """Library default channel count (host/init.cc) unless overridden."""
     rings = ring_orders(n)
     if per_ring is None:
-        per_ring = 16 if n >= 4 else 48 if n == 3 else 96
+        per_ring = default_per_ring(n)
     c = nch if nch is not None else per_ring * len(rings)
     return max(1, min(c, 128))  # kMaxChannels
 
@@ -82,19 +91,42 @@ def _sched(coll, count, esz, n, nch, slot_bytes, nthreads, proto):
                           nthreads=nthreads)
 
 
+_KERNEL_KEY = {0: 1, 1: 1, 2: 3, 3: 3, 4: 5, 5: 5}  # signed ints run the unsigned kernel
+
+
+def group_works(calls, n, nch, slot_bytes=512 << 10, nthreads=512):
+    """VCCL's group plan (oracle/vccl_sched.py plan_schedule) for a group's
+    ring / direct calls of one comm, in call order: calls = [(coll "ar" |
+    "rs" | "ag", op, dtype, count)]; returns every call's CbdWork."""
+    gc = []
+    for coll, op, dt, count in calls:
+        esz = np.dtype(O.NP_DTYPE[dt]).itemsize
+        if coll == "ag":
+            key = func = ("ag", 0, 0)
+        else:
+            dev_op, _ = O.host_to_dev_redop(op, dt, n)
+            key = (coll, dev_op, dt)
+            func = (coll, dev_op, _KERNEL_KEY.get(dt, dt))
+        gc.append(S.GroupCall(coll, count, esz, key, func))
+    return S.plan_schedule(gc, n, nch, buff_size=slot_bytes * S.NCCL_STEPS, nthreads=nthreads)[2]
+
+
 def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=512,
-                       proto=S.PROTO_SIMPLE):
+                       proto=S.PROTO_SIMPLE, work=None):
     """Exact expected ring all-reduce output (identical on every rank): the
     oracle's restatement of VCCL's channel partition and chunking
     (oracle/vccl_sched.py) decides channel and finishing ring index per
-    element, channel c runs on rings[c % len(rings)], the C oracle folds."""
+    element, channel c runs on rings[c % len(rings)], the C oracle folds.
+    `work`: the call's partition inside its group's plan (group_works), else
+    the call planned alone."""
     n = len(inputs)
     rings = rings or ring_orders(n)
     dev_op, arg = O.host_to_dev_redop(op, dtype, n)
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size
     esz = inputs[0].dtype.itemsize
-    work = _sched("ar", count, esz, n, nch, slot_bytes, nthreads, proto)
+    if work is None:
+        work = _sched("ar", count, esz, n, nch, slot_bytes, nthreads, proto)
     chan, owner = S.allreduce_owner(work, count, n)
     out = np.empty_like(inputs[0])
     for c in range(work.channel_lo, work.channel_hi + 1):
@@ -108,7 +140,7 @@ def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=
 
 
 def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=None, nthreads=512,
-                           proto=S.PROTO_SIMPLE):
+                           proto=S.PROTO_SIMPLE, work=None):
     """Per-rank expected outputs; inputs[r] has n*recvcount elements.  Rank
     r's block is folded on the ring of each element's channel (VCCL's cbd
     partition of the recvcount block), finishing at r."""
@@ -117,7 +149,8 @@ def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=N
     dev_op, arg = O.host_to_dev_redop(op, dtype, n)
     pre = dev_op == O.DEV_PREMULSUM
     count = inputs[0].size // n
-    work = _sched("rs", count, inputs[0].dtype.itemsize, n, nch, slot_bytes, nthreads, proto)
+    if work is None:
+        work = _sched("rs", count, inputs[0].dtype.itemsize, n, nch, slot_bytes, nthreads, proto)
     chan = S.channel_of(work, count)
     outs = [np.empty(count, inputs[0].dtype) for _ in range(n)]
     for c in range(work.channel_lo, work.channel_hi + 1):

@@ -7,7 +7,8 @@ Captures [LL all-reduce (small), direct all-reduce (mid), ring all-reduce
 into one graph on a side stream (after an eager call on the current stream,
 and followed by another), replays it 4 times with new integer-valued inputs (exact in any
 fold order) and checks every output; then two captures interleaved on the
-same comm (interleaved_captures); exit code 0 = all replays correct."""
+same comm (interleaved_captures); then collectives that fail inside a
+capture (failing_calls_in_capture); exit code 0 = all replays correct."""
 import os
 import sys
 
@@ -63,6 +64,82 @@ def interleaved_captures(comm, rank, n):
     return ok
 
 
+def failing_calls_in_capture(comm, rank, n):
+    """collectives that fail inside a HIP graph capture return
+    an ncclResult_t and leave the capture and the process usable.
+    (a) inside one capture: a valid all-reduce, then calls the library
+        refuses (invalid datatype; a PreMulSum op of another datatype,
+        enqueue.cc:2301-2305), then another valid all-reduce — the capture
+        ends cleanly and its replay is exact;
+    (b) 17 captures live on one comm at once: the 17th call finds every
+        ordering entry taken by a live capture and is refused with
+        ncclInvalidUsage instead of silently dropping a live capture's
+        ordering; all captures then end cleanly, and an eager
+        call afterwards is exact."""
+    m = 3 << 20
+    xa, xb = torch.empty(m, device="cuda"), torch.empty(m, device="cuda")
+    ya, yb = torch.empty_like(xa), torch.empty_like(xb)
+    scal = torch.ones(1, dtype=torch.float16, device="cuda")
+    uop = comm.create_premulsum(scal.data_ptr(), nccl.ncclFloat16, nccl.ncclScalarDevice)
+    s, g = torch.cuda.Stream(), torch.cuda.CUDAGraph()
+    codes = []
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s):
+        sp = s.cuda_stream
+        comm.all_reduce(xa.data_ptr(), ya.data_ptr(), m, nccl.ncclFloat32, nccl.ncclSum, sp)
+        for dt, op in ((99, nccl.ncclSum), (nccl.ncclFloat32, uop)):
+            try:
+                comm.all_reduce(xa.data_ptr(), ya.data_ptr(), m, dt, op, sp)
+                codes.append(0)
+            except nccl.VcclError as e:
+                codes.append(e.code)
+        comm.all_reduce(xb.data_ptr(), yb.data_ptr(), m, nccl.ncclFloat32, nccl.ncclSum, sp)
+    ok = codes == [nccl.ncclInvalidArgument, nccl.ncclInvalidArgument]
+    for it in range(2):
+        def val(r, k):
+            return ((torch.arange(m, device="cuda") * (r + 2 + k) + 5 * it) % 61).float()
+        xa.copy_(val(rank, 0))
+        xb.copy_(val(rank, 1))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        ok &= torch.equal(ya, sum(val(r, 0) for r in range(n)))
+        ok &= torch.equal(yb, sum(val(r, 1) for r in range(n)))
+    comm.destroy_op(uop)
+    # (b) 17 live captures on one comm (the ordering pool holds 16)
+    k = 17
+    small = 1024
+    xs = [torch.full((small,), float(i + rank), device="cuda") for i in range(k)]
+    ys = [torch.empty(small, device="cuda") for _ in range(k)]
+    streams = [torch.cuda.Stream() for _ in range(k)]
+    graphs = [torch.cuda.CUDAGraph() for _ in range(k)]
+    res = []
+    torch.cuda.synchronize()
+    for i in range(k):
+        with torch.cuda.stream(streams[i]):
+            graphs[i].capture_begin(capture_error_mode="relaxed")
+        try:
+            comm.all_reduce(xs[i].data_ptr(), ys[i].data_ptr(), small, nccl.ncclFloat32, nccl.ncclSum,
+                            streams[i].cuda_stream)
+            res.append(0)
+        except nccl.VcclError as e:
+            res.append(e.code)
+    for i in reversed(range(k)):
+        with torch.cuda.stream(streams[i]):
+            graphs[i].capture_end()
+    ok &= res == [0] * 16 + [nccl.ncclInvalidUsage]
+    # the process is usable: an eager call, exact
+    x = torch.arange(4099, device="cuda", dtype=torch.float32) + rank
+    y = torch.empty_like(x)
+    comm.all_reduce(x.data_ptr(), y.data_ptr(), 4099, nccl.ncclFloat32, nccl.ncclSum,
+                    torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ok &= torch.equal(y, sum(torch.arange(4099, device="cuda", dtype=torch.float32) + r for r in range(n)))
+    if not ok:
+        print(f"rank {rank}: failing calls in capture: codes {codes}, pool {res}", flush=True)
+    return ok
+
+
 def main():
     rank, n = int(sys.argv[1]), int(sys.argv[2])
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
@@ -115,6 +192,7 @@ def main():
     torch.cuda.synchronize()
     ok &= torch.equal(eager_y, exp_eager)
     ok &= interleaved_captures(comm, rank, n)
+    ok &= failing_calls_in_capture(comm, rank, n)
     ok &= comm.async_error() == 0
     comm.destroy()
     sys.exit(0 if ok else 4)

@@ -148,27 +148,46 @@ def gen_group_input(gi, rank):
     return rng.uniform(-1, 1, count).astype(O.NP_DTYPE[dt])
 
 
+def group_plan_works(n_ranks, nch, slot_bytes, ll_max=0, nthreads=512, proto=2):
+    """{group index: CbdWork} of the GROUP_CASES calls the library plans as
+    one VCCL group plan (host/enqueue.cc launch_planned): every call on the
+    SIMPLE ring or the direct path, i.e. above the LL threshold; the LL128
+    ring (proto 1) plans its calls one by one."""
+    if proto != 2:
+        return {}
+    idx = [gi for gi, (name, op, dt, count) in enumerate(GROUP_CASES)
+           if count * np.dtype(O.NP_DTYPE[dt]).itemsize > ll_max]
+    if not idx:
+        return {}
+    works = _ring.group_works([("ar", GROUP_CASES[gi][1], GROUP_CASES[gi][2], GROUP_CASES[gi][3])
+                               for gi in idx], n_ranks, nch, slot_bytes, nthreads)
+    return dict(zip(idx, works))
+
+
 def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
-                   nthreads=512, proto=2):
+                   nthreads=512, proto=2, plan=None):
+    """`plan`: group_plan_works(...) of the group (VCCL's grouped partition)."""
     name, op, dt, count = GROUP_CASES[gi]
     ins = [gen_group_input(gi, r) for r in range(n_ranks)]
     return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                       nthreads, proto)
+                       nthreads, proto, work=(plan or {}).get(gi))
 
 
 def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                nthreads=512, proto=2):
+                nthreads=512, proto=2, work=None):
     """All-reduce result: LL chain fold up to ll_max bytes, the ring's
     owner-map fold (VCCL's ring schedule on these channels) above — for the
     two-shot direct path too, which folds every element in the ring's order
     (direct.hpp phase 2), so neither direct_max nor the inbox chunk
-    (direct_chunk) changes the expected bits."""
+    (direct_chunk) changes the expected bits.  `work`: the call's place in
+    its group's plan."""
     del direct_max, direct_chunk
     count = len(ins[0])
     if count * ins[0].dtype.itemsize <= ll_max:
         dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
         return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
-    return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes, nthreads=nthreads, proto=proto)
+    return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes, nthreads=nthreads, proto=proto,
+                                    work=work)
 
 
 def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
@@ -207,6 +226,19 @@ def vccl_reference(case_idx, n_ranks):
         return _ring.expected_reducescatter(op, dt, ins, VCCL_REF_CHANNELS, VCCL_REF_SLOT, rings=ring)
     e = _ring.expected_allreduce(op, dt, ins, VCCL_REF_CHANNELS, VCCL_REF_SLOT, rings=ring)
     return [e] * n_ranks
+
+
+def vccl_group_reference(gi, n_ranks, vplan):
+    """VCCL's own result for a float sum/prod GROUP_CASES call: its grouped
+    ring schedule (vplan = group_plan_works on VCCL_REF_CHANNELS, every call
+    taken as RING / SIMPLE) folded on identity rings; None outside the
+    tolerance check."""
+    name, op, dt, count = GROUP_CASES[gi]
+    if dt not in (6, 7, 8, 9) or op not in TOLERANCE_OPS:
+        return None
+    ins = [gen_group_input(gi, r) for r in range(n_ranks)]
+    return _ring.expected_allreduce(op, dt, ins, VCCL_REF_CHANNELS, VCCL_REF_SLOT,
+                                    rings=[list(range(n_ranks))], work=vplan[gi])
 
 
 def out_count(case_idx, n_ranks):

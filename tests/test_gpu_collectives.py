@@ -280,11 +280,26 @@ def test_beyond_2gib_two_ranks():
 
 
 def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512, proto=2):
+    """Bit-exact against VCCL's GROUPED schedule on our rings and channels:
+    the calls on the ring / direct paths take their place in VCCL's
+    multi-task plan (oracle plan_schedule); fp sum / prod also
+    within the §8c tolerance of the exact value and of VCCL's grouped result
+    on its reference geometry."""
+    plan = RC.group_plan_works(n, nch, slot, ll_max, nthreads, proto)
+    vplan = RC.group_plan_works(n, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT)
     for gi, (name, op, dt, count) in enumerate(RC.GROUP_CASES):
-        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto)
+        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto, plan=plan)
         for r in range(n):
             assert_bitexact(dt, outs[r][name], exp, minmax=op in (2, 3),
                             what=f"group {name} n={n} rank {r}")
+        vref = RC.vccl_group_reference(gi, n, vplan)
+        if vref is not None:
+            ins = [RC.gen_group_input(gi, r) for r in range(n)]
+            for r in range(n):
+                assert_fold_tolerance(dt, op, outs[r][name], exact_f64(dt, op, ins), ins, exp_is_exact=True,
+                                      what=f"group {name} n={n} rank {r} vs exact")
+                assert_fold_tolerance(dt, op, outs[r][name], vref, ins,
+                                      what=f"group {name} n={n} rank {r} vs VCCL grouped schedule")
 
 
 def test_group_fusion_single_process(monkeypatch):
@@ -426,16 +441,35 @@ def test_group_zero_pattern(n, geom):
     want = {"default": ("ring", "ring"), "test": ("direct", "direct"), "ring_only": ("ring", "ring")}[geom]
     assert (str(res[0]["algo_rs"]), str(res[0]["algo_ar"])) == want
     assert int(res[0]["fused"]) == 2, int(res[0]["fused"])  # one RS launch + one AR launch
-    for name, dt, count in G.GROUP_RS:
+    # VCCL's grouped plan of the 24 calls: bit-exact on our
+    # rings and channels, within tolerance of VCCL's grouped result on its
+    # reference geometry
+    calls = [("rs", 0, dt, count // n) for _, dt, count in G.GROUP_RS] + \
+            [("ar", 0, dt, count) for _, dt, count in G.GROUP_AR]
+    works = _ring.group_works(calls, n, nch, slot)
+    vworks = _ring.group_works(calls, n, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT)
+    ident = [list(range(n))]
+    for i, (name, dt, count) in enumerate(G.GROUP_RS):
         ins = [G.gen(name, dt, count, r) for r in range(n)]
-        exp = _ring.expected_reducescatter(0, dt, ins, nch, slot)
+        exp = _ring.expected_reducescatter(0, dt, ins, nch, slot, work=works[i])
+        vref = _ring.expected_reducescatter(0, dt, ins, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT,
+                                            rings=ident, work=vworks[i])
+        blk = count // n
         for r in range(n):
             assert_bitexact(dt, res[r][name], exp[r], what=f"{name} n={n} {geom} rank {r}")
-    for name, dt, count in G.GROUP_AR:
+            xs = [x[r * blk:(r + 1) * blk] for x in ins]
+            assert_fold_tolerance(dt, 0, res[r][name], vref[r], xs,
+                                  what=f"{name} n={n} {geom} rank {r} vs VCCL grouped")
+    for i, (name, dt, count) in enumerate(G.GROUP_AR):
         ins = [G.gen(name, dt, count, r) for r in range(n)]
-        exp = _ring.expected_allreduce(0, dt, ins, nch, slot)
+        k = len(G.GROUP_RS) + i
+        exp = _ring.expected_allreduce(0, dt, ins, nch, slot, work=works[k])
+        vref = _ring.expected_allreduce(0, dt, ins, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT, rings=ident,
+                                        work=vworks[k])
         for r in range(n):
             assert_bitexact(dt, res[r][name], exp, what=f"{name} n={n} {geom} rank {r}")
+            assert_fold_tolerance(dt, 0, res[r][name], vref, ins,
+                                  what=f"{name} n={n} {geom} rank {r} vs VCCL grouped")
 
 
 @pytest.mark.parametrize("n", [2, 4])

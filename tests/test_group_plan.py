@@ -1,0 +1,182 @@
+"""VCCL's multi-task plan for a group of ring calls — CPU checks.
+
+* the library's group planner (vcclGroupPlan, host/enqueue.cc group_plan)
+  equals the oracle's independent restatement (oracle/vccl_sched.py
+  plan_schedule) over random groups of mixed collectives, types, ops and
+  sizes, and a group of one call equals the one-call partition;
+* hand-derived cases worked through from enqueue.cc:352-437 (sorter, bins,
+  4x aggregation) and :549-681 (shared trafficPerChannel, running channelId /
+  currentTraffic);
+* a group too large for one kernel's argument budget splits into plans whose
+  channel assignment restarts at channel 0 (enqueue.cc:535, :636);
+* NCCL_ALGO / NCCL_PROTO list parsing (vcclAlgoSelection, graph/tuning.cc:
+  53-116 parseList semantics).
+"""
+import numpy as np
+import pytest
+
+from oracle import vccl_sched as S
+from vccl_amd import nccl
+
+COLL = {0: "ar", 1: "rs", 2: "ag"}
+ESZ = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2, 10: 1, 11: 1}
+
+
+def _oracle_calls(calls, n):
+    """GroupCall list for the oracle: bins by (func, devOp, type) — AG as
+    int8 copies — and device functions with the signed -> unsigned kernel
+    equivalence (generate.py:129-137)."""
+    out = []
+    for coll, count, dt, op in calls:
+        if coll == 2:
+            key = func = (2, 0, 0)
+        else:
+            dev_op, _ = nccl.host_to_dev_redop(op, dt, n)
+            key = (coll, dev_op, dt)
+            func = (coll, dev_op, nccl.kernel_type_of(dev_op, dt))
+        out.append(S.GroupCall(COLL[coll], count, ESZ[dt], key, func))
+    return out
+
+
+def _as_tuple(w):
+    per = S.grain_size(w.proto) // w.elt_size
+    return (w.channel_lo, w.channel_hi, w.count_lo, w.count_mid, w.count_hi,
+            w.chunk_grains_lo * per, w.chunk_grains_mid * per, w.chunk_grains_hi * per)
+
+
+def _check_equal(calls, n, nch, slot=512 << 10, nthreads=512):
+    order, plan_of, parts = nccl.group_plan(calls, n, nch, slot, nthreads)
+    o_order, o_plan, o_works = S.plan_schedule(_oracle_calls(calls, n), n, nch,
+                                               buff_size=slot * S.NCCL_STEPS, nthreads=nthreads)
+    assert order == o_order, (calls, order, o_order)
+    assert plan_of == o_plan, (calls, plan_of, o_plan)
+    for i, (lib, w) in enumerate(zip(parts, o_works)):
+        ref = _as_tuple(w)
+        assert lib[:5] == ref[:5], (i, calls[i], lib, ref)
+        for k, cnt in ((5, w.count_lo), (6, w.count_mid), (7, w.count_hi)):
+            if cnt:
+                assert lib[k] == ref[k], (i, calls[i], k)
+    return order, plan_of, parts
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_library_group_plan_equals_oracle(n):
+    rng = np.random.default_rng(100 + n)
+    for trial in range(60):
+        k = int(rng.integers(1, 17))
+        calls = []
+        for _ in range(k):
+            coll = int(rng.integers(0, 3))
+            dt = int(rng.choice([7, 9, 6, 2, 3, 0, 8]))
+            op = int(rng.choice([0, 1, 2, 3]))
+            count = int(rng.choice([1, 100, 4096, 65_536, 1 << 20, (1 << 20) + 37, 3 << 20, 1 << 24])) \
+                + int(rng.integers(0, 64))
+            calls.append((coll, count, dt, op))
+        nch = int(rng.choice([1, 2, 16, 48, 56, 64]))
+        _check_equal(calls, n, nch)
+
+
+def test_single_call_group_is_the_call_partition():
+    for n in (2, 4, 8):
+        for nch in (1, 16, 56):
+            for coll, count, dt in ((0, 1 << 20, 7), (1, 12345, 9), (2, 1 << 22, 6), (0, 3, 7)):
+                _, _, parts = nccl.group_plan([(coll, count, dt, 0)], n, nch)
+                assert parts[0] == nccl.ring_partition(coll, count, dt, n, nch, 512 << 10), \
+                    (n, nch, coll, count)
+
+
+def test_hand_derived_four_allreduces():
+    """4 fp32 all-reduces of 4 MiB at 8 ranks on 56 channels (enqueue.cc:
+    549-681 by hand): traffic 8 MiB each, all in one aggregate (nc stays 56),
+    trafficPerChannel = 32 MiB / 56 = 599,186 B; 8 KiB cells (16 KiB traffic),
+    512 cells per call, cellsPerChannel = 37.
+      call 0 at (ch 0, 0 B):        lo 37, 12 mid, hi 31 -> ch 0..13, next (13, 507,904)
+      call 1 at (13, 507,904):      lo 6,  13 mid, hi 25 -> ch 13..27, next (27, 409,600)
+      call 2 at (27, 409,600):      lo 12, 13 mid, hi 19 -> ch 27..41, next (41, 311,296)
+      call 3 at (41, 311,296):      lo 18, 13 mid, hi 13 -> ch 41..55
+    """
+    calls = [(0, 1 << 20, 7, 0)] * 4
+    order, plan_of, parts = _check_equal(calls, 8, 56)
+    assert order == [0, 1, 2, 3] and plan_of == [0, 0, 0, 0]
+    e = 2048  # elements per 8 KiB cell
+    want = [(0, 13, 37 * e, 37 * e, 31 * e), (13, 27, 6 * e, 37 * e, 25 * e),
+            (27, 41, 12 * e, 37 * e, 19 * e), (41, 55, 18 * e, 37 * e, 13 * e)]
+    assert [p[:5] for p in parts] == want
+
+
+def test_hand_derived_order_and_aggregation():
+    """The plan order (enqueue.cc:352-437): sorter bins by trafficBytes
+    descending (newest first within a bin), then one LIFO per (func, op,
+    type) -> size-ascending lists in order of first appearance.  Calls at 4
+    ranks: 0 = AR f32 2^18 (2 MiB traffic), 1 = RS bf16 recvcount 2^20
+    (8 MiB), 2 = AR f32 2^22 (32 MiB), 3 = AR f32 2^20 (8 MiB).  Sorted:
+    [2, 3, 1, 0] (3 and 1 share a bin, 3 is newer); AR list [0, 3, 2], RS
+    list [1]; AR first -> order [0, 3, 2, 1].  No two AR calls aggregate
+    (8 MiB is not < 4 x 2 MiB, 32 MiB is not < 4 x 8 MiB)."""
+    calls = [(0, 1 << 18, 7, 0), (1, 1 << 20, 9, 0), (0, 1 << 22, 7, 0), (0, 1 << 20, 7, 0)]
+    order, plan_of, parts = _check_equal(calls, 4, 48)
+    assert order == [0, 3, 2, 1]
+    assert set(plan_of) == {0}
+    # channels are handed out in plan order: each call starts where the
+    # previous one stopped
+    assert parts[0][0] == 0
+    for a, b in zip(order, order[1:]):
+        assert parts[b][0] in (parts[a][1], parts[a][1] + 1), (a, b, parts[a], parts[b])
+    # a min and a max reduction share ncclPrepareTasks' bin (one devOp,
+    # MinMax): calls 0 (min), 1 (max), 2 (sum), equal sizes -> one sorter
+    # bin, newest first [2, 1, 0]; the sum bin appears first; the MinMax LIFO
+    # gives [0, 1] -> order [2, 0, 1]
+    o, _, _ = _check_equal([(0, 1 << 20, 7, 3), (0, 1 << 20, 7, 2), (0, 1 << 20, 7, 0)], 4, 48)
+    assert o == [2, 0, 1]
+
+
+def test_aggregation_lowers_channel_tuning():
+    """Four 64 KiB f32 all-reduces aggregate (each within 4x of the first):
+    nMaxChannels is tuned on the aggregate's 256 KiB, not on 64 KiB."""
+    calls = [(0, 16384, 7, 0)] * 4
+    o_works = S.plan_schedule(_oracle_calls(calls, 8), 8, 56)[2]
+    # alone, a 64 KiB all-reduce keeps 2 channels (S.ring_n_max_channels); the
+    # aggregate's 256 KiB gives 8, so the plan spreads the four calls further
+    assert S.ring_n_max_channels("ar", 16384, 4, 8, 56) == 2
+    assert S.ring_n_max_channels("ar", 4 * 16384, 4, 8, 56) == 8
+    assert max(w.channel_hi for w in o_works) >= 4
+    _check_equal(calls, 8, 56)
+
+
+def test_budget_splits_plans():
+    """A group too large for one kernel's arguments is cut into several plans
+    (enqueue.cc:533-545: the estimate admits calls while divUp(calls, 4)
+    16-byte batches fit 4 KiB - 32 B of arguments: call k is admitted while
+    16 * divUp(k, 4) <= 4,064, so 1,017 calls); each
+    plan hands out channels from 0 again."""
+    calls = [(0, 1024 + 4 * (i % 7), 7, 0) for i in range(1100)]
+    order, plan_of, parts = _check_equal(calls, 8, 64)
+    assert plan_of.count(0) == 1017
+    assert max(plan_of) >= 1, plan_of
+    for p in set(plan_of):
+        first = [i for i in order if plan_of[i] == p][0]
+        assert parts[first][0] == 0
+
+
+def test_algo_selection():
+    LL, LL128, SIMPLE, DIRECT = 1, 2, 4, 8
+    cases = {
+        (None, None): (0, LL | LL128 | SIMPLE | DIRECT),
+        (None, "LL128"): (4, LL128),
+        (None, "^LL128"): (0, LL | SIMPLE | DIRECT),      # excludes LL128
+        (None, "LL,LL128"): (0, LL | LL128),              # no longer "LL128 everywhere"
+        (None, "ll"): (2, LL),
+        (None, "Simple"): (0, SIMPLE | DIRECT),
+        ("Ring", None): (0, LL128 | SIMPLE),
+        ("Ring", "Simple"): (1, SIMPLE),
+        ("Tree", None): (2, LL),
+        ("Direct", None): (3, DIRECT),
+        ("^Direct", None): (0, LL | LL128 | SIMPLE),
+        ("ring;allreduce:tree", None): (0, LL128 | SIMPLE),  # per-collective entries ignored
+    }
+    for (algo, proto), want in cases.items():
+        assert nccl.algo_selection(algo, proto) == want, (algo, proto)
+    for algo, proto in ((None, "bogus"), ("Ring,Foo", None), (None, "^LL,LL128,Simple")):
+        with pytest.raises(nccl.VcclError) as e:
+            nccl.algo_selection(algo, proto)
+        assert e.value.code == nccl.ncclInvalidUsage

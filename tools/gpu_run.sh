@@ -26,7 +26,7 @@ export TMPDIR=/tmp
 for s in "$@"; do
   echo "== $s $(date +%T)"
   case $s in
-    test) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 ;;
+    test) timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 ;;
     test:*) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#test:}" > $O/pytest_${s#test:}.log 2>&1 ;;
     bench) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err ;;
     prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --no-extras > $O/bench_prof.json 2> $O/bench_prof.err) ;;

@@ -18,11 +18,14 @@ namespace vccl {
 
 constexpr int kSteps = 8;            // NCCL_STEPS (device.h:24)
 constexpr int kMaxRanks = 64;
-// MAXCHANNELS (device.h:62) is 64 in the reference; here 128: a channel is
-// one workgroup on one CU, and a ring channel's rate is bounded by its CU's
-// memory rate (tools/step_probe.py), so wide rings need more of the 256 CUs
-// than an NVLink GPU's SMs (2 ranks on one GPU: 64 -> 96 -> 128 channels,
-// 512 MiB AR 1039 -> 868 -> 845 us, profiles/r03q).
+// MAXCHANNELS (device.h:62) is 64 in the reference: the default channel
+// counts stay within it (kVcclMaxChannels, host/init.cc), so VCCL can run the
+// same geometry.  NCCL_NCHANNELS / VCCL_CHANNELS_PER_RING may go up to 128
+// here: a channel is one workgroup on one CU, and on one GPU shared by
+// several ranks (the rehearsals) the ring is bound by its channels' copy rate
+// (2 ranks on one GPU: 64 -> 96 -> 128 channels, 512 MiB AR 1039 -> 868 ->
+// 845 us, profiles/r03q).
+constexpr int kVcclMaxChannels = 64;
 #ifndef VCCL_MAX_CHANNELS
 #define VCCL_MAX_CHANNELS 128
 #endif

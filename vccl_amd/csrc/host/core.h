@@ -143,7 +143,8 @@ struct ncclComm {
   vccl::DirectPeers* dPeers = nullptr;  // device-resident peer table
   vccl::NetProxy* net = nullptr;  // inter-node ring connections (proxy.cc)
   int netListenFd = -1;        // proxy listener, open from init until connections are made
-  int algoForce = 0;           // NCCL_ALGO/NCCL_PROTO: 0 auto, 1 ring/SIMPLE, 2 tree/LL, 3 direct
+  int algoForce = 0;           // NCCL_ALGO/NCCL_PROTO: 0 auto, 1 ring/SIMPLE, 2 tree/LL, 3 direct, 4 LL128 ring
+  int algoAllowed = 15;        // paths the NCCL_ALGO / NCCL_PROTO lists leave (init.cc algo_proto_select)
   vccl::DevComm* devComm = nullptr;
   vccl::DevChannel* devChannels = nullptr;
   volatile int* abortFlag = nullptr;  // host pinned, mapped

@@ -26,6 +26,16 @@ namespace vccl {
 
 enum Coll { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2 };
 
+// One call's part of VCCL's channel partition (ncclDevWorkColl channelLo /
+// channelHi + cbd, device.h:258-287): channels [channelLo, channelHi] carry
+// parts of countLo / countMid... / countHi elements, moved in chunks of
+// chunkLo / chunkMid / chunkHi elements.
+struct CbdPlan {
+  int channelLo, channelHi;
+  int64_t countLo, countMid, countHi;
+  int64_t chunkLo, chunkMid, chunkHi;  // elements
+};
+
 struct Task {
   int coll;
   const void* sendbuff;
@@ -37,6 +47,10 @@ struct Task {
   const void* argPtr;  // ncclScalarDevice PreMulSum scalar
   ncclComm* comm;
   hipStream_t stream;
+  // Set by the group planner (plan_group): this call's partition inside its
+  // group's VCCL plan; otherwise the call is planned alone (cbd_schedule).
+  bool planned;
+  CbdPlan plan;
 };
 
 static thread_local int tl_groupDepth = 0;
@@ -209,25 +223,40 @@ static ncclResult_t capture_state(hipStream_t s, CaptureState* cs) {
 }
 // The ordering state of capture `id`: comm->caps is a pool of kMaxCaptures
 // entries created at init (no HIP object is created during a capture); a new
-// id takes the least recently used entry.
-static void capture_entry(ncclComm* comm, unsigned long long id, bool create,
-                          ncclComm::CapOrder** out) {
+// id takes the least recently used entry whose capture has ended.  When every
+// entry still belongs to a live capture, the call fails (ncclInvalidUsage)
+// rather than silently dropping a live capture's ordering.
+static bool capture_live(const ncclComm::CapOrder& c) {
+  if (!c.used || !c.has) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  if (hipStreamGetCaptureInfo(c.last, &st, &id) != hipSuccess) return false;
+  return st == hipStreamCaptureStatusActive && id == c.id;
+}
+static ncclResult_t capture_entry(ncclComm* comm, unsigned long long id, bool create,
+                                  ncclComm::CapOrder** out) {
   *out = nullptr;
   auto& caps = comm->caps;
   for (size_t i = 0; i < caps.size(); i++) {
     if (caps[i].used && caps[i].id == id) {
       std::rotate(caps.begin(), caps.begin() + i, caps.begin() + i + 1);  // to the front
       *out = &caps[0];
-      return;
+      return ncclSuccess;
     }
   }
-  if (!create || caps.empty()) return;
-  std::rotate(caps.begin(), caps.end() - 1, caps.end());  // the oldest entry, to the front
-  caps[0].id = id;
-  caps[0].used = true;
-  caps[0].last = nullptr;
-  caps[0].has = false;
-  *out = &caps[0];
+  if (!create || caps.empty()) return ncclSuccess;
+  for (size_t i = caps.size(); i-- > 0;) {  // least recently used first
+    if (capture_live(caps[i])) continue;
+    std::rotate(caps.begin(), caps.begin() + i, caps.begin() + i + 1);
+    caps[0].id = id;
+    caps[0].used = true;
+    caps[0].last = nullptr;
+    caps[0].has = false;
+    *out = &caps[0];
+    return ncclSuccess;
+  }
+  VWARN("more than %d stream captures are active on this communicator at once", (int)caps.size());
+  return ncclInvalidUsage;
 }
 // One capture query per call: stream_order fills `cs`, stream_mark and
 // stream_last_event reuse it (the capture state of s cannot change between
@@ -236,7 +265,7 @@ static ncclResult_t stream_order(ncclComm* comm, hipStream_t s, CaptureState* cs
   NCCLCHECK(capture_state(s, cs));
   if (cs->active) {
     ncclComm::CapOrder* c;
-    capture_entry(comm, cs->id, false, &c);
+    NCCLCHECK(capture_entry(comm, cs->id, true, &c));  // reserved before the launch
     if (c && c->has && c->last != s) HIPCHECK(hipStreamWaitEvent(s, c->ev, 0));
     return ncclSuccess;
   }
@@ -247,7 +276,7 @@ static ncclResult_t stream_order(ncclComm* comm, hipStream_t s, CaptureState* cs
 static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s, const CaptureState& cs) {
   if (cs.active) {
     ncclComm::CapOrder* c;
-    capture_entry(comm, cs.id, true, &c);
+    NCCLCHECK(capture_entry(comm, cs.id, true, &c));
     if (!c) return ncclInternalError;
     HIPCHECK(hipEventRecord(c->ev, s));
     c->last = s;
@@ -297,59 +326,76 @@ static ncclResult_t launch_one_rank(const Task& t) {
   return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
 }
 
-// VCCL's channel partition of one ring collective (scheduleCollTasksToPlan
-// for a plan holding one task, enqueue.cc:518-565 + 597-644, with the
-// channel tuning of topoGetAlgoInfo :1902-1925 and calcCollChunking's RING /
-// SIMPLE chunk :2027-2030, 2093), so every element lands on the same channel
-// and the same chunk of the same loop as in VCCL — hence the same ring and
-// fold order.  `count` / `eltSize` are already AG-rewritten to bytes.
-// Restated for the tests in oracle/vccl_sched.py.
-struct CbdPlan {
-  int channelLo, channelHi;
-  int64_t countLo, countMid, countHi;
-  int64_t chunkLo, chunkMid, chunkHi;  // elements
-};
+// VCCL's channel partition of ring collectives: the host side of
+// scheduleCollTasksToPlan (enqueue.cc:518-769) with the ring channel tuning
+// of topoGetAlgoInfo (:1902-1925) and calcCollChunking's RING chunk
+// (:2027-2032, 2093), so every element lands on the same channel and the same
+// chunk of the same loop as in VCCL — hence the same ring and fold order.
+// `count` / `eltSize` are already AG-rewritten to bytes.  Restated for the
+// tests in oracle/vccl_sched.py.
+//
 // proto: kProtoSimple or kProtoLL128.  stepBytes: that protocol's FIFO step
 // (buffSize / NCCL_STEPS).  nThreads: maxThreads[RING][proto] — NCCL_NTHREADS
 // for SIMPLE (the ring kernel's own block size here, comm->nThreads),
 // NCCL_LL128_NTHREADS (640) for LL128 (tuning.cc:198-211).
-static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
-                            int proto, int64_t stepBytes, int64_t nThreads) {
-  constexpr int64_t kMinTraffic = 16 << 10;         // enqueue.cc:528
-  // thread thresholds (comm.h:38-40): SIMPLE 64, LL128 8; grains
-  // ncclProtoGrainSize (device.h:290-295): SIMPLE 512, LL128 1920
-  const bool ll128 = proto == kProtoLL128;
-  const int64_t kSimpleThreshold = ll128 ? 8 : 64;
-  const int64_t kGrain = ll128 ? 1920 : 512;
-  auto divUp = [](int64_t a, int64_t b) { return (a + b - 1) / b; };
-  const int64_t tpb = coll == kAllReduce ? 2 : nRanks;  // ncclFuncTrafficPerByte (enqueue.cc:67-74)
+constexpr uint64_t kMinTraffic = 16 << 10;  // MinTrafficPerChannel, enqueue.cc:528
+static int64_t div_up(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static int64_t traffic_per_byte(int coll, int nRanks) {  // ncclFuncTrafficPerByte (enqueue.cc:67-74)
+  return coll == kAllReduce ? 2 : nRanks;
+}
+
+// nMaxChannels of a task (or of an aggregate of tasks, ncclPrepareTasks):
+// the ring channel tuning on nBytes = eltSize * ncclFuncMaxSendRecvCount
+// (enqueue.cc:1955, 1921-1924); thread thresholds (comm.h:38-40) SIMPLE 64,
+// LL128 8.
+static int ring_nmax_channels(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
+                              int proto, int64_t nThreads) {
+  const int64_t threshold = proto == kProtoLL128 ? 8 : 64;
   const int64_t nBytes = eltSize * (coll == kAllReduce ? count : (int64_t)nRanks * count);
-  int64_t nc = commChannels;                        // enqueue.cc:1921-1924
-  while (nBytes < nc * nThreads * kSimpleThreshold && nc >= 2) nc--;
-  const int64_t traffic = std::max(kMinTraffic, count * eltSize * tpb);
-  const int64_t nMax = commChannels;
-  const int64_t trafficPerChannel = std::max(kMinTraffic, traffic / std::min(nc, nMax));
-  int64_t channelId = 0;
-  const int64_t cellSize = divUp(divUp(kMinTraffic, tpb), 16) * 16;
-  const int64_t eltsPerCell = cellSize / eltSize;
-  const int64_t cells = divUp(count * eltSize, cellSize);
-  const int64_t trafficPerCell = cellSize * tpb;
-  int64_t cellsPerChannel = std::min(cells, divUp(trafficPerChannel, trafficPerCell));
-  int64_t cellsLo = channelId + 1 == nMax ? cells : std::min(cells, divUp(trafficPerChannel, trafficPerCell));
-  int64_t nMid = (cells - cellsLo) / cellsPerChannel;
-  int64_t cellsHi = (cells - cellsLo) % cellsPerChannel;
-  int64_t nCh = (cellsLo ? 1 : 0) + nMid + (cellsHi ? 1 : 0);
-  if (nMax < channelId + nCh) {
-    nMid = nMax - channelId - 2;
-    cellsPerChannel = (cells - cellsLo) / (nMid + 1);
-    cellsHi = cellsPerChannel + (cells - cellsLo) % (nMid + 1);
+  int64_t nc = commChannels;
+  while (nBytes < nc * nThreads * threshold && nc >= 2) nc--;
+  return (int)nc;
+}
+
+// The running channel position of a plan (scheduleCollTasksToPlan's
+// trafficPerChannel / channelId / currentTraffic, enqueue.cc:549-565).
+struct PlanCursor {
+  uint64_t trafficPerChannel;
+  int channelId;
+  uint64_t currentTraffic;
+  int nMax;  // nMaxChannels[kind] = comm->nChannels
+};
+
+// The cbd cell split of one task at the cursor (enqueue.cc:597-644), then
+// the cursor advanced past it (:667-681).  Returns the task's channel count.
+static CbdPlan cbd_place(PlanCursor& pc, int coll, int64_t count, int64_t eltSize, int nRanks,
+                         int proto, int64_t stepBytes) {
+  const bool ll128 = proto == kProtoLL128;
+  const uint64_t tpb = (uint64_t)traffic_per_byte(coll, nRanks);
+  const uint64_t cellSize = (uint64_t)div_up(div_up(kMinTraffic, tpb), 16) * 16;
+  const uint64_t eltsPerCell = cellSize / (uint64_t)eltSize;
+  const uint64_t cells = (uint64_t)div_up(count * eltSize, (int64_t)cellSize);
+  const uint64_t trafficPerElement = (uint64_t)eltSize * tpb;
+  const uint64_t trafficPerCell = cellSize * tpb;
+  const uint64_t tpc = pc.trafficPerChannel;
+  uint64_t cellsPerChannel = std::min(cells, (tpc + trafficPerCell - 1) / trafficPerCell);
+  uint64_t cellsLo;
+  if (pc.channelId + 1 == pc.nMax) cellsLo = cells;  // on the last channel everything goes to "lo"
+  else cellsLo = std::min(cells, (tpc - pc.currentTraffic + trafficPerCell - 1) / trafficPerCell);
+  int nMid = (int)((cells - cellsLo) / cellsPerChannel);
+  uint64_t cellsHi = (cells - cellsLo) % cellsPerChannel;
+  int nCh = (cellsLo != 0 ? 1 : 0) + nMid + (cellsHi != 0 ? 1 : 0);
+  if (pc.nMax < pc.channelId + nCh) {  // overflowed the available channels
+    nMid = pc.nMax - pc.channelId - 2;
+    cellsPerChannel = (cells - cellsLo) / (uint64_t)(nMid + 1);
+    cellsHi = cellsPerChannel + (cells - cellsLo) % (uint64_t)(nMid + 1);
   }
   if (cellsHi == 0 && nMid != 0) {
     cellsHi = cellsPerChannel;
     nMid -= 1;
   }
-  if (cellsLo == 0) {
-    channelId += 1;
+  if (cellsLo == 0) {  // least channel skipped: the next one becomes the least
+    pc.channelId += 1;
     if (nMid == 0) {
       cellsLo = cellsHi;
       cellsHi = 0;
@@ -359,21 +405,192 @@ static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks
     }
   }
   CbdPlan p{};
-  p.countMid = nMid != 0 ? cellsPerChannel * eltsPerCell : 0;
-  p.countLo = cellsLo * eltsPerCell;
-  p.countHi = cellsHi * eltsPerCell;
-  (p.countHi != 0 ? p.countHi : p.countLo) -= cells * eltsPerCell - count;
-  nCh = (p.countLo ? 1 : 0) + nMid + (cellsHi ? 1 : 0);
-  p.channelLo = (int)channelId;
-  p.channelHi = (int)(channelId + nCh - 1);
+  p.countMid = nMid != 0 ? (int64_t)(cellsPerChannel * eltsPerCell) : 0;
+  p.countLo = (int64_t)(cellsLo * eltsPerCell);
+  p.countHi = (int64_t)(cellsHi * eltsPerCell);
+  (p.countHi != 0 ? p.countHi : p.countLo) -= (int64_t)(cells * eltsPerCell) - count;
+  nCh = (p.countLo != 0 ? 1 : 0) + nMid + (cellsHi != 0 ? 1 : 0);
+  p.channelLo = pc.channelId;
+  p.channelHi = pc.channelId + nCh - 1;
   // RING chunk (calcCollChunking, enqueue.cc:2027-2032, 2093): SIMPLE =
   // chunkSteps (4) FIFO steps of buffSize / NCCL_STEPS (= one slot here);
-  // LL128 = one step, 15/16 of it data; rounded down to the protocol grain;
-  // independent of size.
+  // LL128 = one step, 15/16 of it data; rounded down to the protocol grain
+  // (device.h:290-295: SIMPLE 512, LL128 1920); independent of size.
+  const int64_t grain = ll128 ? 1920 : 512;
   const int64_t chunkBytes = ll128 ? stepBytes / 16 * 15 : 4 * stepBytes;
-  const int64_t chunkElts = chunkBytes / kGrain * kGrain / eltSize;
+  const int64_t chunkElts = chunkBytes / grain * grain / eltSize;
   p.chunkLo = p.chunkMid = p.chunkHi = chunkElts;
+  // advance the cursor (enqueue.cc:667-681)
+  if (p.countHi != 0) {
+    pc.channelId += nCh - 1;
+    pc.currentTraffic = cellsHi * eltsPerCell * trafficPerElement;
+  } else if (nMid != 0) {
+    pc.channelId += nCh;
+    pc.currentTraffic = 0;
+  } else {
+    pc.currentTraffic += cellsLo * eltsPerCell * trafficPerElement;
+  }
+  if (pc.currentTraffic >= tpc && pc.channelId + 1 != pc.nMax) {
+    pc.channelId += 1;
+    pc.currentTraffic = 0;
+  }
   return p;
+}
+
+// A plan holding one ring collective (a call outside a group).
+static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
+                            int proto, int64_t stepBytes, int64_t nThreads) {
+  const int nc = ring_nmax_channels(coll, count, eltSize, nRanks, commChannels, proto, nThreads);
+  const uint64_t traffic = std::max<uint64_t>(kMinTraffic, (uint64_t)(count * eltSize) * traffic_per_byte(coll, nRanks));
+  PlanCursor pc{std::max<uint64_t>(kMinTraffic, traffic / (uint64_t)std::min(nc, commChannels)), 0, 0,
+                commChannels};
+  return cbd_place(pc, coll, count, eltSize, nRanks, proto, stepBytes);
+}
+
+// ---------------------------------------------------------------- group plan
+// VCCL's plan for a group's ring collectives of one comm (every call here
+// taken to run as RING / SIMPLE, the protocol VCCL's tuner picks for
+// bandwidth-bound buckets):
+//  * taskAppend: trafficBytes = count * eltSize * trafficPerByte, inserted
+//    into the size sorter (enqueue.cc:2405-2413; comm.h:294-343: 81 bins of
+//    u32fpEncode(min(bytes, 1 GiB) >> 10, 2 bits) in descending size, LIFO
+//    within a bin, bitops.h:252-262);
+//  * ncclPrepareTasks (enqueue.cc:352-437): the sorted list binned by
+//    (func, devOp, type) in LIFO order — each bin size-ascending, bins in
+//    order of first appearance; runs within 4x of the run's first
+//    trafficBytes aggregated and nMaxChannels tuned on the aggregate's bytes;
+//  * scheduleCollTasksToPlan (enqueue.cc:518-769): trafficPerChannel = the
+//    plan's traffic / min(sum nMaxChannels, comm channels), each task placed
+//    at the running channelId / currentTraffic; a task that would overflow
+//    the kernel-argument budget (testBudget :278-286: 16-byte work batches
+//    within 4 KiB - 32 B of kernel arguments, 96-byte works within half the
+//    1 MiB work FIFO; batches counted as addWorkBatchToPlan :91-156 does)
+//    starts the next plan.
+// Restated for the tests in oracle/vccl_sched.py (plan_schedule).
+struct GroupTask {
+  int coll;
+  int64_t count, eltSize;  // AG in bytes
+  int binKey;              // (func, devOp, type): ncclPrepareTasks' bins
+  int funcKey;             // the device function (batches merge per function)
+};
+struct GroupPlanOut {
+  std::vector<int> order;        // tasks in execution (plan) order
+  std::vector<int> planOf;       // per task: the plan (kernel) it lands in
+  std::vector<CbdPlan> cbd;      // per task
+};
+static uint32_t u32fp_encode(uint32_t x, int bitsPerPow2) {  // bitops.h:252-262
+  const int log2x = 31 - __builtin_clz(x | 1);
+  const uint32_t mantissa = x >> (log2x >= bitsPerPow2 ? log2x - bitsPerPow2 : 0) & ((1u << bitsPerPow2) - 1);
+  const uint32_t exponent = log2x >= bitsPerPow2 ? log2x - (bitsPerPow2 - 1) : 0;
+  return exponent << bitsPerPow2 | mantissa;
+}
+static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commChannels, int64_t stepBytes,
+                       int64_t nThreads, GroupPlanOut* out) {
+  const int n = (int)ts.size();
+  std::vector<uint64_t> traffic(n);
+  for (int i = 0; i < n; i++)
+    traffic[i] = (uint64_t)(ts[i].count * ts[i].eltSize) * traffic_per_byte(ts[i].coll, nRanks);
+  // the size sorter: bins in descending size, LIFO within a bin
+  constexpr int kBinCount = 1 + (30 - 10) * 4;
+  std::vector<std::vector<int>> bins(kBinCount);
+  for (int i = 0; i < n; i++) {
+    const uint32_t x = (uint32_t)(std::min<uint64_t>(traffic[i], 1ull << 30) >> 10);
+    bins[kBinCount - 1 - (int)u32fp_encode(x, 2)].push_back(i);
+  }
+  std::vector<int> sorted;
+  for (auto& b : bins) sorted.insert(sorted.end(), b.rbegin(), b.rend());
+  // (func, op, type) bins, LIFO, in order of first appearance
+  std::vector<int> keys;
+  std::vector<std::vector<int>> byKey;
+  for (int i : sorted) {
+    const size_t k = std::find(keys.begin(), keys.end(), ts[i].binKey) - keys.begin();
+    if (k == keys.size()) {
+      keys.push_back(ts[i].binKey);
+      byKey.emplace_back();
+    }
+    byKey[k].insert(byKey[k].begin(), i);
+  }
+  std::vector<int> nMax(n), queue;
+  for (auto& lst : byKey) {
+    for (size_t a = 0; a < lst.size();) {
+      size_t e = a + 1;
+      int64_t aggCount = ts[lst[a]].count;
+      while (e < lst.size() && traffic[lst[e]] < 4 * traffic[lst[a]]) aggCount += ts[lst[e++]].count;
+      const int nc = ring_nmax_channels(ts[lst[a]].coll, aggCount, ts[lst[a]].eltSize, nRanks, commChannels,
+                                        kProtoSimple, nThreads);
+      for (size_t j = a; j < e; j++) nMax[lst[j]] = nc;
+      a = e;
+    }
+    queue.insert(queue.end(), lst.begin(), lst.end());
+  }
+  out->order = queue;
+  out->planOf.assign(n, -1);
+  out->cbd.assign(n, CbdPlan{});
+  constexpr int64_t kWorkBytes = 96, kBatchBytes = 16;   // sizeof ncclDevWorkColl / ncclDevWorkBatch
+  constexpr int64_t kInArgs = (4 << 10) - 32;            // workArgsBytes - sizeof(ncclDevKernelArgs)
+  constexpr int64_t kOutArgs = (1 << 20) / 2;            // workFifoBytes / 2
+  auto budget_ok = [&](int64_t nBatches, int64_t workBytes) {
+    const int64_t bb = nBatches * kBatchBytes;
+    return bb + workBytes <= kInArgs || (bb <= kInArgs && workBytes <= kOutArgs);
+  };
+  size_t head = 0;
+  for (int plan = 0; head < queue.size(); plan++) {
+    int nPlanColls = 0;
+    uint64_t tb = 0;
+    int nch = 0;
+    for (size_t q = head, wb = 0; q < queue.size(); q++) {
+      if (!budget_ok(div_up(nPlanColls, 4), (int64_t)wb + kWorkBytes)) break;
+      nPlanColls++;
+      wb += kWorkBytes;
+      tb += std::max<uint64_t>(kMinTraffic, traffic[queue[q]]);
+      nch = std::min(nch + nMax[queue[q]], commChannels);
+    }
+    PlanCursor pc{std::max<uint64_t>(kMinTraffic, tb / (uint64_t)std::max(nch, 1)), 0, 0, commChannels};
+    // per channel: the work batch being filled (addWorkBatchToPlan)
+    std::vector<int> lastFunc(commChannels, -1);
+    std::vector<int64_t> offsetBase(commChannels, 0), wipBytes(commChannels, 0);
+    int64_t nWorkBatches = 0, workBytes = 0;
+    while (nPlanColls != 0 && head < queue.size()) {
+      const int i = queue[head];
+      PlanCursor trial = pc;
+      const CbdPlan p = cbd_place(trial, ts[i].coll, ts[i].count, ts[i].eltSize, nRanks, kProtoSimple, stepBytes);
+      const int nChTask = p.channelHi - p.channelLo + 1;
+      if (!budget_ok(nWorkBatches + nChTask, workBytes + kWorkBytes)) break;  // the next plan
+      pc = trial;
+      for (int c = p.channelLo; c <= p.channelHi && c < commChannels; c++) {
+        const bool fresh = lastFunc[c] < 0 || lastFunc[c] != ts[i].funcKey ||
+                           wipBytes[c] + kWorkBytes > 1024;  // NCCL_MAX_DEV_WORK_BATCH_BYTES
+        const int64_t off = fresh ? 0 : workBytes - offsetBase[c];
+        if (fresh || 63 * kWorkBytes < off) {
+          offsetBase[c] = workBytes;
+          if (fresh) wipBytes[c] = 0;
+          nWorkBatches++;
+        }
+        lastFunc[c] = ts[i].funcKey;
+        wipBytes[c] += kWorkBytes;
+      }
+      workBytes += kWorkBytes;
+      out->planOf[i] = plan;
+      out->cbd[i] = p;
+      head++;
+      nPlanColls--;
+    }
+  }
+}
+
+// A call's partition: its place in its group's plan (plan_group), else the
+// plan of the call alone.
+static CbdPlan task_plan(const Task& t, int proto) {
+  const ncclComm* comm = t.comm;
+  if (t.planned && proto == kProtoSimple) return t.plan;
+  const bool ag = t.coll == kAllGather;
+  const int64_t esz = ag ? 1 : type_size(t.datatype);
+  const int64_t count = ag ? (int64_t)t.count * type_size(t.datatype) : (int64_t)t.count;
+  return proto == kProtoLL128
+             ? cbd_schedule(t.coll, count, esz, comm->nRanks, comm->nChannels, kProtoLL128,
+                            comm->ll128StepBytes, comm->ll128Threads)
+             : cbd_schedule(t.coll, count, esz, comm->nRanks, comm->nChannels, kProtoSimple,
+                            comm->stepBytes, comm->nThreads);
 }
 
 // The ring work of one call (its kernel element type and device op too).
@@ -401,11 +618,7 @@ static ncclResult_t ring_work_of(const Task& t, bool ll128, RingWork* out, int* 
   }
   w.redArgPtr = t.argPtr;  // ncclScalarDevice: dereferenced by the kernel (nccl.h.in:255-262)
   w.redArgBytes = type_size(t.datatype);
-  const int64_t esz = t.coll == kAllGather ? 1 : type_size(t.datatype);
-  const CbdPlan p = ll128 ? cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
-                                          kProtoLL128, comm->ll128StepBytes, comm->ll128Threads)
-                         : cbd_schedule(t.coll, (int64_t)w.count, esz, comm->nRanks, comm->nChannels,
-                                        kProtoSimple, comm->stepBytes, comm->nThreads);
+  const CbdPlan p = ll128 ? task_plan(t, kProtoLL128) : task_plan(t, kProtoSimple);
   if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
     return ncclInternalError;
   w.channelLo = p.channelLo;
@@ -487,9 +700,8 @@ static int dev_coll(int coll) {
 
 // The cbd partition of a reduce-scatter's block, for the one-hop LL / direct
 // reduce-scatters' per-channel fold order (the ring's own, cbd_schedule).
-static CbdLite rs_cbd(const ncclComm* comm, const Task& t) {
-  const CbdPlan p = cbd_schedule(kReduceScatter, (int64_t)t.count, type_size(t.datatype), comm->nRanks,
-                                 comm->nChannels, kProtoSimple, comm->stepBytes, comm->nThreads);
+static CbdLite rs_cbd(const Task& t) {
+  const CbdPlan p = task_plan(t, kProtoSimple);
   return CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)t.count};
 }
 
@@ -527,7 +739,7 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   }
   w.nParts = nTasks;
   w.nLines = lines;
-  if (t.coll == kReduceScatter) w.cbd = rs_cbd(comm, t);
+  if (t.coll == kReduceScatter) w.cbd = rs_cbd(t);
   if (lines > comm->llLines) return ncclInternalError;
   const int kt = t.coll == kAllGather ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
@@ -552,8 +764,10 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
 }
 
 // The direct work of one call (direct.hpp): two-shot all-reduce, one-hop
-// reduce-scatter / all-gather.
-static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, int* devOpOut) {
+// reduce-scatter / all-gather.  `blkForce` > 0 imposes the block length (a
+// fused batch's common geometry, launch_direct).
+static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, int* devOpOut,
+                                   int64_t blkForce = 0) {
   ncclComm* comm = t.comm;
   const int n = comm->nRanks;
   const bool ag = t.coll == kAllGather;
@@ -583,8 +797,7 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
     shard0 = direct_shard_elts(w.chunkElts, n, eltAlign);
     // the ring's partition of this bucket: phase 2 folds every element in the
     // order VCCL's ring all-reduce gives it on these channels (ar_chunk_of)
-    const CbdPlan p = cbd_schedule(kAllReduce, count, esz, n, comm->nChannels, kProtoSimple,
-                                   comm->stepBytes, comm->nThreads);
+    const CbdPlan p = task_plan(t, kProtoSimple);
     w.cbd = CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, count};
     w.arChunk = p.chunkLo;
   } else {
@@ -592,7 +805,7 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
     // (count elements) that fits a region; it is cut into blocks directly.
     w.chunkElts = std::min<int64_t>(count, regionElts / eltAlign * eltAlign);
     shard0 = w.chunkElts;
-    if (t.coll == kReduceScatter) w.cbd = rs_cbd(comm, t);
+    if (t.coll == kReduceScatter) w.cbd = rs_cbd(t);
   }
   w.nChunks = (int)((count + w.chunkElts - 1) / w.chunkElts);
   // Blocks of >= 16 KiB (one 512-thread x 2-pack hunk), at most the cap.
@@ -603,6 +816,10 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
   nb = std::max<int64_t>(std::min<int64_t>(nb, comm->maxCTAs), comm->minCTAs);
   nb = std::max<int64_t>(1, std::min<int64_t>({nb, (int64_t)comm->directMaxBlocks, (int64_t)kDirectMaxBlocks}));
   w.blkElts = align_up((shard0 + nb - 1) / nb, eltAlign);
+  if (blkForce > 0) {
+    if (blkForce < w.blkElts || blkForce % eltAlign) return ncclInternalError;
+    w.blkElts = blkForce;
+  }
   w.nBlocks = (int)((shard0 + w.blkElts - 1) / w.blkElts);
   w.regionBytes = comm->dRegionBytes;
   if (shard0 * esz > w.regionBytes || w.nBlocks > kDirectMaxBlocks || w.nBlocks < 1)
@@ -617,17 +834,32 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
 
 // 1 .. kDirectMaxWorks direct calls of one comm with the same collective,
 // kernel type and op in one launch on ts[0].stream (the largest part's grid).
+// Every part of a batch uses ONE block length (the largest part's): block b
+// then covers the same inbox bytes [b * blkElts, (b + 1) * blkElts) in every
+// part, so the per-block flags that order a part's region reuse also order
+// the next part's (a kernel boundary no longer separates them) — with
+// per-part lengths, workgroup b's next-part scatter could overwrite bytes a
+// peer's workgroup b' was still folding.
 static ncclResult_t launch_direct(const Task* ts, int nTasks) {
   const Task& t = ts[0];
   if (nTasks < 1 || nTasks > kDirectMaxWorks) return ncclInternalError;
   DirectBatch b{};
   int kt = -1, devOp = -1;
-  NCCLCHECK(direct_work_of(t, &b.w, &kt, &devOp));
-  for (int i = 1; i < nTasks; i++) {
+  int64_t blk = 0;
+  for (int i = 0; i < nTasks; i++) {
     DirectWork wi;
     int kti, opi;
     NCCLCHECK(direct_work_of(ts[i], &wi, &kti, &opi));
-    if (kti != kt || opi != devOp) return ncclInternalError;
+    if (i > 0 && (kti != kt || opi != devOp)) return ncclInternalError;
+    kt = kti;
+    devOp = opi;
+    blk = std::max(blk, wi.blkElts);
+  }
+  NCCLCHECK(direct_work_of(t, &b.w, &kt, &devOp, nTasks > 1 ? blk : 0));
+  for (int i = 1; i < nTasks; i++) {
+    DirectWork wi;
+    int kti, opi;
+    NCCLCHECK(direct_work_of(ts[i], &wi, &kti, &opi, blk));
     b.more[i - 1] = direct_part_of(wi);
     b.w.nBlocks = std::max(b.w.nBlocks, wi.nBlocks);
   }
@@ -740,16 +972,23 @@ static int max_parts(int algo) {
   return algo == kAlgoLL ? kLLMaxParts : algo == kAlgoDirect ? kDirectMaxWorks : kRingMaxWorks;
 }
 
-static ncclResult_t launch_fused(const std::vector<Task>& ts, int algo) {
-  ncclComm* comm = ts[0].comm;
-  const hipStream_t s0 = ts[0].stream;
+// Runs of calls of one comm, each run one launch (1 .. max_parts calls), in
+// order on the first task's stream; the other tasks' streams are joined
+// before the first launch and wait for the last.
+static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, const std::vector<int>& algos) {
+  ncclComm* comm = runs[0][0].comm;
+  const hipStream_t s0 = runs[0][0].stream;
   int old = -1;
   HIPCHECK(hipGetDevice(&old));
   if (old != comm->device) HIPCHECK(hipSetDevice(comm->device));
   std::vector<hipStream_t> others;
-  for (const Task& t : ts)
-    if (t.stream != s0 && std::find(others.begin(), others.end(), t.stream) == others.end())
-      others.push_back(t.stream);
+  size_t nTasks = 0;
+  for (const auto& run : runs) {
+    nTasks += run.size();
+    for (const Task& t : run)
+      if (t.stream != s0 && std::find(others.begin(), others.end(), t.stream) == others.end())
+        others.push_back(t.stream);
+  }
   CaptureState cs{false, 0};
   ncclResult_t r = stream_order(comm, s0, &cs);
   for (hipStream_t s : others) {
@@ -758,45 +997,101 @@ static ncclResult_t launch_fused(const std::vector<Task>& ts, int algo) {
         hipStreamWaitEvent(s0, comm->joinEvent, 0) != hipSuccess)
       r = ncclUnhandledCudaError;
   }
-  if (r == ncclSuccess) {
-    const int n = (int)ts.size();
-    r = algo == kAlgoLL ? launch_ll(ts.data(), n)
-        : algo == kAlgoDirect ? launch_direct(ts.data(), n)
-                              : launch_ring(ts.data(), n, algo == kAlgoRingLL128);
+  for (size_t k = 0; k < runs.size() && r == ncclSuccess; k++) {
+    const int n = (int)runs[k].size(), algo = algos[k];
+    r = algo == kAlgoLL ? launch_ll(runs[k].data(), n)
+        : algo == kAlgoDirect ? launch_direct(runs[k].data(), n)
+                              : launch_ring(runs[k].data(), n, algo == kAlgoRingLL128);
+    if (n > 1) comm->fusedLaunches++;
   }
   if (r == ncclSuccess) r = stream_mark(comm, s0, cs);
   const hipEvent_t done = stream_last_event(comm, cs);
   for (hipStream_t s : others)
     if (r == ncclSuccess && hipStreamWaitEvent(s, done, 0) != hipSuccess)
       r = ncclUnhandledCudaError;
-  comm->opCount += ts.size();
-  comm->fusedLaunches++;
+  comm->opCount += nTasks;
   if (old != comm->device) (void)hipSetDevice(old);
   return r;
 }
 
+// The group's calls of one comm that take the SIMPLE ring or the direct path
+// (`idx`, in call order): placed on VCCL's plan for them (group_plan) — the
+// direct path folds every element in the order of its place in that plan,
+// as the ring does — and launched in plan order, consecutive calls of one
+// path with the same collective, type and op fused (<= max_parts).
+static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<int>& idx,
+                                   const std::vector<int>& algo) {
+  ncclComm* comm = tasks[idx[0]].comm;
+  std::vector<GroupTask> g;
+  for (int j : idx) {
+    const Task& t = tasks[j];
+    const bool ag = t.coll == kAllGather;
+    const int tsz = type_size(t.datatype);
+    const int op = ag ? OP_SUM : t.devOp;  // AG: int8 copies (enqueue.cc:2400-2404)
+    const int dt = ag ? (int)ncclInt8 : (int)t.datatype;
+    const int kt = ag ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
+    g.push_back(GroupTask{t.coll, ag ? (int64_t)t.count * tsz : (int64_t)t.count, ag ? 1 : tsz,
+                          (t.coll * 16 + op) * 32 + dt, (t.coll * 16 + op) * 32 + kt});
+  }
+  GroupPlanOut plan;
+  group_plan(g, comm->nRanks, comm->nChannels, comm->stepBytes, comm->nThreads, &plan);
+  for (size_t k = 0; k < idx.size(); k++) {
+    if (plan.planOf[k] < 0) return ncclInternalError;
+    tasks[idx[k]].planned = true;
+    tasks[idx[k]].plan = plan.cbd[k];
+  }
+  std::vector<std::vector<Task>> runs;
+  std::vector<int> runAlgo, runPlan;
+  for (int k : plan.order) {
+    const Task& t = tasks[idx[k]];
+    const int a = algo[idx[k]];
+    if (!runs.empty() && runPlan.back() == plan.planOf[k] && runAlgo.back() == a &&
+        runs.back().size() < (size_t)max_parts(a) && fusable(runs.back()[0], t, a)) {
+      runs.back().push_back(t);
+      continue;
+    }
+    runs.push_back({t});
+    runAlgo.push_back(a);
+    runPlan.push_back(plan.planOf[k]);
+  }
+  return launch_runs(runs, runAlgo);
+}
+
 static ncclResult_t launch_group(std::vector<Task>& tasks) {
   ncclResult_t ret = ncclSuccess;
-  std::vector<char> done(tasks.size(), 0);
+  const size_t n = tasks.size();
+  std::vector<char> done(n, 0);
   const bool fuse = param_int("GROUP_FUSE", 1) != 0;
-  for (size_t i = 0; i < tasks.size(); i++) {
+  // VCCL_GROUP_PLAN=0: every call keeps the partition of a call planned alone
+  const bool plan = fuse && param_int("GROUP_PLAN", 1) != 0;
+  std::vector<int> algo(n, -1);
+  if (fuse)
+    for (size_t i = 0; i < n; i++) algo[i] = fuse_key_algo(tasks[i]);
+  auto planned_path = [&](size_t i) { return plan && (algo[i] == kAlgoRing || algo[i] == kAlgoDirect); };
+  for (size_t i = 0; i < n; i++) {
     if (done[i]) continue;
     ncclResult_t r;
-    const int algo = fuse ? fuse_key_algo(tasks[i]) : -1;
-    if (algo >= 0 && (algo != kAlgoLL || tasks[i].coll == kAllReduce)) {
+    if (planned_path(i)) {
+      // every ring / direct call of this comm in the group, one VCCL plan
+      std::vector<int> idx;
+      for (size_t j = i; j < n; j++)
+        if (!done[j] && tasks[j].comm == tasks[i].comm && planned_path(j)) idx.push_back((int)j);
+      for (int j : idx) done[j] = 1;
+      r = launch_planned(tasks, idx, algo);
+    } else if (algo[i] >= 0 && (algo[i] != kAlgoLL || tasks[i].coll == kAllReduce)) {
       std::vector<Task> batch{tasks[i]};
       int64_t lines = ll_lines_of(tasks[i]);
-      for (size_t j = i + 1; j < tasks.size() && batch.size() < (size_t)max_parts(algo); j++) {
+      for (size_t j = i + 1; j < n && batch.size() < (size_t)max_parts(algo[i]); j++) {
         if (done[j] || tasks[j].comm != tasks[i].comm) continue;
-        if (!fusable(tasks[i], tasks[j], algo)) break;
-        if (algo == kAlgoLL) {
+        if (!fusable(tasks[i], tasks[j], algo[i])) break;
+        if (algo[i] == kAlgoLL) {
           if (lines + ll_lines_of(tasks[j]) > tasks[i].comm->llLines) break;
           lines += ll_lines_of(tasks[j]);
         }
         batch.push_back(tasks[j]);
         done[j] = 1;
       }
-      r = batch.size() == 1 ? launch_task(tasks[i]) : launch_fused(batch, algo);
+      r = batch.size() == 1 ? launch_task(tasks[i]) : launch_runs({batch}, {algo[i]});
     } else {
       r = launch_task(tasks[i]);
     }
@@ -1076,6 +1371,39 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingChunkOf(
   out[0] = ar_chunk_of(cbd, p.chunkLo, nRanks, std::max<int64_t>(1, 16 / esz), (int64_t)i, &k, &end);
   out[1] = k;
   out[2] = end;
+  return ncclSuccess;
+}
+
+extern "C" __attribute__((visibility("default"))) ncclResult_t vcclGroupPlan(
+    int nCalls, const int* colls, const size_t* counts, const int* datatypes, const int* ops, int nRanks,
+    int nChannels, size_t stepBytes, int nThreads, int* order, int* planOf, int64_t* cbd) {
+  if (nCalls < 1 || !colls || !counts || !datatypes || !ops || !order || !planOf || !cbd || nRanks < 1 ||
+      nChannels < 1 || nChannels > kMaxChannels || stepBytes < 4096 || nThreads < 64)
+    return ncclInvalidArgument;
+  std::vector<GroupTask> g;
+  for (int i = 0; i < nCalls; i++) {
+    const ncclDataType_t dt = (ncclDataType_t)datatypes[i];
+    const int tsz = type_size(dt);
+    if (colls[i] < 0 || colls[i] > 2 || tsz < 1 || counts[i] == 0) return ncclInvalidArgument;
+    const int c = colls[i] == 0 ? kAllReduce : colls[i] == 1 ? kReduceScatter : kAllGather;
+    const bool ag = c == kAllGather;
+    int devOp = OP_SUM;
+    uint64_t arg = 0;
+    if (!ag) NCCLCHECK(host_to_dev_redop((ncclRedOp_t)ops[i], dt, nRanks, &devOp, &arg));
+    const int kt = ag ? K_U8 : kernel_type_of(devOp, (int)dt);
+    if (kt < 0) return ncclInvalidArgument;
+    g.push_back(GroupTask{c, ag ? (int64_t)counts[i] * tsz : (int64_t)counts[i], ag ? 1 : tsz,
+                          (c * 16 + devOp) * 32 + (ag ? (int)ncclInt8 : (int)dt), (c * 16 + devOp) * 32 + kt});
+  }
+  GroupPlanOut p;
+  group_plan(g, nRanks, nChannels, (int64_t)stepBytes, nThreads, &p);
+  for (int i = 0; i < nCalls; i++) {
+    order[i] = p.order[i];
+    planOf[i] = p.planOf[i];
+    const CbdPlan& q = p.cbd[i];
+    const int64_t v[8] = {q.channelLo, q.channelHi, q.countLo, q.countMid, q.countHi, q.chunkLo, q.chunkMid, q.chunkHi};
+    memcpy(cbd + 8 * (size_t)i, v, sizeof(v));
+  }
   return ncclSuccess;
 }
 

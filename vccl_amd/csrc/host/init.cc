@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstring>
+#include <string>
 #include <thread>
 
 #include "../../../include/vccl_ext.h"
@@ -80,6 +81,81 @@ std::vector<std::vector<int>> ring_orders(int n) {
   std::vector<int> id(n);
   for (int i = 0; i < n; i++) id[i] = i;
   return {id};
+}
+
+// NCCL_ALGO / NCCL_PROTO (read once at init): the reference's parseList
+// (graph/tuning.cc:53-116) — a comma list of names, case-insensitive, a
+// leading '^' enables everything but the listed ones; per-collective
+// "func:list" entries after a ';' are not supported here (WARNed and
+// ignored).  Unknown names fail init with ncclInvalidUsage, as the
+// reference's tuner does.  Paths: LL (protocol LL / algorithm Tree), LL128
+// ring, SIMPLE ring, and the direct path (algorithm "Direct", an extension;
+// allowed only while NCCL_ALGO is unset or lists it).  A path is forced when
+// it is the only one the lists leave; otherwise the excluded ones are
+// dropped from the automatic choice.
+enum { kAllowLL = 1, kAllowLL128 = 2, kAllowSimple = 4, kAllowDirect = 8 };
+static ncclResult_t parse_name_list(const char* env, const char* str, const char* const* names, int nNames,
+                                    unsigned* mask) {
+  *mask = (1u << nNames) - 1;
+  if (!str || !*str) return ncclSuccess;
+  std::string s(str);
+  const size_t semi = s.find(';');
+  if (semi != std::string::npos) {
+    VWARN("%s=%s: per-collective entries are not supported, using \"%s\"", env, str, s.substr(0, semi).c_str());
+    s = s.substr(0, semi);
+  }
+  if (s.find(':') != std::string::npos) {
+    VWARN("%s=%s: per-collective entries are not supported, ignored", env, str);
+    return ncclSuccess;
+  }
+  bool exclude = false;
+  if (!s.empty() && s[0] == '^') {
+    exclude = true;
+    s = s.substr(1);
+  }
+  unsigned listed = 0;
+  size_t pos = 0;
+  while (pos <= s.size()) {
+    size_t comma = s.find(',', pos);
+    if (comma == std::string::npos) comma = s.size();
+    const std::string tok = s.substr(pos, comma - pos);
+    pos = comma + 1;
+    if (tok.empty()) continue;
+    int k = 0;
+    while (k < nNames && strcasecmp(tok.c_str(), names[k]) != 0) k++;
+    if (k == nNames) {
+      VWARN("Unrecognized element token \"%s\" when parsing %s=\"%s\"", tok.c_str(), env, str);
+      return ncclInvalidUsage;
+    }
+    listed |= 1u << k;
+  }
+  *mask = exclude ? ((1u << nNames) - 1) & ~listed : listed;
+  return ncclSuccess;
+}
+ncclResult_t algo_proto_select(const char* algo, const char* proto, int* force, int* allowed) {
+  static const char* const kProtos[] = {"LL", "LL128", "Simple"};
+  static const char* const kAlgos[] = {"Tree", "Ring", "CollnetDirect", "CollnetChain", "NVLS", "NVLSTree",
+                                       "PAT", "Direct"};
+  unsigned p = 0, a = 0;
+  NCCLCHECK(parse_name_list("NCCL_PROTO", proto, kProtos, 3, &p));
+  NCCLCHECK(parse_name_list("NCCL_ALGO", algo, kAlgos, 8, &a));
+  const bool tree = a & 1, ring = a & 2, direct = a & 0x80;
+  // the one-hop LL path restates VCCL's chain-tree LL fold: algorithm Tree;
+  // the direct path moves SIMPLE-style bulk copies
+  int m = 0;
+  if ((p & 1) && tree) m |= kAllowLL;
+  if ((p & 2) && ring) m |= kAllowLL128;
+  if ((p & 4) && ring) m |= kAllowSimple;
+  if ((p & 4) && direct) m |= kAllowDirect;
+  if (m == 0) {
+    VWARN("NCCL_ALGO=%s / NCCL_PROTO=%s leave no algorithm and protocol", algo ? algo : "",
+          proto ? proto : "");
+    return ncclInvalidUsage;
+  }
+  const int f = m == kAllowDirect ? 3 : m == kAllowLL128 ? 4 : m == kAllowSimple ? 1 : m == kAllowLL ? 2 : 0;
+  *force = f;
+  *allowed = m;
+  return ncclSuccess;
 }
 
 static uint64_t host_hash() {
@@ -177,24 +253,23 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   const int n = c->nRanks;
   const auto rings = ring_orders(n);
   const int nRings = (int)rings.size();
-  // Channel count: NCCL_NCHANNELS total, else VCCL_CHANNELS_PER_RING x rings.
-  // Defaults from tools/sweep_ring.py (profiles/r01_sweep_ring*.log): a
-  // channel is one workgroup whose throughput is bounded by the per-slot
-  // credit round trip and its CU's memory rate (tools/step_probe.py; the
-  // slot timeline, tools/ring_trace.py, shows < 2 us of protocol per 512 KiB
-  // slot: the copy is the bound), so bandwidth scales with channels: 16 per
-  // ring from 4 ranks (112 workgroups for the 8-GPU ring set, 96 for the
-  // 4-GPU one): a channel then carries 7 x 76.8 / 112 = 4.8 GB/s per
-  // direction at the xGMI spec, about a tenth of the slowest ring shape's
-  // per-channel rate on one GPU, as headroom for remote-store latency that
-  // no single-GPU run can show (RCCL's MI300X guidance uses 112 channels
-  // too); 96 for 2 GPUs (profiles/r02g/sweep_ring_1g.log: 16 / 32 / 48
-  // channels -> 199 / 299 / 436 GB/s busbw at 1 GiB; profiles/r03m, r03q:
-  // 48 / 64 / 96 / 128 channels -> 512 MiB AR 1289 / 1039 / 868 / 845 us,
-  // 2 ranks on one GPU; 96 leaves a quarter of the CUs to the peer ranks'
-  // other work when two ranks share a GPU).
-  // (3 ranks: 2 rings x 48 = the 96 workgroups of the 2-rank default)
-  int perRing = (int)param_int("CHANNELS_PER_RING", n >= 4 ? 16 : n == 3 ? 48 : 96);
+  // Channel count: NCCL_NCHANNELS total, else VCCL_CHANNELS_PER_RING x rings,
+  // by default from a link-bound model, within VCCL's
+  // MAXCHANNELS of 64 (device.h:62) so that VCCL can run the same geometry:
+  //   channels per ring = ceil(H * L / (k * R)), at most 64 / rings in all,
+  // L = 76.8 GB/s per xGMI link and direction (MI355X spec), k = rings
+  // sharing an arc (2 for the 4-GPU set of all 6 Hamiltonian cycles, else 1),
+  // R = 40 GB/s, the per-channel rate of the ring step shapes that read the
+  // own input from HBM (tools/step_probe, profiles/r03l: 36-44 GB/s at 96
+  // concurrent channels), H = 8 headroom for remote-store latency that no
+  // single-GPU run can measure (a channel then carries <= 1/8 of its local
+  // rate at link peak).  2 GPUs: 16; 3: 2 x 16; 4: 6 x 8 = 48; 5, 6: 4 x 16
+  // = 64; 7: 6 x 10 = 60; 8: 7 x 9 = 63.  The shared-GPU rehearsals, which
+  // are bound by CUs rather than links, set their counts with the knobs.
+  const int arcShare = n == 4 ? 2 : 1;
+  const int perRingModel = (int)((8 * 768 + 10 * 40 * arcShare - 1) / (10 * 40 * arcShare));  // ceil(8*76.8/(40k))
+  int perRing = (int)param_int("CHANNELS_PER_RING",
+                               std::max(1, std::min(perRingModel, kVcclMaxChannels / nRings)));
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
   // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490)
   nch = std::max(c->minCTAs, std::min(nch, c->maxCTAs));
@@ -223,15 +298,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
           "in %d slots, using the step", c->stepBytes, kSteps / 2);
     c->slotBytes = c->stepBytes;
   }
-  {
-    const char* algo = getenv("NCCL_ALGO");
-    const char* proto = getenv("NCCL_PROTO");
-    auto has = [](const char* s, const char* w) { return s && strcasestr(s, w) != nullptr; };
-    if (has(proto, "LL") || has(algo, "tree")) c->algoForce = 2;
-    if (has(algo, "direct")) c->algoForce = 3;
-    if (has(proto, "LL128")) c->algoForce = 4;  // the LL128 ring (ring.hpp prim_ll128)
-    if (has(proto, "simple") || (has(algo, "ring") && !has(algo, "tree"))) c->algoForce = 1;
-  }
+  NCCLCHECK(algo_proto_select(getenv("NCCL_ALGO"), getenv("NCCL_PROTO"), &c->algoForce, &c->algoAllowed));
   // Threads per ring channel (NCCL_NTHREADS, tuning.cc:198-200): 256 or 512
   // (the ring kernel's launch bound, ring_launch.hpp kRingMaxThreads).
   c->nThreads = (int)param_int("NTHREADS", kRingMaxThreads);
@@ -352,7 +419,11 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     // chunk; the slot holds that many data bytes in 64-byte lines of 56.
     // (VCCL_LL128_ALLOC=1: the buffers only — vcclCommSetAlgo may pick the
     // LL128 ring per call, the automatic choice is unchanged)
-    const bool want = c->algoForce == 4 || param_int("LL128", 0) != 0 || param_int("LL128_ALLOC", 0) != 0;
+    // NCCL_PROTO without SIMPLE but with LL128 (e.g. "LL,LL128"): the LL128
+    // ring carries every call LL does not
+    const bool ll128Only = (c->algoAllowed & kAllowLL128) && !(c->algoAllowed & kAllowSimple);
+    const bool want = c->algoForce == 4 || ll128Only || param_int("LL128", 0) != 0 ||
+                      param_int("LL128_ALLOC", 0) != 0;
     if (want) {
       c->ll128StepBytes = std::max<int64_t>(param_int("LL128_BUFFSIZE", 120 * 640 * kSteps * 8) / kSteps, 1920 * 16);
       c->ll128Threads = (int)std::max<int64_t>(param_int("LL128_NTHREADS", 640), 64);
@@ -363,12 +434,18 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       HIPCHECK(hipMemset(c->ll128Buf, 0, bytes));
       HIPCHECK(hipIpcGetMemHandle(&me.ll128Handle, c->ll128Buf));
       me.ll128Ptr = c->ll128Buf;
-      if (param_int("LL128", 0) != 0) {
+      if (ll128Only) {
+        c->ll128MinBytes = 0;
+        c->ll128MaxBytes = ~(size_t)0;
+      } else if (param_int("LL128", 0) != 0 && (c->algoAllowed & kAllowLL128)) {
         c->ll128MinBytes = (size_t)param_int("LL128_MIN", 64 << 10);
         c->ll128MaxBytes = (size_t)param_int("LL128_MAX", 8 << 20);
       }
     }
   }
+  // paths NCCL_ALGO / NCCL_PROTO exclude drop out of the automatic choice
+  if (!(c->algoAllowed & kAllowLL)) c->llMaxBytes = c->llRsAgMaxBytes = 0;
+  if (!(c->algoAllowed & kAllowDirect)) c->directMaxBytes = c->directRsAgMaxBytes = 0;
   if (n > 1) NCCLCHECK(net_listen(c, &me));
   VINFO("rank %d: exchange peer info", c->rank);
   c->peers.assign(n, PeerMap{});
@@ -394,6 +471,11 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     c->directMaxBytes = c->directRsAgMaxBytes = 0;
     c->ll128MinBytes = c->ll128MaxBytes = 0;
     if (c->algoForce == 4) c->algoForce = 1;  // LL128 lines need the xGMI mesh: SIMPLE
+    // ... so no LL128 FIFO is mapped: drop the local one too, so that neither
+    // the automatic choice nor vcclCommSetAlgo(LL128) can pick a ring whose
+    // channels carry no LL128 slots
+    if (c->ll128Buf) (void)hipFree(c->ll128Buf);
+    c->ll128Buf = nullptr;
     c->nChannels = std::max(1, std::min(c->nChannels, (int)param_int("NET_NCHANNELS", 8)));
     VINFO("rank %d: inter-node ring through the net proxy, %d channels", c->rank, c->nChannels);
   }
@@ -704,6 +786,11 @@ VCCL_EXPORT ncclResult_t vcclRingOrders(int nRanks, int maxRings, int* orders, i
   for (size_t k = 0; k < rings.size(); k++)
     for (int i = 0; i < nRanks; i++) orders[k * nRanks + i] = rings[k][i];
   return ncclSuccess;
+}
+
+VCCL_EXPORT ncclResult_t vcclAlgoSelection(const char* algo, const char* proto, int* force, int* allowed) {
+  if (!force || !allowed) return ncclInvalidArgument;
+  return algo_proto_select(algo, proto, force, allowed);
 }
 
 VCCL_EXPORT ncclResult_t ncclGetVersion(int* version) {

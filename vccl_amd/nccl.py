@@ -41,7 +41,7 @@ EXPORTED = [
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
     "vcclCommRingTrace",
-    "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders",
+    "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders", "vcclGroupPlan", "vcclAlgoSelection",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
 ]
@@ -111,6 +111,11 @@ def lib() -> ctypes.CDLL:
         "vcclRingChunkOf": [c_size, c_int, c_int, c_int, c_size, c_int, c_size,
                             ctypes.POINTER(ctypes.c_int64)],
         "vcclRingOrders": [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
+        "vcclGroupPlan": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_size), ctypes.POINTER(c_int),
+                          ctypes.POINTER(c_int), c_int, c_int, c_size, c_int, ctypes.POINTER(c_int),
+                          ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_int64)],
+        "vcclAlgoSelection": [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_int),
+                              ctypes.POINTER(c_int)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -205,6 +210,32 @@ def ring_chunk_of(count: int, dtype: int, nranks: int, nchannels: int, slot_byte
     check(lib().vcclRingChunkOf(count, dtype, nranks, nchannels, slot_bytes, nthreads, i, out),
           "vcclRingChunkOf")
     return tuple(out)
+
+
+def group_plan(calls, nranks: int, nchannels: int, slot_bytes: int = 512 << 10,
+               nthreads: int = 512):
+    """vcclGroupPlan: VCCL's multi-task plan of a group of ring / direct calls.
+    calls = [(coll, count, dtype, op)]; returns (order, plan_of, parts) with
+    parts[i] = (channelLo, channelHi, countLo, countMid, countHi, chunkLo,
+    chunkMid, chunkHi) as ring_partition gives it."""
+    n = len(calls)
+    ci = ctypes.c_int * n
+    colls, dts, ops = ci(*[c[0] for c in calls]), ci(*[c[2] for c in calls]), ci(*[c[3] for c in calls])
+    counts = (ctypes.c_size_t * n)(*[c[1] for c in calls])
+    order, plan_of = ci(), ci()
+    cbd = (ctypes.c_int64 * (8 * n))()
+    check(lib().vcclGroupPlan(n, colls, counts, dts, ops, nranks, nchannels, slot_bytes, nthreads, order,
+                              plan_of, cbd), "vcclGroupPlan")
+    return list(order), list(plan_of), [tuple(cbd[8 * i:8 * i + 8]) for i in range(n)]
+
+
+def algo_selection(algo: str | None, proto: str | None) -> tuple[int, int]:
+    """vcclAlgoSelection: (force, allowed mask) for NCCL_ALGO / NCCL_PROTO strings."""
+    f, a = ctypes.c_int(), ctypes.c_int()
+    check(lib().vcclAlgoSelection(algo.encode() if algo is not None else None,
+                                  proto.encode() if proto is not None else None, ctypes.byref(f),
+                                  ctypes.byref(a)), "vcclAlgoSelection")
+    return f.value, a.value
 
 
 def reduce_copy(dev_op: int, dtype: int, red_arg: int, srcs, dsts, n_elts: int, stream: int = 0,
