@@ -163,20 +163,22 @@ struct RingCtx {
 
 // ---------------------------------------------------------------- LL128
 // LL128 protocol (prims_ll128.h:176-324, recvReduceSendCopy / GenericOp),
-// gfx950 wire format.  A step's data travels as 64-byte lines: lanes 4i..4i+2
-// carry 16-byte data pieces, lane 4i+3 an 8-byte data piece and the 8-byte
-// flag (step + 1, as recvFlag / sendFlag).  One wave instruction moves 16
-// lines = 1 KiB ("a round") carrying 896 data bytes: lane l's piece is bytes
-// [16 (3 (l/4) + l%4), +16) of the round, or for a flag lane the half
-// [16 (48 + l/8) + 8 ((l/4) & 1), +8).  The receiver polls its round's lines
+// gfx950 wire format (ring_types.hpp kLL128*).  A step's data travels as
+// lines of S = kLL128LaneSpan lanes x 16 bytes: lane S i + j (j < S - 1)
+// carries a 16-byte data piece, lane S i + S - 1 an 8-byte data piece and the
+// 8-byte flag (step + 1, as recvFlag / sendFlag).  One wave instruction moves
+// 1 KiB ("a round") of 64 / S lines: lane l's piece is bytes
+// [16 ((S - 1) (l / S) + l % S), +16) of the round's data, or for a flag lane
+// [16 (S - 1) 64 / S + 8 (l / S), +8).  The receiver polls its round's lines
 // (one 16-byte sc0 sc1 load per lane) until every flag lane shows the step,
-// and uses the data of that same load: a line is one 64-byte write request
-// of the sender's wave store (sc0 sc1 write-through), the granule the flag
-// covers.  The reference puts one 8-byte flag in each 128-byte NVLink line
-// (15/16 efficiency, atomic on NVLink); here a flag per 64-byte request
-// (7/8).  No tail flag and no drain per step: the sender waits for the
-// credit (head) like SIMPLE, the receiver posts the head after the step.
-// Steps and credits are the channel's SIMPLE ones (ring_types.hpp).
+// and uses the data of that same load: the sender's wave store (sc0 sc1
+// write-through) must deliver a line whole — with 64-byte lines the flag
+// covers one 64-byte write request (the granule the PMC passes show); the
+// 128-byte line (VCCL's 15/16 NVLink line, -DVCCL_LL128_LINE=128) spans two
+// requests and relies on them landing together (0 tears in the intra-GPU
+// probe, tests/test_gpu_ll128.py).  No tail flag and no drain per step: the
+// sender waits for the credit (head) like SIMPLE, the receiver posts the
+// head after the step.  Steps and credits are the channel's SIMPLE ones.
 template <class T>
 __device__ __forceinline__ void ll128_put(uint64_t& lo, uint64_t& hi, int q, T x) {
   uint64_t v;
@@ -263,9 +265,10 @@ __device__ void ll128_prim(RingCtx& R, const Fn& fn, const void* srcv, void* dst
   const char* rslot = RECV ? R.ch->ll128Recv + (int64_t)(R.recvStep % kSteps) * R.ll128Slot : nullptr;
   char* sslot = SEND ? R.ch->ll128Send + (int64_t)(R.sendStep % kSteps) * R.ll128Slot : nullptr;
   const int lane = R.tid & 63, wave = R.tid >> 6, nw = R.nthreads >> 6;
-  const int line = lane >> 2;
-  const bool flagLane = (lane & 3) == 3;
-  const int dOff = flagLane ? (48 + (line >> 1)) * 16 + (line & 1) * 8 : (line * 3 + (lane & 3)) * 16;
+  constexpr int S = kLL128LaneSpan;
+  const int line = lane / S, sub = lane % S;
+  const bool flagLane = sub == S - 1;
+  const int dOff = flagLane ? 16 * (S - 1) * kLL128LinesPerRound + 8 * line : (line * (S - 1) + sub) * 16;
   const int dLen = flagLane ? 8 : 16;
   const bool srcAl = SRC && (((uintptr_t)src & 15) == 0);
   const bool dstAl = DST && (((uintptr_t)dst & 15) == 0);

@@ -78,11 +78,14 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
   r.trace = w.comm->trace ? (RingTraceRec*)w.comm->trace + (int64_t)blockIdx.x * w.comm->traceCap : nullptr;
   r.traceN = 0;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
+  const uint64_t recv0 = r.recvStep, send0 = r.sendStep;
   ring_run<COLL, Fn, UNROLL, PROTO>(r, fn, w);
   for (int i = 1; i < b.nParts; i++)
     ring_run<COLL, Fn, UNROLL, PROTO>(r, fn, ring_work_with(w, b.more[i - 1]));
   __syncthreads();
-  if (threadIdx.x == 0) {
+  // a channel none of the parts touched (below every part's channelLo) keeps
+  // its counters untouched
+  if (threadIdx.x == 0 && (r.recvStep != recv0 || r.sendStep != send0)) {
     ch->recvStep = r.recvStep;
     ch->sendStep = r.sendStep;
   }

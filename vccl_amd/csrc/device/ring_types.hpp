@@ -197,12 +197,24 @@ struct RingWork {
 
 // Protocols of the ring kernels (nccl_common.h ids).
 enum : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2 };
-// LL128 wire format on gfx950 (ring.hpp prim_ll128): 64-byte lines of three
-// 16-byte data pieces + one {8-byte data, 8-byte flag} piece, one line per 4
-// lanes, 16 lines (1 KiB) per wave instruction carrying 896 data bytes.
-constexpr int kLL128LineBytes = 64;
+// LL128 wire format on gfx950 (ring.hpp ll128_prim): lines of L bytes, one
+// per L/16 lanes — every lane but the line's last carries a 16-byte data
+// piece, the last an 8-byte data piece and the 8-byte flag — so one wave
+// instruction moves 1 KiB ("a round") of 1024/L lines.
+//   L = 64 (default): 16 lines, 896 data bytes per round (7/8), one flag per
+//       64-byte write request (the granule the PMC passes show);
+//   L = 128 (-DVCCL_LL128_LINE=128): 8 lines, 960 data bytes (15/16, VCCL's
+//       NVLink line, device.h:82-83); VCCL's 576,000-byte LL128 chunk is then
+//       exactly 600 rounds = its 614,400-byte step.
+#ifndef VCCL_LL128_LINE
+#define VCCL_LL128_LINE 64
+#endif
+static_assert(VCCL_LL128_LINE == 64 || VCCL_LL128_LINE == 128, "LL128 line: 64 or 128 bytes");
+constexpr int kLL128LineBytes = VCCL_LL128_LINE;
+constexpr int kLL128LaneSpan = kLL128LineBytes / 16;    // lanes per line
+constexpr int kLL128LinesPerRound = 64 / kLL128LaneSpan;
 constexpr int kLL128RoundWire = 1024;
-constexpr int kLL128RoundData = 896;
+constexpr int kLL128RoundData = kLL128RoundWire - 8 * kLL128LinesPerRound;
 
 // Group aggregation (the reference's planner packing a group's collectives
 // into one plan, enqueue.cc:352-508 / :518-769, run by one kernel over its

@@ -998,10 +998,14 @@ static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, cons
       r = ncclUnhandledCudaError;
   }
   for (size_t k = 0; k < runs.size() && r == ncclSuccess; k++) {
-    const int n = (int)runs[k].size(), algo = algos[k];
-    r = algo == kAlgoLL ? launch_ll(runs[k].data(), n)
-        : algo == kAlgoDirect ? launch_direct(runs[k].data(), n)
-                              : launch_ring(runs[k].data(), n, algo == kAlgoRingLL128);
+    // every launch goes onto s0 (the launchers use their first task's
+    // stream): runs of one comm must never overlap on its channels
+    std::vector<Task> run = runs[k];
+    for (Task& t : run) t.stream = s0;
+    const int n = (int)run.size(), algo = algos[k];
+    r = algo == kAlgoLL ? launch_ll(run.data(), n)
+        : algo == kAlgoDirect ? launch_direct(run.data(), n)
+                              : launch_ring(run.data(), n, algo == kAlgoRingLL128);
     if (n > 1) comm->fusedLaunches++;
   }
   if (r == ncclSuccess) r = stream_mark(comm, s0, cs);
@@ -1042,10 +1046,11 @@ static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<i
   }
   std::vector<std::vector<Task>> runs;
   std::vector<int> runAlgo, runPlan;
+  static const bool fusePlanned = param_int("GROUP_PLAN_FUSE", 1) != 0;
   for (int k : plan.order) {
     const Task& t = tasks[idx[k]];
     const int a = algo[idx[k]];
-    if (!runs.empty() && runPlan.back() == plan.planOf[k] && runAlgo.back() == a &&
+    if (fusePlanned && !runs.empty() && runPlan.back() == plan.planOf[k] && runAlgo.back() == a &&
         runs.back().size() < (size_t)max_parts(a) && fusable(runs.back()[0], t, a)) {
       runs.back().push_back(t);
       continue;
@@ -1290,8 +1295,11 @@ VCCL_EXPORT ncclResult_t vcclHostToDevRedOp(ncclRedOp_t op, ncclDataType_t datat
 }
 
 VCCL_EXPORT const char* vcclBuildInfo(void) {
-  return "vccl-mi355x " __DATE__ " gfx950; one-shot LL / two-shot direct / SIMPLE ring over "
-         "xGMI (uncached receiver buffers); reduce-copy 16B packs; group-fused LL";
+#define VCCL_STR2(x) #x
+#define VCCL_STR(x) VCCL_STR2(x)
+  return "vccl-mi355x " __DATE__ " gfx950; one-shot LL / two-shot direct / SIMPLE ring / LL128 ring "
+         "(" VCCL_STR(VCCL_LL128_LINE) "-byte lines) over xGMI (uncached receiver buffers); "
+         "reduce-copy 16B packs; VCCL group plans";
 }
 
 extern "C" {
