@@ -942,6 +942,11 @@ def _ar_graph_row(dist, comm, rank, world, S, dtype="f16", calls=50, replays=10)
             graph.capture_end()
     torch.cuda.synchronize()
     dt = _time_coll(dist, graph.replay, replays, 2)
+    # each replay alone (barrier, replay, synchronize; max over ranks): shows
+    # whether the average hides a single slow replay
+    per = []
+    for _ in range(replays):
+        per.append(_time_coll(dist, graph.replay, 1, 0) / calls * 1e6)
     sp = torch.cuda.current_stream().cuda_stream
     comm.all_reduce(x.data_ptr(), ref.data_ptr(), n, code, nccl.ncclSum, sp)
     torch.cuda.synchronize()
@@ -951,6 +956,7 @@ def _ar_graph_row(dist, comm, rank, world, S, dtype="f16", calls=50, replays=10)
     us = dt / (replays * calls) * 1e6
     return {"bytes": n * esz, "us": round(us, 2), "calls_per_graph": calls,
             "busbw": round(n * esz / us / 1e3 * 2 * (world - 1) / world, 3),
+            "us_per_call_each_replay": [round(v, 2) for v in per],
             "algo": comm.coll_algo(0, n, code), "matches_eager": ok}
 
 

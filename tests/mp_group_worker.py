@@ -23,6 +23,13 @@ from vccl_amd import nccl  # noqa: E402
 
 GROUP_RS = [(f"rs{i}", 9, (8 << 20) // 2) for i in range(16)]        # (name, dtype, bucket elements)
 GROUP_AR = [(f"ar{i}", 7, (2 << 20) // 4 + 37 * i) for i in range(8)]
+# ADVICE r3 (direct batches of very different sizes): all-reduces of 1.1 MiB
+# and 4 MiB, reduce-scatters of 5 MiB and 48 MiB buckets (f32), interleaved —
+# on the direct path under the test geometry at 4 ranks, one fused launch per
+# collective whose parts differ ~4-10x in size (one block length for all)
+MIXED_RS = [("mrs0", 7, (48 << 20) // 4), ("mrs1", 7, (5 << 20) // 4), ("mrs2", 7, (48 << 20) // 4 + 4096)]
+MIXED_AR = [("mar0", 7, (1 << 20) // 4 + 70_000), ("mar1", 7, (4 << 20) // 4), ("mar2", 7, 300_001)]
+SETS = {"zero": (GROUP_RS, GROUP_AR, 1), "mixed": (MIXED_RS, MIXED_AR, 3)}
 
 
 def gen(name, dt, count, rank):
@@ -35,30 +42,51 @@ def main():
     rank, n = int(sys.argv[1]), int(sys.argv[2])
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
     outdir = sys.argv[4]
+    group_rs, group_ar, reps = SETS[sys.argv[5] if len(sys.argv) > 5 else "zero"]
     torch.cuda.set_device(0)
     comm = nccl.Comm.init_rank(n, uid, rank)
     s = torch.cuda.current_stream().cuda_stream
     bufs = {}
-    for name, dt, count in GROUP_RS + GROUP_AR:
+    for name, dt, count in group_rs + group_ar:
         x = gen(name, dt, count, rank)
         xb = torch.from_numpy(x.view(np.uint8).copy()).cuda()
-        nout = count // n if name.startswith("rs") else count
+        nout = count // n if (name, dt, count) in group_rs else count
         yb = torch.empty(nout * x.dtype.itemsize, dtype=torch.uint8, device="cuda")
         bufs[name] = (xb, yb, x.dtype)
-    algos = {"rs": comm.coll_algo(1, GROUP_RS[0][2] // n, 9), "ar": comm.coll_algo(0, GROUP_AR[0][2], 7)}
+    algos = {"rs": comm.coll_algo(1, group_rs[0][2] // n, group_rs[0][1]),
+             "ar": comm.coll_algo(0, group_ar[0][2], group_ar[0][1])}
     torch.cuda.synchronize()
-    f0 = comm.launch_stats()[1]
-    nccl.group_start()
-    for name, dt, count in GROUP_RS:
-        xb, yb, _ = bufs[name]
-        comm.reduce_scatter(xb.data_ptr(), yb.data_ptr(), count // n, dt, nccl.ncclSum, s)
-    for name, dt, count in GROUP_AR:
-        xb, yb, _ = bufs[name]
-        comm.all_reduce(xb.data_ptr(), yb.data_ptr(), count, dt, nccl.ncclSum, s)
-    nccl.group_end()
-    torch.cuda.synchronize()
-    fused = comm.launch_stats()[1] - f0
-    res = {name: yb.cpu().numpy().view(npdt) for name, (xb, yb, npdt) in bufs.items()}
+    res, fused = {}, 0
+    for rep in range(reps):
+        for name, (xb, yb, npdt) in bufs.items():
+            yb.fill_(0xFF)  # NaN / all-ones: stale output cannot pass
+        torch.cuda.synchronize()
+        f0 = comm.launch_stats()[1]
+        nccl.group_start()
+        # reduce-scatters and all-reduces interleaved in call order (the
+        # planner bins them per collective)
+        for i in range(max(len(group_rs), len(group_ar))):
+            if i < len(group_rs):
+                name, dt, count = group_rs[i]
+                xb, yb, _ = bufs[name]
+                comm.reduce_scatter(xb.data_ptr(), yb.data_ptr(), count // n, dt, nccl.ncclSum, s)
+            if i < len(group_ar) and reps > 1:
+                name, dt, count = group_ar[i]
+                xb, yb, _ = bufs[name]
+                comm.all_reduce(xb.data_ptr(), yb.data_ptr(), count, dt, nccl.ncclSum, s)
+        if reps == 1:
+            for name, dt, count in group_ar:
+                xb, yb, _ = bufs[name]
+                comm.all_reduce(xb.data_ptr(), yb.data_ptr(), count, dt, nccl.ncclSum, s)
+        nccl.group_end()
+        torch.cuda.synchronize()
+        fused = comm.launch_stats()[1] - f0
+        for name, (xb, yb, npdt) in bufs.items():
+            out = yb.cpu().numpy().view(npdt)
+            if rep == 0:
+                res[name] = out
+            elif not np.array_equal(out.view(np.uint8), res[name].view(np.uint8)):
+                res[name + "_differs"] = np.array(rep)
     res["fused"] = np.array(fused)
     res["algo_rs"] = np.array(algos["rs"])
     res["algo_ar"] = np.array(algos["ar"])

@@ -472,6 +472,57 @@ def test_group_zero_pattern(n, geom):
                                   what=f"{name} n={n} {geom} rank {r} vs VCCL grouped")
 
 
+def test_group_mixed_direct_sizes():
+    """a fused direct launch whose parts differ in size —
+    reduce-scatters of 5 MiB and 48 MiB buckets and all-reduces of 1.1 MiB
+    and 4 MiB, interleaved in one group, 4 ranks, direct path (test
+    geometry) — must not let one part's scatter overwrite inbox bytes a
+    peer's other workgroup still folds: every part of a batch uses one block
+    length.  The group runs 3 times (outputs NaN-filled before each) and
+    every run is bit-exact against VCCL's grouped plan."""
+    from tests import mp_group_worker as G
+    n = 4
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    env.update(TEST_GEOM)
+    nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_group_worker.py"),
+                                   str(r), str(n), hexid, d, "mixed"], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
+    assert (str(res[0]["algo_rs"]), str(res[0]["algo_ar"])) == ("direct", "direct")
+    assert int(res[0]["fused"]) == 2, int(res[0]["fused"])
+    for r in range(n):
+        assert not [k for k in res[r] if k.endswith("_differs")], (r, [k for k in res[r] if k.endswith("_differs")])
+    calls = []
+    for i in range(max(len(G.MIXED_RS), len(G.MIXED_AR))):
+        if i < len(G.MIXED_RS):
+            calls.append(("rs", 0, G.MIXED_RS[i][1], G.MIXED_RS[i][2] // n))
+        if i < len(G.MIXED_AR):
+            calls.append(("ar", 0, G.MIXED_AR[i][1], G.MIXED_AR[i][2]))
+    works = iter(_ring.group_works(calls, n, nch, slot))
+    for i in range(max(len(G.MIXED_RS), len(G.MIXED_AR))):
+        for lst, coll in ((G.MIXED_RS, "rs"), (G.MIXED_AR, "ar")):
+            if i >= len(lst):
+                continue
+            name, dt, count = lst[i]
+            ins = [G.gen(name, dt, count, r) for r in range(n)]
+            w = next(works)
+            if coll == "rs":
+                exp = _ring.expected_reducescatter(0, dt, ins, nch, slot, work=w)
+                for r in range(n):
+                    assert_bitexact(dt, res[r][name], exp[r], what=f"{name} rank {r}")
+            else:
+                exp = _ring.expected_allreduce(0, dt, ins, nch, slot, work=w)
+                for r in range(n):
+                    assert_bitexact(dt, res[r][name], exp, what=f"{name} rank {r}")
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_ring_trace_and_shared_cap(n):
     """The SIMPLE ring's slot timeline (VCCL_RING_TRACE, vcclCommRingTrace)
