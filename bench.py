@@ -918,7 +918,7 @@ def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
             "busbw": round(algbw * 2 * (world - 1) / world, 3), "algo": comm.coll_algo(0, n, code)}
 
 
-def _ar_graph_row(dist, comm, rank, world, S, dtype="f16", calls=50, replays=10):
+def _ar_graph_row(dist, comm, rank, world, S, dtype="f16", calls=50, replays=10, stream=None):
     """Config 5 in graph mode (nccl-tests ``-G``): ``calls`` all-reduces of S
     bytes captured into one HIP graph, replayed ``replays`` times; us per call
     = replay time / calls (no per-call launch cost).  The replayed output is
@@ -929,7 +929,7 @@ def _ar_graph_row(dist, comm, rank, world, S, dtype="f16", calls=50, replays=10)
     g = torch.Generator(device="cuda").manual_seed(3000 + rank)
     x = (torch.rand(n, device="cuda", generator=g) * 2 - 1).to(tdt)
     y, ref = torch.empty_like(x), torch.empty_like(x)
-    cs = torch.cuda.Stream()
+    cs = stream if stream is not None else torch.cuda.Stream()
     cs.wait_stream(torch.cuda.current_stream())
     graph = torch.cuda.CUDAGraph()
     torch.cuda.synchronize()
@@ -1049,7 +1049,13 @@ def bench_extras(dist, comm, rank, world, args):
     # with 8 ranks sharing one GPU (rehearsal) that oversubscribes the
     # scheduler's queues and every later row would run time-sliced.
     try:
-        ex["allreduce_f16_ll_graph"] = [_ar_graph_row(dist, comm, rank, world, S) for S in EXTRA_F16_SIZES]
+        # one capture stream for every row: with ranks sharing one GPU, the
+        # second stream a process creates served ~28 us per replayed call
+        # whatever the size, while every row on one shared stream ran at
+        # ~4.2 us (tools/ll_graph_probe.py, profiles/r04g)
+        cap = torch.cuda.Stream()
+        ex["allreduce_f16_ll_graph"] = [_ar_graph_row(dist, comm, rank, world, S, stream=cap)
+                                        for S in EXTRA_F16_SIZES]
     except Exception as e:  # noqa: BLE001
         ex["graph_error"] = repr(e)
     ex["async_error"] = comm.async_error()

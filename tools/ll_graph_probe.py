@@ -30,11 +30,16 @@ def main():
     comm = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank)
     sizes = [int(v) for v in os.environ.get(
         "PROBE_SIZES", "8,64,256,512,768,1024,1536,2048,4096,8192,16384").split(",")]
+    # PROBE_STREAM=fresh: a new capture stream per row (as the bench line);
+    # shared: one capture stream for every row
+    shared = torch.cuda.Stream() if os.environ.get("PROBE_STREAM", "fresh") == "shared" else None
     for dtype in os.environ.get("PROBE_DTYPES", "f16,f32").split(","):
-        for S in sizes:
-            row = bench._ar_graph_row(dist, comm, rank, world, S, dtype)
+        for i, S in enumerate(sizes):
+            row = bench._ar_graph_row(dist, comm, rank, world, S, dtype, stream=shared)
             if rank == 0:
                 row["dtype"] = dtype
+                row["row"] = i
+                row["stream"] = "shared" if shared is not None else "fresh"
                 print(json.dumps(row), flush=True)
     comm.destroy()
     dist.destroy_process_group()

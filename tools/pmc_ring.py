@@ -7,12 +7,12 @@ allocation, channel count) this launcher runs:
   * one plain timing run (both ranks unprofiled): us per call;
   * one rocprofv3 pass per counter group with rank 0 under
     `rocprofv3 --pmc` (kernel trace only, each pass under its own
-    `timeout -s KILL`) and rank 1 unprofiled.  The TCC counters are device
-    wide, so a rank-0 k_ring dispatch window counts BOTH ranks' traffic of
-    that all-reduce (the two ranks' kernels run concurrently, coupled step by
-    step through the FIFOs): the algorithmic bytes to compare with are
-    2 ranks x 4 S (per rank: reads S/2 + S + S/2, writes S/2 + S + S/2 over
-    the three step shapes S->F, S+F->F+O, F->O).
+    `timeout -s KILL`) and rank 1 unprofiled.  The counters of a rank-0
+    k_ring dispatch count rank 0's own traffic only (measured: the first
+    version of this tool assumed device-wide TCC counts of both ranks and
+    found exactly half of 2 x 4 S), so the algorithmic bytes to compare with
+    are 4 S (per rank: reads S/2 + S + S/2, writes S/2 + S + S/2 over the
+    three step shapes S->F, S+F->F+O, F->O; two ranks move 8 S per call).
 FETCH_SIZE is doubled per MI355X_MICROARCH.md §HBM (gfx950 tallies wide
 streaming reads at half); WRITE_SIZE is taken as is; both in KiB.
 Writes gpurun_out/pmc_ring.json.  This script never touches the GPU itself:
@@ -37,7 +37,14 @@ VARIANTS = {
     "alloc1_ch96": {"VCCL_FIFO_ALLOC": "1", "VCCL_NCHANNELS": "96"},
     "alloc2_ch96": {"VCCL_FIFO_ALLOC": "2", "VCCL_NCHANNELS": "96"},
     "alloc0_ch16": {"VCCL_FIFO_ALLOC": "0"},
+    # FIFO slot = 2 steps (VCCL's SliceSteps for the ring, collectives.h:17-22)
+    # or a whole 4-step chunk: fewer drains and hand-offs, same fold order
+    "slice1m_ch96": {"VCCL_NCHANNELS": "96", "VCCL_SLICE_BYTES": str(1 << 20)},
+    "slice2m_ch96": {"VCCL_NCHANNELS": "96", "VCCL_SLICE_BYTES": str(2 << 20)},
+    "slice1m_ch16": {"VCCL_SLICE_BYTES": str(1 << 20)},
 }
+# PMC_RING_TIMING_ONLY=1: the plain timing runs only (no counter passes)
+TIMING_ONLY = os.environ.get("PMC_RING_TIMING_ONLY", "0") == "1"
 PORT = [29600]
 
 
@@ -80,7 +87,8 @@ def parse(d):
 
 
 def main():
-    res = {"bytes_per_rank": NBYTES, "algorithmic_bytes_both_ranks": 2 * 4 * NBYTES, "variants": {}}
+    res = {"bytes_per_rank": NBYTES, "algorithmic_bytes_per_rank": 4 * NBYTES,
+           "algorithmic_bytes_both_ranks": 2 * 4 * NBYTES, "variants": {}}
     only = os.environ.get("PMC_RING_VARIANTS")
     for name, extra in VARIANTS.items():
         if only and name not in only.split(","):
@@ -96,7 +104,7 @@ def main():
         best = min(t["us"])
         v["hbm_TBps_algorithmic_at_best"] = round(2 * 4 * NBYTES / (best * 1e-6) / 1e12, 3)
         counters = {}
-        for ctrs in PASSES:
+        for ctrs in ([] if TIMING_ONLY else PASSES):
             d = os.path.join(OUT, name, "_".join(c.lower() for c in ctrs))
             r = run_pair(extra, ["--pmc", *ctrs, "--output-format", "csv", "-d", d, "-o", "run"],
                          tag=f"{name} {ctrs}")
@@ -111,13 +119,16 @@ def main():
             fetch = 2 * c["FETCH_SIZE"] * 1024
             write = c["WRITE_SIZE"] * 1024
             v["traffic_bytes"] = {"fetch_x2": fetch, "write": write, "total": fetch + write,
-                                  "ratio_to_algorithmic": round((fetch + write) / (2 * 4 * NBYTES), 4)}
+                                  "ratio_to_algorithmic_per_rank": round((fetch + write) / (4 * NBYTES), 4),
+                                  "read_ratio": round(fetch / (2 * NBYTES), 4),
+                                  "write_ratio": round(write / (2 * NBYTES), 4)}
         res["variants"][name] = v
         print(json.dumps({name: v}), flush=True)
         if "error" in v:
             break
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "pmc_ring.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(ROOT, "gpurun_out", os.environ.get("PMC_RING_OUT", "pmc_ring.json")), "w"),
+              indent=1)
 
 
 if __name__ == "__main__":

@@ -32,17 +32,21 @@
 // slots (ring.hpp).  Flags carry the call epoch (device-resident, see
 // epoch_next), so no buffer is ever cleared and graph replays stay in step.
 //
-// Buffer reuse without double buffering: rank r can rewrite region (0, r),
-// block b at p only in its NEXT chunk (or call), i.e. after its workgroup b
-// finished phase 3 of this one, which waited for p's flag (1, p, b), which p
-// raised only after reading every region (0, *) block b.  Region (1, o) is
-// rewritten by o only after o received the reader's phase-1 data of the next
-// chunk, which workgroup b of the reader sends only after its own phase 3.
-// The one-hop reduce-scatter / all-gather below write only (0, *) regions
-// and guard reuse with explicit acknowledgements; any of the three kernels
-// may follow any other on the same inbox (a peer one call ahead writes only
-// (0, *) regions, which the previous call has finished reading before that
-// peer could complete it).
+// Buffer reuse.  Every guarantee is per block: workgroup b of every rank
+// only ever touches the inbox bytes [b * blkElts, (b + 1) * blkElts) of a
+// region, so the per-block flags order all reuse of those bytes.  A fused
+// batch (DirectBatch) keeps that true across its parts by giving every part
+// ONE block length (host/enqueue.cc launch_direct).
+//  * the all-reduce double-buffers its chunks by parity (regions and flags,
+//    direct_allreduce_part): parity p is rewritten for chunk c+2 only after
+//    the readers' flags of chunk c were awaited;
+//  * the one-hop reduce-scatter / all-gather use parity 0 only and guard
+//    reuse with explicit acknowledgements (phase 3 below);
+// and a region of one parity is rewritten by its writer's next chunk, part
+// or call only after its reader's flag for the previous use, so any of the
+// three kernels may follow any other on the same inbox (a peer one call
+// ahead writes only (0, *) regions, which the previous call has finished
+// reading before that peer could complete it).
 #pragma once
 #include "coll_types.hpp"
 #include "ll.hpp"

@@ -412,11 +412,12 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   }
   if (n > 1) {
     // LL128 ring buffers: with NCCL_PROTO=LL128, or VCCL_LL128=1 (the
-    // automatic window VCCL_LL128_MIN..MAX, default 64 KiB - 8 MiB: the range
-    // VCCL's tuner gives LL128, enqueue.cc:2032).  VCCL's LL128 step
+    // automatic window VCCL_LL128_MIN..MAX, default 64 KiB - 1 MiB, inside
+    // the range VCCL's tuner gives LL128, enqueue.cc:2032).  VCCL's LL128 step
     // (NCCL_LL128_BUFFSIZE / 8, default 120 x 640 x 8 x 8 B / 8 = 614,400 B)
     // carries 15/16 of it as data, rounded to the 1,920 B grain: 576,000 B per
-    // chunk; the slot holds that many data bytes in 64-byte lines of 56.
+    // chunk; the slot holds that many data bytes in lines of kLL128LineBytes
+    // (600 rounds of 1 KiB with the default 128-byte line).
     // (VCCL_LL128_ALLOC=1: the buffers only — vcclCommSetAlgo may pick the
     // LL128 ring per call, the automatic choice is unchanged)
     // NCCL_PROTO without SIMPLE but with LL128 (e.g. "LL,LL128"): the LL128
@@ -439,7 +440,10 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
         c->ll128MaxBytes = ~(size_t)0;
       } else if (param_int("LL128", 0) != 0 && (c->algoAllowed & kAllowLL128)) {
         c->ll128MinBytes = (size_t)param_int("LL128_MIN", 64 << 10);
-        c->ll128MaxBytes = (size_t)param_int("LL128_MAX", 8 << 20);
+        // 1 MiB: the rehearsals have the LL128 ring ahead of the SIMPLE ring
+        // up to 256 KiB - 1 MiB and behind at 8 MiB, inside
+        // VCCL's own 64 KiB - 8 MiB LL128 range (enqueue.cc:2032)
+        c->ll128MaxBytes = (size_t)param_int("LL128_MAX", 1 << 20);
       }
     }
   }
