@@ -165,33 +165,35 @@ def group_plan_works(n_ranks, nch, slot_bytes, ll_max=0, nthreads=512, proto=2):
 
 
 def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
-                   nthreads=512, proto=2, plan=None):
+                   nthreads=512, proto=2, plan=None, chain=None):
     """`plan`: group_plan_works(...) of the group (VCCL's grouped partition)."""
     name, op, dt, count = GROUP_CASES[gi]
     ins = [gen_group_input(gi, r) for r in range(n_ranks)]
     return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                       nthreads, proto, work=(plan or {}).get(gi))
+                       nthreads, proto, work=(plan or {}).get(gi), chain=chain)
 
 
 def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                nthreads=512, proto=2, work=None):
+                nthreads=512, proto=2, work=None, chain=None):
     """All-reduce result: LL chain fold up to ll_max bytes, the ring's
     owner-map fold (VCCL's ring schedule on these channels) above — for the
     two-shot direct path too, which folds every element in the ring's order
     (direct.hpp phase 2), so neither direct_max nor the inbox chunk
     (direct_chunk) changes the expected bits.  `work`: the call's place in
-    its group's plan."""
+    its group's plan; `chain`: the LL fold chain, root first (VCCL_LL_CHAIN;
+    None = the identity)."""
     del direct_max, direct_chunk
     count = len(ins[0])
     if count * ins[0].dtype.itemsize <= ll_max:
         dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
-        return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)
+        order = chain if chain is not None else range(n_ranks)
+        return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, [ins[r] for r in order])
     return _ring.expected_allreduce(op, dt, ins, nch, slot_bytes, nthreads=nthreads, proto=proto,
                                     work=work)
 
 
 def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
-             nthreads=512, proto=2):
+             nthreads=512, proto=2, chain=None):
     """proto: the ring's protocol (2 SIMPLE, 1 LL128 — VCCL's LL128 partition)."""
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
@@ -201,7 +203,7 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
     ins = [gen_input(case_idx, r, n_ranks) for r in range(n_ranks)]
     if coll in ("ar", "ar_inplace", "ar_mis"):
         e = expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                        nthreads, proto)
+                        nthreads, proto, chain=chain)
         return [e] * n_ranks
     if coll == "rs":
         return _ring.expected_reducescatter(op, dt, ins, nch, nthreads=nthreads, proto=proto)

@@ -45,13 +45,14 @@ DIRECT_TEST = 4 << 20
 DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in chunks
 
 
-def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST, nthreads=512, proto=2):
+def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST, nthreads=512, proto=2,
+           chain=None):
     """Bit-exact against the path's own fold order (the ring's IS VCCL's
     schedule on our rings and channels); for fp sum / prod additionally
     within the §8c tolerance of the exact value and of VCCL's result on its
     reference geometry (RC.vccl_reference)."""
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto)
+    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto, chain)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
     vref = RC.vccl_reference(ci, n)
@@ -166,15 +167,24 @@ def test_single_process_ranks(n, monkeypatch):
 @pytest.mark.parametrize("n,geom", [(2, "default"), (3, "test"), (4, "test"), (6, "test"), (8, "test"),
                                     (2, "ring_only"), (4, "ring_only"), (7, "ring_only"),
                                     (8, "ring_only"), (4, "direct_only"), (8, "default8"), (2, "net"),
-                                    (3, "net"), (2, "ll128"), (4, "ll128"), (8, "ll128")])
+                                    (3, "net"), (2, "ll128"), (4, "ll128"), (8, "ll128"),
+                                    (4, "chain"), (8, "chain")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
     ll_max, direct_max, chunk = LL_DEFAULT, DIRECT_TEST, DIRECT_CHUNK_TEST
-    nthreads, proto = 512, 2
-    if geom == "ll128":
+    nthreads, proto, chain = 512, 2, None
+    if geom == "chain":
+        # VERDICT r3 missing #2: the LL all-reduce folds along a chain other
+        # than the identity (VCCL's tree chain follows its topology order,
+        # graph/connect.cc:64-65), pinned with VCCL_LL_CHAIN
+        env.update(TEST_GEOM)
+        chain = {4: [2, 0, 3, 1], 8: [5, 2, 7, 0, 3, 6, 1, 4]}[n]
+        env["VCCL_LL_CHAIN"] = ",".join(map(str, chain))
+        nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+    elif geom == "ll128":
         # NCCL_PROTO=LL128: every collective on the LL128 ring (ring.hpp
         # prim_ll128), on VCCL's LL128 partition and chunking
         env.update(TEST_GEOM)
@@ -234,9 +244,9 @@ def test_multi_process_ranks(n, geom):
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
             _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk,
-                   nthreads, proto)
+                   nthreads, proto, chain)
         _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot, ll_max,
-                     direct_max, chunk, nthreads, proto)
+                     direct_max, chunk, nthreads, proto, chain)
         # every geometry fuses the group's runs (LL, direct or ring batches)
         fused = int(res[0]["launch_stats"][1])
         assert fused > 0, f"fused group launches: {fused}"
@@ -279,7 +289,7 @@ def test_beyond_2gib_two_ranks():
     assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
 
 
-def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512, proto=2):
+def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512, proto=2, chain=None):
     """Bit-exact against VCCL's GROUPED schedule on our rings and channels:
     the calls on the ring / direct paths take their place in VCCL's
     multi-task plan (oracle plan_schedule); fp sum / prod also
@@ -288,7 +298,8 @@ def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512, pr
     plan = RC.group_plan_works(n, nch, slot, ll_max, nthreads, proto)
     vplan = RC.group_plan_works(n, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT)
     for gi, (name, op, dt, count) in enumerate(RC.GROUP_CASES):
-        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto, plan=plan)
+        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto, plan=plan,
+                                chain=chain)
         for r in range(n):
             assert_bitexact(dt, outs[r][name], exp, minmax=op in (2, 3),
                             what=f"group {name} n={n} rank {r}")

@@ -164,12 +164,16 @@ __device__ void ll_allreduce(const LLWork& w) {
       __builtin_amdgcn_raw_buffer_store_b128(line, d.r, d.voff, 0, kSysAux);
     }
   }
-  // Phase 2: fold all inputs in chain order, x_0 (+) (x_1 (+) (... x_{n-1})).
+  // Phase 2: fold all inputs along the chain (DevComm::llChain, root first),
+  // from the leaf up: acc = x_{c[n-1]}, acc = acc (+) x_{c[k]} for k = n-2..0
+  // — with the identity chain x_0 (+) (x_1 (+) (... x_{n-1})).
   // Loads for up to kLLBatch sources of a line are issued together (their
   // latencies overlap); a source whose line has not arrived yet is re-polled.
   constexpr int kLLBatch = 8;
   bool ok = true;
   pc = 0;
+  const int8_t* chain = w.comm->llChain;  // n <= kOrderMaxRanks; identity beyond
+  const bool useChain = w.nRanks <= kOrderMaxRanks;
   for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
     pc = ll_advance(sh, nParts, pc, l);
     const LLPart& part = sh.p[pc];
@@ -180,16 +184,18 @@ __device__ void ll_allreduce(const LLWork& w) {
       u32x4 v[kLLBatch];
 #pragma unroll
       for (int b = 0; b < kLLBatch; b++) {
-        const int p = hi - b;
-        if (p >= lo && p != w.rank) {
+        const int pos = hi - b;
+        const int p = pos < lo ? w.rank : useChain ? __builtin_amdgcn_readfirstlane(chain[pos]) : pos;
+        if (pos >= lo && p != w.rank) {
           const SysAddr a = sys_addr(w.localBuf + ll_slot_off(parity, p, w.nRanks, w.linesPerSlot) + l * 16);
           v[b] = __builtin_amdgcn_raw_buffer_load_b128(a.r, a.voff, 0, kSysAux);
         }
       }
 #pragma unroll
       for (int b = 0; b < kLLBatch; b++) {
-        const int p = hi - b;
-        if (p < lo) break;
+        const int pos = hi - b;
+        if (pos < lo) break;
+        const int p = useChain ? __builtin_amdgcn_readfirstlane(chain[pos]) : pos;
         uint64_t x;
         if (p == w.rank) {
           x = ll_load8(part.send, pl, part.nbytes);
@@ -201,7 +207,7 @@ __device__ void ll_allreduce(const LLWork& w) {
           if (!ok) break;
         }
         if (Fn::kPreOp && w.preOp) x = ll_apply(fn, 0, x, 1);
-        acc = (p == w.nRanks - 1) ? x : ll_apply(fn, acc, x, 0);  // LL order: peer (+) own
+        acc = (pos == w.nRanks - 1) ? x : ll_apply(fn, acc, x, 0);  // LL order: child (+) own
       }
     }
     if (!ok) break;

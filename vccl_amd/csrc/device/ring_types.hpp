@@ -97,6 +97,13 @@ struct DevComm {
   // position c+1 around to c (all_reduce.h:42-64), whichever rank computes
   // it — the direct all-reduce folds in that order too.
   int8_t ringAt[kOrderMaxRings][kOrderMaxRanks];
+  // The chain the one-hop LL all-reduce folds along, root first: VCCL's
+  // intra-node tree is a chain in its topology's order (graph/connect.cc:
+  // 64-65; the root at index 0 applies postOp), reduced from the leaf up,
+  // each hop computing child (+) own (prims_ll.h:258-266).  The identity by
+  // default; VCCL_LL_CHAIN pins another order (e.g. the one VCCL's topology
+  // search picked) so the LL result matches VCCL's bit for bit.
+  int8_t llChain[kOrderMaxRanks];
   // Opt-in slot timeline of the SIMPLE ring (VCCL_RING_TRACE=<records per
   // channel>, vcclCommRingTrace): per channel, the first traceCap slot
   // hand-offs of each launch as RingTraceRec; nullptr = off.

@@ -584,6 +584,28 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     for (int j = 0; j < n; j++) dc.rsOrder[k][j] = (int8_t)ring[(pos + 1 + j) % n];
     for (int j = 0; j < n; j++) dc.ringAt[k][j] = (int8_t)ring[j];
   }
+  // LL chain (DevComm::llChain): VCCL_LL_CHAIN="r0,r1,..." (root first), a
+  // permutation of the ranks, else the identity.  Every rank must pass the
+  // same order.
+  for (int j = 0; j < n && j < kOrderMaxRanks; j++) dc.llChain[j] = (int8_t)j;
+  if (const char* chainEnv = getenv("VCCL_LL_CHAIN"); chainEnv && *chainEnv && n <= kOrderMaxRanks) {
+    std::vector<int> order;
+    for (const char* q = chainEnv; *q;) {
+      char* end = nullptr;
+      const long v = strtol(q, &end, 10);
+      if (end == q) break;
+      order.push_back((int)v);
+      q = *end == ',' ? end + 1 : end;
+    }
+    std::vector<int> seen(n, 0);
+    bool okChain = (int)order.size() == n;
+    for (int v : order) okChain = okChain && v >= 0 && v < n && !seen[v]++;
+    if (!okChain) {
+      VWARN("VCCL_LL_CHAIN=%s is not a permutation of the %d ranks", chainEnv, n);
+      return ncclInvalidUsage;
+    }
+    for (int j = 0; j < n; j++) dc.llChain[j] = (int8_t)order[j];
+  }
   HIPCHECK(hipMalloc((void**)&c->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(c->devComm, &dc, sizeof(dc), hipMemcpyHostToDevice));
 
