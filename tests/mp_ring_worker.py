@@ -24,6 +24,8 @@ def main():
     outdir = sys.argv[5]
     torch.cuda.set_device(device)
     comm = nccl.Comm.init_rank(nranks, uid, rank)
+    if os.environ.get("VCCL_TEST_SET_ALGO"):  # vcclCommSetAlgo for every call
+        comm.set_algo(os.environ["VCCL_TEST_SET_ALGO"])
     s = torch.cuda.current_stream().cuda_stream
     res = {}
     for ci, (name, coll, op, dt, count) in enumerate(RC.CASES):

@@ -168,7 +168,7 @@ def test_single_process_ranks(n, monkeypatch):
                                     (2, "ring_only"), (4, "ring_only"), (7, "ring_only"),
                                     (8, "ring_only"), (4, "direct_only"), (8, "default8"), (2, "net"),
                                     (3, "net"), (2, "ll128"), (4, "ll128"), (8, "ll128"),
-                                    (4, "chain"), (8, "chain")])
+                                    (4, "chain"), (8, "chain"), (2, "net_ll128")])
 def test_multi_process_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
@@ -201,7 +201,7 @@ def test_multi_process_ranks(n, geom):
         if geom == "direct_only":  # every collective takes the direct path, any size
             env["NCCL_ALGO"] = "Direct"
             ll_max, direct_max = 0, 1 << 62
-    elif geom == "net":
+    elif geom in ("net", "net_ll128"):
         # every ring connection through the net proxy (host-pinned staging +
         # TCP, proxy.cc), as between nodes; LL / direct need the xGMI mesh,
         # so every all-reduce takes the ring, on NET_NCHANNELS channels
@@ -209,6 +209,12 @@ def test_multi_process_ranks(n, geom):
         env.update(VCCL_NET_FORCE="1", VCCL_NET_NCHANNELS="3", VCCL_SLOT_BYTES=str(64 << 10))
         nch, slot = 3, 64 << 10
         ll_max = direct_max = 0
+        if geom == "net_ll128":
+            # LL128 FIFOs requested (VCCL_LL128_ALLOC) and the LL128
+            # ring forced per call (vcclCommSetAlgo) on a comm with net peers —
+            # no LL128 slot is mapped there, so every call must take the
+            # SIMPLE ring, not a ring of null LL128 slots
+            env.update(VCCL_LL128_ALLOC="1", VCCL_TEST_SET_ALGO="ll128")
     elif geom == "default8":
         # library defaults except the LL grid (8 ranks share the one GPU)
         for k in TEST_GEOM:
@@ -252,7 +258,7 @@ def test_multi_process_ranks(n, geom):
         assert fused > 0, f"fused group launches: {fused}"
         for r in range(n):
             sent, recvd, conns = (int(v) for v in res[r]["net_stats"])
-            if geom == "net":  # one send and one receive connection per channel
+            if geom.startswith("net"):  # one send and one receive connection per channel
                 assert conns == 2 * nch and sent > 0 and recvd > 0, (r, sent, recvd, conns)
             else:
                 assert conns == 0 and sent == 0, (r, sent, conns)

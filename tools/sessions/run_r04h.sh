@@ -6,7 +6,7 @@ cd ${GRAFT_REPO_ROOT:-$(pwd)}
 O=gpurun_out/r04h; mkdir -p $O
 export TMPDIR=/tmp
 echo "== chain tests $(date +%T)"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_collectives.py -m gpu -x -q --timeout 300 --timeout-method thread -k "chain or 4-test" > $O/pytest_chain.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_collectives.py -m gpu -x -q --timeout 300 --timeout-method thread -k "chain or 4-test or net_ll128" > $O/pytest_chain.log 2>&1
 echo "== ring timing $(date +%T)"
 PMC_RING_TIMING_ONLY=1 PMC_RING_OUT=ring_slices.json PMC_RING_VARIANTS=alloc0_ch96,slice1m_ch96,slice2m_ch96,alloc0_ch16,slice1m_ch16 timeout -k 10 600 python -u tools/pmc_ring.py > $O/ring_slices.log 2>&1
 cp gpurun_out/ring_slices.json $O/
