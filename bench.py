@@ -708,6 +708,29 @@ def check_group(dist, comm, rank, world, nbytes, k):
     return _all_ok(dist, ok and comm.async_error() == 0)
 
 
+def check_zero_group(dist, comm, rank, world, nbytes, k, dtype="bf16"):
+    """The ZeRO bucket loop: k reduce-scatters of `nbytes` buckets in one
+    ncclGroupStart/End (VCCL's grouped plan, host/enqueue.cc group_plan),
+    pattern inputs; True on every rank iff every shard is exact."""
+    tdt = _TDT[dtype]
+    n = nbytes // torch.tensor([], dtype=tdt).element_size()
+    rc = n // world
+    xs = [torch.empty(rc * world, dtype=tdt, device="cuda") for _ in range(k)]
+    ys = [torch.full((rc,), float("nan"), dtype=tdt, device="cuda") for _ in range(k)]
+    for j, x in enumerate(xs):
+        pattern_fill(x, rank, world, base=j << 26)
+    sp = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    nccl.group_start()
+    for x, y in zip(xs, ys):
+        comm.reduce_scatter(x.data_ptr(), y.data_ptr(), rc, _CODE[dtype], nccl.ncclSum, sp)
+    nccl.group_end()
+    torch.cuda.synchronize()
+    ok = all(pattern_ok(y, world, base=(j << 26) + rank * rc) for j, y in enumerate(ys))
+    del xs, ys
+    return _all_ok(dist, ok and comm.async_error() == 0)
+
+
 def _fences_plan(plan, algo_of):
     """One check per path family (kind, dtype, algorithm actually run) for the
     fences-on pass, at the family's smallest planned size (RS + AG at <= 64
@@ -735,10 +758,13 @@ def run_checks(dist, comm, rank, world, plan):
     def algo_of(kind, kw):
         if kw.get("algo"):
             return kw["algo"]
-        esz = torch.tensor([], dtype=_TDT[kw.get("dtype", "f32" if kind != "rs_ag" else "bf16")]).element_size()
+        dflt = "bf16" if kind in ("rs_ag", "zero_group") else "f32"
+        esz = torch.tensor([], dtype=_TDT[kw.get("dtype", dflt)]).element_size()
         n = max(1, kw["nbytes"] // esz)
-        code = _CODE[kw.get("dtype", "f32" if kind != "rs_ag" else "bf16")]
-        return comm.coll_algo(1, n // world, code) if kind == "rs_ag" else comm.coll_algo(0, n, code)
+        code = _CODE[kw.get("dtype", dflt)]
+        if kind in ("rs_ag", "zero_group"):
+            return comm.coll_algo(1, n // world, code)
+        return comm.coll_algo(0, n, code)
 
     res = {"check_ms": {}}
     for mode, fences, pl in (("fences_off", False, plan),
@@ -752,6 +778,8 @@ def run_checks(dist, comm, rank, world, plan):
                     r[name] = check_ar(dist, comm, rank, world, **kw)
                 elif kind == "group":
                     r[name] = check_group(dist, comm, rank, world, **kw)
+                elif kind == "zero_group":
+                    r[name] = check_zero_group(dist, comm, rank, world, **kw)
                 else:
                     rs_ok, ag_ok = check_rs_ag(dist, comm, rank, world, **kw)
                     r[name + "_rs"], r[name + "_ag"] = rs_ok, ag_ok
@@ -838,6 +866,7 @@ def bench_allreduce(args):
                 plan[f"ar_mid_{algo}_{S}"] = ("ar", {"nbytes": S, "algo": algo})
         for S in EXTRA_GROUP_SIZES:
             plan[f"group16_{S}"] = ("group", {"nbytes": S, "k": 16})
+        plan[f"zero_group16_{ZERO_BUCKET}"] = ("zero_group", {"nbytes": ZERO_BUCKET, "k": 16})
         plan[f"rs_ag_bf16_{args.rs_ag_bytes}"] = ("rs_ag", {"nbytes": args.rs_ag_bytes})
         plan[f"rs_ag_bf16_direct_{args.rs_ag_bytes}"] = ("rs_ag", {"nbytes": args.rs_ag_bytes,
                                                                    "algo": "direct"})
@@ -985,6 +1014,40 @@ def _group_row(dist, comm, rank, world, S, k, steps=20, warmup=3):
             "algo": comm.coll_algo(0, n, nccl.ncclFloat32)}
 
 
+ZERO_BUCKET = 8 << 20  # bytes per bucket of the ZeRO reduce-scatter group row
+
+
+def _zero_group_row(dist, comm, rank, world, S=ZERO_BUCKET, k=16, steps=10, warmup=2):
+    """The ZeRO bucket loop: k reduce-scatters of S-byte bf16 buckets issued
+    one by one vs inside one ncclGroupStart/End, where they take VCCL's
+    grouped plan (shared channels, one fused launch); busbw per rank over the
+    k buckets, (k S / t) (n-1)/n."""
+    sp = torch.cuda.current_stream().cuda_stream
+    n = S // 2
+    rc = n // world
+    xs = [torch.rand(rc * world, device="cuda").to(torch.bfloat16) for _ in range(k)]
+    ys = [torch.empty(rc, dtype=torch.bfloat16, device="cuda") for _ in range(k)]
+
+    def calls():
+        for x, y in zip(xs, ys):
+            comm.reduce_scatter(x.data_ptr(), y.data_ptr(), rc, nccl.ncclBfloat16, nccl.ncclSum, sp)
+
+    def grouped():
+        nccl.group_start()
+        calls()
+        nccl.group_end()
+    t_sep = _time_coll(dist, calls, steps, warmup)
+    f0 = comm.launch_stats()[1]
+    t_grp = _time_coll(dist, grouped, steps, warmup)
+    bw = lambda t: round(k * S * steps / t / 1e9 * (world - 1) / world, 2)  # noqa: E731
+    del xs, ys
+    return {"bucket_bytes": S, "calls": k, "dtype": "bf16", "us_separate": round(t_sep / steps * 1e6, 2),
+            "us_grouped": round(t_grp / steps * 1e6, 2), "busbw_separate": bw(t_sep),
+            "busbw_grouped": bw(t_grp),
+            "fused_launches_per_group": (comm.launch_stats()[1] - f0) / (steps + warmup),
+            "algo": comm.coll_algo(1, rc, nccl.ncclBfloat16)}
+
+
 def bench_extras(dist, comm, rank, world, args):
     """Secondary BASELINE configs measured in the same multi-GPU run (reported
     beside the headline, never as ``value``): config 3 at a few sizes (fp32),
@@ -1001,6 +1064,7 @@ def bench_extras(dist, comm, rank, world, args):
         ex["allreduce_error"] = repr(e)
     try:
         ex["group_fusion_f32"] = [_group_row(dist, comm, rank, world, S, 16) for S in EXTRA_GROUP_SIZES]
+        ex["zero_group_rs_bf16"] = _zero_group_row(dist, comm, rank, world)
     except Exception as e:  # noqa: BLE001
         ex["group_error"] = repr(e)
     try:  # each algorithm forced at two bucket sizes (vcclCommSetAlgo): the SIMPLE
