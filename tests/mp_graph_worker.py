@@ -7,8 +7,10 @@ Captures [LL all-reduce (small), direct all-reduce (mid), ring all-reduce
 into one graph on a side stream (after an eager call on the current stream,
 and followed by another), replays it 4 times with new integer-valued inputs (exact in any
 fold order) and checks every output; then two captures interleaved on the
-same comm (interleaved_captures); then collectives that fail inside a
-capture (failing_calls_in_capture); exit code 0 = all replays correct."""
+same comm (interleaved_captures); a group of ring and direct calls on two
+streams inside one capture (group_in_capture); then collectives that fail
+inside a capture (failing_calls_in_capture); exit code 0 = all replays
+correct."""
 import os
 import sys
 
@@ -61,6 +63,48 @@ def interleaved_captures(comm, rank, n):
             ok &= torch.equal(y, sum(val(r, k) for r in range(n)))
     if not ok:
         print(f"rank {rank}: interleaved captures mismatch", flush=True)
+    return ok
+
+
+def group_in_capture(comm, rank, n):
+    """A group of ring and direct calls on two streams inside one capture:
+    the planned sequence (VCCL's group plan, several launches joined onto one
+    stream) is captured as a fork / join in the graph and replays exactly."""
+    sizes = [(0, 5 << 20), (0, 300_001), (1, 1 << 20), (0, 9 << 20), (0, 500_001)]  # (coll, count)
+    xs = [torch.empty(c * n if coll == 1 else c, device="cuda") for coll, c in sizes]
+    ys = [torch.empty(c, device="cuda") for _, c in sizes]
+    sA, sB = torch.cuda.Stream(), torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    f32, add = nccl.ncclFloat32, nccl.ncclSum
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sA):
+        g.capture_begin(capture_error_mode="relaxed")
+    sB.wait_stream(sA)
+    nccl.group_start()
+    for i, ((coll, c), x, y) in enumerate(zip(sizes, xs, ys)):
+        st = (sA if i % 2 == 0 else sB).cuda_stream
+        if coll == 0:
+            comm.all_reduce(x.data_ptr(), y.data_ptr(), c, f32, add, st)
+        else:
+            comm.reduce_scatter(x.data_ptr(), y.data_ptr(), c, f32, add, st)
+    nccl.group_end()
+    sA.wait_stream(sB)
+    with torch.cuda.stream(sA):
+        g.capture_end()
+    ok = True
+    for it in range(3):
+        def val(r, m, k):
+            return ((torch.arange(m, device="cuda") * (r + 3 + k) + 5 * it) % 83).float()
+        for k, ((coll, c), x) in enumerate(zip(sizes, xs)):
+            x.copy_(val(rank, x.numel(), k))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        for k, ((coll, c), y) in enumerate(zip(sizes, ys)):
+            full = sum(val(r, c * n if coll == 1 else c, k) for r in range(n))
+            ok &= torch.equal(y, full[rank * c:(rank + 1) * c] if coll == 1 else full)
+    if not ok:
+        print(f"rank {rank}: group in capture mismatch", flush=True)
     return ok
 
 
@@ -192,6 +236,7 @@ def main():
     torch.cuda.synchronize()
     ok &= torch.equal(eager_y, exp_eager)
     ok &= interleaved_captures(comm, rank, n)
+    ok &= group_in_capture(comm, rank, n)
     ok &= failing_calls_in_capture(comm, rank, n)
     ok &= comm.async_error() == 0
     comm.destroy()
