@@ -108,6 +108,40 @@ def group_in_capture(comm, rank, n):
     return ok
 
 
+def captures_on_destroyed_streams(comm, rank, n):
+    """The capture-ordering pool after 16 captures whose streams were
+    destroyed: each entry's capture has ended and its stream is gone, so a
+    new capture must find a free entry (the liveness query on a destroyed
+    stream handle reads as ended, host/enqueue.cc capture_live) — no crash, no
+    refusal — and replay exactly."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp = ctypes.c_void_p
+    small = 2048
+    x = torch.arange(small, device="cuda", dtype=torch.float32) + rank
+    y = torch.empty_like(x)
+    torch.cuda.synchronize()
+    for i in range(16):
+        st, graph = vp(), vp()
+        assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+        assert hip.hipStreamBeginCapture(st, 2) == 0  # hipStreamCaptureModeRelaxed
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), small, nccl.ncclFloat32, nccl.ncclSum, st.value)
+        assert hip.hipStreamEndCapture(st, ctypes.byref(graph)) == 0
+        assert hip.hipGraphDestroy(graph) == 0
+        assert hip.hipStreamDestroy(st) == 0
+    s, g = torch.cuda.Stream(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), small, nccl.ncclFloat32, nccl.ncclSum, s.cuda_stream)
+    y.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    ok = torch.equal(y, sum(torch.arange(small, device="cuda", dtype=torch.float32) + r for r in range(n)))
+    if not ok:
+        print(f"rank {rank}: capture after destroyed-stream captures mismatch", flush=True)
+    return ok
+
+
 def failing_calls_in_capture(comm, rank, n):
     """collectives that fail inside a HIP graph capture return
     an ncclResult_t and leave the capture and the process usable.
@@ -238,6 +272,7 @@ def main():
     ok &= interleaved_captures(comm, rank, n)
     ok &= group_in_capture(comm, rank, n)
     ok &= failing_calls_in_capture(comm, rank, n)
+    ok &= captures_on_destroyed_streams(comm, rank, n)
     ok &= comm.async_error() == 0
     comm.destroy()
     sys.exit(0 if ok else 4)
