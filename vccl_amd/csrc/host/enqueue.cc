@@ -226,6 +226,9 @@ static ncclResult_t capture_state(hipStream_t s, CaptureState* cs) {
 // id takes the least recently used entry whose capture has ended.  When every
 // entry still belongs to a live capture, the call fails (ncclInvalidUsage)
 // rather than silently dropping a live capture's ordering.
+// A capture is live while its last stream still captures under its id; a
+// stream destroyed since reads as ended (HIP validates the handle and fails
+// the query — tests/mp_graph_worker.py captures_on_destroyed_streams).
 static bool capture_live(const ncclComm::CapOrder& c) {
   if (!c.used || !c.has) return false;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
