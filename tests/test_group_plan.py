@@ -59,10 +59,10 @@ def _check_equal(calls, n, nch, slot=512 << 10, nthreads=512):
     return order, plan_of, parts
 
 
-@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8])
 def test_library_group_plan_equals_oracle(n):
     rng = np.random.default_rng(100 + n)
-    for trial in range(60):
+    for trial in range(40):
         k = int(rng.integers(1, 17))
         calls = []
         for _ in range(k):
@@ -72,8 +72,9 @@ def test_library_group_plan_equals_oracle(n):
             count = int(rng.choice([1, 100, 4096, 65_536, 1 << 20, (1 << 20) + 37, 3 << 20, 1 << 24])) \
                 + int(rng.integers(0, 64))
             calls.append((coll, count, dt, op))
-        nch = int(rng.choice([1, 2, 16, 48, 56, 64]))
-        _check_equal(calls, n, nch)
+        nch = int(rng.choice([1, 2, 16, 32, 48, 56, 60, 63, 64]))  # incl. the defaults at 2-8 ranks
+        nt = int(rng.choice([256, 512]))
+        _check_equal(calls, n, nch, nthreads=nt)
 
 
 def test_single_call_group_is_the_call_partition():
