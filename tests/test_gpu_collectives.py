@@ -540,6 +540,60 @@ def test_group_mixed_direct_sizes():
                     assert_bitexact(dt, res[r][name], exp, what=f"{name} rank {r}")
 
 
+@pytest.mark.parametrize("geom", ["test", "ring_only"])
+def test_group_plan_stress(geom):
+    """36 calls in one group (AR / RS / AG of f32 / bf16 / i32, sum and max,
+    1 KiB - 6 MiB, two streams) at 4 ranks: several (func, op, type) bins,
+    aggregates and batches of up to 16 parts with channels skipped per part.
+    Every output bit-exact: ring / direct calls against VCCL's grouped plan
+    (the path of each call read back with vcclCommCollAlgo), LL calls against
+    their own fold; a second run of the group is bitwise identical."""
+    from oracle import oracle as O
+    from tests import mp_group_stress_worker as G
+    n = 4
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    env.update(TEST_GEOM)
+    if geom == "ring_only":
+        env["NCCL_ALGO"] = "Ring"
+    nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_group_stress_worker.py"),
+                                   str(r), str(n), hexid, d], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
+    calls = G.stress_calls(n)
+    algos = [str(a) for a in res[0]["algos"]]
+    assert set(algos) <= {"ll", "ring", "direct"}, algos
+    if geom == "ring_only":
+        assert set(algos) == {"ring"}
+    else:
+        assert len(set(algos)) >= 2, algos  # the plan spans paths
+    for r in range(n):
+        assert not [k for k in res[r] if k.endswith("_differs")], r
+    planned = [i for i, a in enumerate(algos) if a in ("ring", "direct")]
+    works = dict(zip(planned, _ring.group_works([(calls[i][1], calls[i][3], calls[i][2], calls[i][4])
+                                                 for i in planned], n, nch, slot)))
+    for i, (name, coll, dt, op, count) in enumerate(calls):
+        ins = [G.gen(name, dt, G.in_count(coll, count, n), r) for r in range(n)]
+        if coll == "ag":
+            exp = [np.concatenate(ins)] * n
+        elif coll == "rs":
+            exp = _ring.expected_reducescatter(op, dt, ins, nch, slot, work=works.get(i))
+        elif algos[i] == "ll":
+            dev_op, arg = O.host_to_dev_redop(op, dt, n)
+            exp = [O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)] * n
+        else:
+            exp = [_ring.expected_allreduce(op, dt, ins, nch, slot, work=works[i])] * n
+        for r in range(n):
+            assert_bitexact(dt, res[r][name], exp[r], minmax=op in (2, 3),
+                            what=f"{name} ({algos[i]}) {geom} rank {r}")
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_ring_trace_and_shared_cap(n):
     """The SIMPLE ring's slot timeline (VCCL_RING_TRACE, vcclCommRingTrace)
