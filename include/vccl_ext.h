@@ -47,7 +47,7 @@
  *                     call (host only): VCCL's cbd split and chunking
  *                     (scheduleCollTasksToPlan, src/enqueue.cc:518-644, for a
  *                     plan of one collective) for `nChannels` channels,
- *                     protocol `proto` (2 SIMPLE, 1 LL128) with a FIFO step
+ *                     protocol `proto` (2 SIMPLE, 1 LL128, 0 LL) with a FIFO step
  *                     of `stepBytes` (that protocol's buffer size / 8) and
  *                     `nThreads` ring threads (NCCL_NTHREADS: the channel
  *                     tuning's maxThreads[RING][SIMPLE], tuning.cc:198-200).
@@ -74,7 +74,23 @@
  *                     ignored for all-gather).  Outputs: order[0..n) the calls
  *                     in plan (execution) order, planOf[i] the kernel plan of
  *                     call i, cbd[8 i .. 8 i + 8) its partition as in
- *                     vcclRingPartition.
+ *                     vcclRingPartition.  Every call is taken as RING /
+ *                     SIMPLE (LL128 geometry: VCCL's defaults).
+ *   vcclGroupPlanEx    the same plan with a path per aggregate, as a comm
+ *                     lays out a group: each aggregate takes the path the
+ *                     library's selection gives its summed count (VCCL gives
+ *                     getAlgoInfo's choice to every member, enqueue.cc:
+ *                     387-427) and is placed under that path's protocol (LL
+ *                     traffic x4).  geometry[4] = SIMPLE step bytes,
+ *                     NCCL_NTHREADS, LL128 step bytes, NCCL_LL128_NTHREADS;
+ *                     policy[10] (NULL: every call RING / SIMPLE) =
+ *                     algoForce (0 automatic, 1 ring, 2 LL, 3 direct,
+ *                     4 LL128), LL slot bytes (0: no LL buffers), LL
+ *                     all-reduce max bytes, LL RS / AG max bucket bytes,
+ *                     LL128 FIFOs (0/1), LL128 window min, max (0: off),
+ *                     direct inboxes (0/1), direct all-reduce max bytes,
+ *                     direct RS / AG max bucket bytes; algos[i] (may be
+ *                     NULL) = the vcclAlgo_t of call i.
  *   vcclAlgoSelection  how NCCL_ALGO / NCCL_PROTO strings select paths (the
  *                     reference's parseList, graph/tuning.cc:53-116: comma
  *                     lists, a leading '^' excludes): *force = 0 automatic,
@@ -99,7 +115,7 @@ typedef enum {
   vcclAlgoLL = 1,       /* one-shot LL all-reduce, chain-tree fold */
   vcclAlgoDirect = 2,   /* two-shot direct all-reduce over the full mesh */
   vcclAlgoOneRank = 3,  /* nRanks == 1: copy / PreMulSum kernel */
-  vcclAlgoLL128 = 4     /* ring over LL128 FIFOs (64-byte lines, in-line flags) */
+  vcclAlgoLL128 = 4     /* ring over LL128 FIFOs (128-byte lines, in-line flags) */
 } vcclAlgo_t;
 
 ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count, ncclDataType_t datatype,
@@ -123,6 +139,9 @@ ncclResult_t vcclRingOrders(int nRanks, int maxRings, int* orders, int* nRings);
 ncclResult_t vcclGroupPlan(int nCalls, const int* colls, const size_t* counts, const int* datatypes,
                            const int* ops, int nRanks, int nChannels, size_t stepBytes, int nThreads,
                            int* order, int* planOf, int64_t* cbd);
+ncclResult_t vcclGroupPlanEx(int nCalls, const int* colls, const size_t* counts, const int* datatypes,
+                             const int* ops, int nRanks, int nChannels, const int64_t* geometry,
+                             const int64_t* policy, int* algos, int* order, int* planOf, int64_t* cbd);
 ncclResult_t vcclAlgoSelection(const char* algo, const char* proto, int* force, int* allowed);
 
 #ifdef __cplusplus

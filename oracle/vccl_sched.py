@@ -110,10 +110,13 @@ def chunk_size(proto, buff_size=None):
 
 def ring_n_max_channels(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPLE,
                         nthreads=None):
-    """topoGetAlgoInfo's ring channel count for this call (enqueue.cc:1902-1925)."""
+    """topoGetAlgoInfo's ring / tree channel count for this call
+    (enqueue.cc:1902-1925); LL's threshold is times nRanks on the ring
+    (tuning.cc:493) — reduce-scatter / all-gather — not on the tree that
+    carries VCCL's LL all-reduce."""
     nbytes = elt_size * max_send_recv_count(coll, nranks, count)
     nt = MAX_THREADS[proto] if nthreads is None else nthreads
-    thr = THREAD_THRESHOLD[proto] * (nranks if proto == PROTO_LL else 1)
+    thr = THREAD_THRESHOLD[proto] * (nranks if proto == PROTO_LL and coll != "ar" else 1)
     nc = comm_channels
     while nbytes < nc * nt * thr:
         if nc >= 2:
@@ -132,7 +135,7 @@ def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPL
     if coll == "ag":
         count, elt_size = count * elt_size, 1
     tpb = traffic_per_byte(coll, nranks)
-    task_traffic = count * elt_size * tpb
+    task_traffic = count * elt_size * tpb * (4 if proto == PROTO_LL else 1)   # enqueue.cc:418
     n_task_ch = ring_n_max_channels(coll, count, elt_size, nranks, comm_channels, proto, nthreads)
     traffic = max(MIN_TRAFFIC_PER_CHANNEL, task_traffic)
     n_ch = min(n_task_ch, comm_channels)
@@ -185,8 +188,8 @@ def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPL
 
 
 # ------------------------------------------------------------------ group plan
-# VCCL's plan for a GROUP of ring collectives of one communicator (all taken
-# as RING / SIMPLE):
+# VCCL's plan for a GROUP of collectives of one communicator (every call RING
+# / SIMPLE unless `algo_of` gives each aggregate its path):
 #   * taskAppend (enqueue.cc:2398-2413): AG as int8 bytes, trafficBytes =
 #     count * eltSize * trafficPerByte, inserted into ncclTaskCollSorter;
 #   * the sorter (comm.h:294-343): bin = BinCount-1 - u32fpEncode(min(size,
@@ -195,7 +198,10 @@ def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPL
 #   * ncclPrepareTasks (enqueue.cc:352-437): pushed onto one LIFO per
 #     (func, devOp, type) -> each list size-ascending, lists in order of first
 #     appearance; runs within 4x of the run's first trafficBytes aggregated,
-#     nMaxChannels from the ring tuning on the aggregate's count;
+#     the aggregate's path (getAlgoInfo, :398 — here `algo_of`, the library's
+#     selection standing in for VCCL's tuner) and nMaxChannels from the
+#     channel tuning on the aggregate's count, both given to every member;
+#     an LL member's trafficBytes x4 (:418);
 #   * scheduleCollTasksToPlan (enqueue.cc:518-769): per plan, the tasks that
 #     pass the work-budget estimate give trafficPerChannel = sum(max(16K,
 #     traffic)) / min(sum nMaxChannels, comm channels); every task is split
@@ -232,9 +238,10 @@ class GroupCall:
 
 
 def _place(cur, coll, count, elt_size, nranks, proto, buff_size):
-    """One task's cbd split at the plan cursor (enqueue.cc:597-644) and the
-    cursor advanced (:667-681).  cur = dict(tpc, ch, cur, nmax)."""
-    tpb = traffic_per_byte(coll, nranks)
+    """One task's cbd split at the plan cursor (enqueue.cc:597-644; LL traffic
+    x4, :599) and the cursor advanced (:667-681).  cur = dict(tpc, ch, cur,
+    nmax)."""
+    tpb = traffic_per_byte(coll, nranks) * (4 if proto == PROTO_LL else 1)
     cell = _div_up(_div_up(MIN_TRAFFIC_PER_CHANNEL, tpb), 16) * 16
     epc = cell // elt_size
     cells = _div_up(count * elt_size, cell)
@@ -280,11 +287,21 @@ def _place(cur, coll, count, elt_size, nranks, proto, buff_size):
     return work, dict(tpc=tpc, ch=ch, cur=used, nmax=nmax)
 
 
-def plan_schedule(calls, nranks, comm_channels, buff_size=None, nthreads=None):
-    """VCCL's plans for a group of ring calls.  Returns (order, plan_of,
-    works): the calls in execution order, the plan (kernel) index of every
-    call, and every call's CbdWork (indexed like `calls`)."""
-    proto = PROTO_SIMPLE
+ALGO_PROTO = {"ring": PROTO_SIMPLE, "direct": PROTO_SIMPLE, "ll": PROTO_LL, "ll128": PROTO_LL128}
+
+
+def plan_schedule(calls, nranks, comm_channels, buff_size=None, nthreads=None, algo_of=None,
+                  ll128_buff=None, ll128_threads=None, algos_out=None):
+    """VCCL's plans for a group of calls.  Returns (order, plan_of, works):
+    the calls in execution order, the plan (kernel) index of every call, and
+    every call's CbdWork (indexed like `calls`).
+
+    algo_of(i, agg_count) -> "ring" | "direct" | "ll" | "ll128": the path of
+    the aggregate headed by call i with agg_count elements in total (AG in
+    bytes); None = every call "ring".  The direct path is placed as a SIMPLE
+    ring call, "ll" as VCCL's LL (tree for the all-reduce, ring otherwise),
+    "ll128" as the LL128 ring (ll128_buff / ll128_threads: VCCL's defaults).
+    algos_out (a list) receives every call's path."""
     calls = [GroupCall(c.coll, c.count * c.elt_size, 1, c.key, c.func) if c.coll == "ag" else c
              for c in calls]
     traffic = [c.count * c.elt_size * traffic_per_byte(c.coll, nranks) for c in calls]
@@ -296,7 +313,7 @@ def plan_schedule(calls, nranks, comm_channels, buff_size=None, nthreads=None):
     by_key = {}
     for i in sorted_:
         by_key.setdefault(calls[i].key, []).insert(0, i)   # dicts keep first-appearance order
-    nmax, queue = {}, []
+    nmax, proto, algo, queue = {}, {}, {}, []
     for lst in by_key.values():
         a = 0
         while a < len(lst):
@@ -305,11 +322,19 @@ def plan_schedule(calls, nranks, comm_channels, buff_size=None, nthreads=None):
                 agg += calls[lst[e]].count
                 e += 1
             c0 = calls[lst[a]]
-            nc = ring_n_max_channels(c0.coll, agg, c0.elt_size, nranks, comm_channels, proto, nthreads)
+            path = algo_of(lst[a], agg) if algo_of is not None else "ring"
+            pr = ALGO_PROTO[path]
+            nt = (ll128_threads or MAX_THREADS[PROTO_LL128]) if pr == PROTO_LL128 else nthreads
+            nc = ring_n_max_channels(c0.coll, agg, c0.elt_size, nranks, comm_channels, pr, nt)
             for j in lst[a:e]:
-                nmax[j] = nc
+                nmax[j], proto[j], algo[j] = nc, pr, path
+                if pr == PROTO_LL:
+                    traffic[j] *= 4
             a = e
         queue += lst
+    if algos_out is not None:
+        algos_out[:] = [algo[i] for i in range(len(calls))]
+    buffs = {PROTO_SIMPLE: buff_size, PROTO_LL: None, PROTO_LL128: ll128_buff}
 
     def budget_ok(n_batches, work_bytes):
         bb = n_batches * WORK_BATCH_BYTES
@@ -332,18 +357,19 @@ def plan_schedule(calls, nranks, comm_channels, buff_size=None, nthreads=None):
         while n_plan and head < len(queue):
             i = queue[head]
             c = calls[i]
-            w, nxt = _place(cur, c.coll, c.count, c.elt_size, nranks, proto, buff_size)
+            w, nxt = _place(cur, c.coll, c.count, c.elt_size, nranks, proto[i], buffs[proto[i]])
             if not budget_ok(n_batches + w.channel_hi - w.channel_lo + 1, work_bytes + WORK_COLL_BYTES):
                 break
             cur = nxt
             for ch in range(w.channel_lo, w.channel_hi + 1):
                 b = batch.get(ch)
-                new = b is None or b[0] != c.func or b[2] + WORK_COLL_BYTES > MAX_BATCH_BYTES
+                fn = (c.func, proto[i])   # devFuncId: (func, op, type, algo, proto)
+                new = b is None or b[0] != fn or b[2] + WORK_COLL_BYTES > MAX_BATCH_BYTES
                 off = 0 if new else work_bytes - b[1]
                 if new or 63 * WORK_COLL_BYTES < off:
-                    b = [c.func, work_bytes, 0 if new else b[2]]
+                    b = [fn, work_bytes, 0 if new else b[2]]
                     n_batches += 1
-                b[0] = c.func
+                b[0] = fn
                 b[2] += WORK_COLL_BYTES
                 batch[ch] = b
             work_bytes += WORK_COLL_BYTES

@@ -83,10 +83,13 @@ def _div_up(x, a):
 
 
 def _sched(coll, count, esz, n, nch, slot_bytes, nthreads, proto):
-    """The ring's partition: SIMPLE with the comm's slot and NCCL_NTHREADS, or
-    LL128 with VCCL's default LL128 buffer and NCCL_LL128_NTHREADS (640)."""
+    """The ring's partition: SIMPLE with the comm's slot and NCCL_NTHREADS,
+    LL128 with VCCL's default LL128 buffer and NCCL_LL128_NTHREADS (640), or
+    LL (the one-hop LL reduce-scatter's per-channel fold) with NCCL_NTHREADS."""
     if proto == S.PROTO_LL128:
         return S.cbd_schedule(coll, count, esz, n, nch, proto=S.PROTO_LL128)
+    if proto == S.PROTO_LL:
+        return S.cbd_schedule(coll, count, esz, n, nch, proto=S.PROTO_LL, nthreads=nthreads)
     return S.cbd_schedule(coll, count, esz, n, nch, buff_size=slot_bytes * S.NCCL_STEPS,
                           nthreads=nthreads)
 
@@ -94,10 +97,7 @@ def _sched(coll, count, esz, n, nch, slot_bytes, nthreads, proto):
 _KERNEL_KEY = {0: 1, 1: 1, 2: 3, 3: 3, 4: 5, 5: 5}  # signed ints run the unsigned kernel
 
 
-def group_works(calls, n, nch, slot_bytes=512 << 10, nthreads=512):
-    """VCCL's group plan (oracle/vccl_sched.py plan_schedule) for a group's
-    ring / direct calls of one comm, in call order: calls = [(coll "ar" |
-    "rs" | "ag", op, dtype, count)]; returns every call's CbdWork."""
+def _group_calls(calls, n):
     gc = []
     for coll, op, dt, count in calls:
         esz = np.dtype(O.NP_DTYPE[dt]).itemsize
@@ -108,7 +108,62 @@ def group_works(calls, n, nch, slot_bytes=512 << 10, nthreads=512):
             key = (coll, dev_op, dt)
             func = (coll, dev_op, _KERNEL_KEY.get(dt, dt))
         gc.append(S.GroupCall(coll, count, esz, key, func))
-    return S.plan_schedule(gc, n, nch, buff_size=slot_bytes * S.NCCL_STEPS, nthreads=nthreads)[2]
+    return gc
+
+
+def group_works(calls, n, nch, slot_bytes=512 << 10, nthreads=512, algos=None):
+    """VCCL's group plan (oracle/vccl_sched.py plan_schedule) for a group's
+    calls of one comm, in call order: calls = [(coll "ar" | "rs" | "ag", op,
+    dtype, count)], algos = every call's path (group_algos; None = every call
+    "ring"); returns every call's CbdWork (under its path's protocol)."""
+    algo_of = None if algos is None else (lambda i, agg: algos[i])
+    return S.plan_schedule(_group_calls(calls, n), n, nch, buff_size=slot_bytes * S.NCCL_STEPS,
+                           nthreads=nthreads, algo_of=algo_of)[2]
+
+
+_COLL_CODE = {"ar": 0, "rs": 1, "ag": 2}
+
+
+def group_algos(calls, n, coll_algo):
+    """The path of every call of a group, as the library lays the group out:
+    each (func, op, type) aggregate of VCCL's ncclPrepareTasks (the oracle's
+    restatement) takes the path coll_algo(coll code, aggregate count, dtype)
+    — the comm's single-call selection (vcclCommCollAlgo) on the summed count
+    (all-gathers: bytes, as int8) — and every member takes it."""
+    out = []
+    def algo_of(i, agg):
+        coll, op, dt, count = calls[i]
+        return coll_algo(_COLL_CODE[coll], agg, 0 if coll == "ag" else dt)
+    S.plan_schedule(_group_calls(calls, n), n, 1, nthreads=512, algo_of=algo_of, algos_out=out)
+    return out
+
+
+def select_algo(policy, coll, esz, count, n):
+    """The library's path of one bucket (host/enqueue.cc select_algo) on an
+    explicit policy dict (vcclGroupPlanEx's policy fields); coll "ar" | "rs" |
+    "ag", count in elements of esz."""
+    if n < 2 or policy["force"] == 1:
+        return "ring"
+    if policy["force"] == 4:
+        return "ll128" if policy["ll128"] else "ring"
+    block = count * esz
+    nbytes = block if coll == "ar" else block * n
+    if coll == "ar":
+        ll_fits = policy["ll_slot"] > 0 and nbytes <= policy["ll_max"]
+        direct_fits = policy["direct"] and nbytes <= policy["direct_max"]
+    else:
+        ll_fits = (policy["ll_slot"] > 0 and n <= 8 and block <= policy["ll_slot"]
+                   and nbytes <= policy["ll_rsag_max"])
+        direct_fits = policy["direct"] and nbytes <= policy["direct_rsag_max"]
+    if policy["force"] == 2:
+        return "ll" if ll_fits else "ring"
+    if policy["force"] == 3:
+        return "direct" if policy["direct"] and n <= 8 else "ring"
+    if ll_fits:
+        return "ll"
+    if policy["ll128"] and policy["ll128_max"] and policy["ll128_min"] <= nbytes <= policy["ll128_max"]:
+        return "ll128"
+    return "direct" if direct_fits else "ring"
 
 
 def expected_allreduce(op, dtype, inputs, nch, slot_bytes, rings=None, nthreads=512,

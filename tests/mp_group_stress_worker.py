@@ -7,7 +7,8 @@ all-gathers of f32 / bf16 / i32 (sum, max) from 1 KiB to 6 MiB, issued on
 two streams in turn — so the group plan spans several (func, op, type) bins,
 aggregates, and launches of up to 16 parts with channels skipped per part.
 Saves every output and the path the library chose for each call
-(vcclCommCollAlgo) for the test's expectation; the group runs twice (outputs
+(its aggregate's, vcclCommCollAlgo on the summed count) for the test's
+expectation; the group runs twice (outputs
 NaN-filled before each) and the second run must equal the first bit for bit.
 """
 import os
@@ -21,6 +22,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from oracle import oracle as O  # noqa: E402
+from tests import _ring  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 COLLS = ("ar", "rs", "ag")
@@ -42,6 +44,11 @@ def stress_calls(n, k=36, seed=4242):
             count = max(1, count // n)
         out.append((f"s{i}_{coll}", coll, dt, op, count))
     return out
+
+
+def group_calls(calls):
+    """(coll, op, dtype, count) per call, as _ring.group_works takes them."""
+    return [(coll, op, dt, count) for _, coll, dt, op, count in calls]
 
 
 def gen(name, dt, total, rank):
@@ -68,13 +75,14 @@ def main():
     comm = nccl.Comm.init_rank(n, uid, rank)
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     calls = stress_calls(n)
-    bufs, algos = {}, []
+    bufs = {}
     for name, coll, dt, op, count in calls:
         x = gen(name, dt, in_count(coll, count, n), rank)
         xb = torch.from_numpy(x.view(np.uint8).copy()).cuda()
         yb = torch.empty(out_count(coll, count, n) * x.dtype.itemsize, dtype=torch.uint8, device="cuda")
         bufs[name] = (xb, yb, x.dtype)
-        algos.append(comm.coll_algo(COLLS.index(coll), count, dt))
+    # every call's path: its aggregate's (ncclPrepareTasks, _ring.group_algos)
+    algos = _ring.group_algos(group_calls(calls), n, comm.coll_algo)
     res = {}
     for rep in range(2):
         for xb, yb, _ in bufs.values():

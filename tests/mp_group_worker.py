@@ -19,6 +19,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from oracle import oracle as O  # noqa: E402
+from tests import _ring  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 GROUP_RS = [(f"rs{i}", 9, (8 << 20) // 2) for i in range(16)]        # (name, dtype, bucket elements)
@@ -30,6 +31,19 @@ GROUP_AR = [(f"ar{i}", 7, (2 << 20) // 4 + 37 * i) for i in range(8)]
 MIXED_RS = [("mrs0", 7, (48 << 20) // 4), ("mrs1", 7, (5 << 20) // 4), ("mrs2", 7, (48 << 20) // 4 + 4096)]
 MIXED_AR = [("mar0", 7, (1 << 20) // 4 + 70_000), ("mar1", 7, (4 << 20) // 4), ("mar2", 7, 300_001)]
 SETS = {"zero": (GROUP_RS, GROUP_AR, 1), "mixed": (MIXED_RS, MIXED_AR, 3)}
+
+
+def call_list(group_rs, group_ar, reps, n):
+    """The group's calls in call order, as _ring.group_works takes them:
+    interleaved RS / AR when reps > 1, else every RS then every AR."""
+    rs = [("rs", 0, dt, count // n) for _, dt, count in group_rs]
+    ar = [("ar", 0, dt, count) for _, dt, count in group_ar]
+    if reps == 1:
+        return rs + ar
+    out = []
+    for i in range(max(len(rs), len(ar))):
+        out += ([rs[i]] if i < len(rs) else []) + ([ar[i]] if i < len(ar) else [])
+    return out
 
 
 def gen(name, dt, count, rank):
@@ -53,8 +67,11 @@ def main():
         nout = count // n if (name, dt, count) in group_rs else count
         yb = torch.empty(nout * x.dtype.itemsize, dtype=torch.uint8, device="cuda")
         bufs[name] = (xb, yb, x.dtype)
-    algos = {"rs": comm.coll_algo(1, group_rs[0][2] // n, group_rs[0][1]),
-             "ar": comm.coll_algo(0, group_ar[0][2], group_ar[0][1])}
+    # every call's path: its aggregate's (ncclPrepareTasks, _ring.group_algos)
+    calls = call_list(group_rs, group_ar, reps, n)
+    group_algos = _ring.group_algos(calls, n, comm.coll_algo)
+    algos = {"rs": group_algos[[c[0] for c in calls].index("rs")],
+             "ar": group_algos[[c[0] for c in calls].index("ar")]}
     torch.cuda.synchronize()
     res, fused = {}, 0
     for rep in range(reps):
@@ -90,6 +107,7 @@ def main():
     res["fused"] = np.array(fused)
     res["algo_rs"] = np.array(algos["rs"])
     res["algo_ar"] = np.array(algos["ar"])
+    res["group_algos"] = np.array(group_algos)
     err = comm.async_error()
     comm.destroy()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)

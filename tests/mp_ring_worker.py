@@ -57,6 +57,8 @@ def main():
         streams.append(torch.cuda.Stream())
     g = RC.run_group([(comm, streams)], [rank], nranks)[0]
     res.update(g)
+    # every call's path in the group: its aggregate's (RC.group_algos)
+    res["group_algos"] = np.array(RC.group_algos(comm.coll_algo, nranks))
     before = comm.launch_stats()
     res["launch_stats"] = np.array(before, dtype=np.int64)
     res["net_stats"] = np.array(comm.net_stats(), dtype=np.int64)

@@ -148,43 +148,46 @@ def gen_group_input(gi, rank):
     return rng.uniform(-1, 1, count).astype(O.NP_DTYPE[dt])
 
 
-def group_plan_works(n_ranks, nch, slot_bytes, ll_max=0, nthreads=512, proto=2):
-    """{group index: CbdWork} of the GROUP_CASES calls the library plans as
-    one VCCL group plan (host/enqueue.cc launch_planned): every call on the
-    SIMPLE ring or the direct path, i.e. above the LL threshold; the LL128
-    ring (proto 1) plans its calls one by one."""
-    if proto != 2:
-        return {}
-    idx = [gi for gi, (name, op, dt, count) in enumerate(GROUP_CASES)
-           if count * np.dtype(O.NP_DTYPE[dt]).itemsize > ll_max]
-    if not idx:
-        return {}
-    works = _ring.group_works([("ar", GROUP_CASES[gi][1], GROUP_CASES[gi][2], GROUP_CASES[gi][3])
-                               for gi in idx], n_ranks, nch, slot_bytes, nthreads)
-    return dict(zip(idx, works))
+GROUP_CALLS = [("ar", op, dt, count) for name, op, dt, count in GROUP_CASES]
 
 
-def expected_group(gi, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
-                   nthreads=512, proto=2, plan=None, chain=None):
-    """`plan`: group_plan_works(...) of the group (VCCL's grouped partition)."""
+def group_algos(coll_algo, n_ranks):
+    """Every GROUP_CASES call's path as the comm lays the group out (the path
+    of its 4x aggregate, _ring.group_algos; coll_algo = Comm.coll_algo)."""
+    return _ring.group_algos(GROUP_CALLS, n_ranks, coll_algo)
+
+
+def group_plan_works(n_ranks, nch, slot_bytes, nthreads=512, algos=None):
+    """[CbdWork per GROUP_CASES call]: the group's VCCL plan
+    (host/enqueue.cc launch_planned) with every call on its aggregate's path
+    (`algos`, group_algos; None = every call RING / SIMPLE)."""
+    return _ring.group_works(GROUP_CALLS, n_ranks, nch, slot_bytes, nthreads, algos=algos)
+
+
+def expected_group(gi, n_ranks, nch, slot_bytes, nthreads=512, plan=None, algos=None, chain=None):
+    """`plan`: group_plan_works(...) of the group (VCCL's grouped partition),
+    `algos`: the calls' paths (LL: the chain fold; ring / LL128 ring / direct:
+    the ring's fold on the call's place in the plan)."""
     name, op, dt, count = GROUP_CASES[gi]
     ins = [gen_group_input(gi, r) for r in range(n_ranks)]
-    return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                       nthreads, proto, work=(plan or {}).get(gi), chain=chain)
+    path = "ll" if algos[gi] == "ll" else "ring"
+    return expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, 0, 0, 0, nthreads, plan[gi].proto,
+                       work=plan[gi], chain=chain, path=path)
 
 
 def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direct_chunk,
-                nthreads=512, proto=2, work=None, chain=None):
+                nthreads=512, proto=2, work=None, chain=None, path=None):
     """All-reduce result: LL chain fold up to ll_max bytes, the ring's
     owner-map fold (VCCL's ring schedule on these channels) above — for the
     two-shot direct path too, which folds every element in the ring's order
     (direct.hpp phase 2), so neither direct_max nor the inbox chunk
     (direct_chunk) changes the expected bits.  `work`: the call's place in
     its group's plan; `chain`: the LL fold chain, root first (VCCL_LL_CHAIN;
-    None = the identity)."""
+    None = the identity); `path`: "ll" | "ring" when known (a grouped call
+    takes its aggregate's path), else from ll_max."""
     del direct_max, direct_chunk
     count = len(ins[0])
-    if count * ins[0].dtype.itemsize <= ll_max:
+    if path == "ll" or (path is None and count * ins[0].dtype.itemsize <= ll_max):
         dev_op, arg = O.host_to_dev_redop(op, dt, n_ranks)
         order = chain if chain is not None else range(n_ranks)
         return O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, [ins[r] for r in order])
@@ -206,7 +209,12 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
                         nthreads, proto, chain=chain)
         return [e] * n_ranks
     if coll == "rs":
-        return _ring.expected_reducescatter(op, dt, ins, nch, nthreads=nthreads, proto=proto)
+        # the one-hop LL reduce-scatter (one rank's block within the LL
+        # threshold, n <= 8; n x the threshold is the RS / AG default) folds
+        # per channel of VCCL's LL ring partition
+        ll = n_ranks <= 8 and count * ins[0].dtype.itemsize <= ll_max
+        return _ring.expected_reducescatter(op, dt, ins, nch, nthreads=nthreads,
+                                            proto=_ring.S.PROTO_LL if ll else proto)
     full = np.concatenate(ins)
     return [full] * n_ranks
 

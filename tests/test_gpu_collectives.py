@@ -40,6 +40,10 @@ TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": 
              "VCCL_LL_MAX_BLOCKS": "32", "VCCL_DIRECT_THRESHOLD": str(4 << 20),
              "VCCL_DIRECT_MAX_BLOCKS": "16", "VCCL_DIRECT_CHUNK_BYTES": str(1 << 20),
              "VCCL_DIRECT_RSAG_THRESHOLD": str(64 << 20)}
+# the group tests' direct thresholds: a group's aggregate takes the path of
+# its summed size, so the ZeRO loop's 128 MiB of reduce-scatters and 16 MiB
+# of all-reduces need raised thresholds to stay on the direct path
+GROUP_DIRECT = {"VCCL_DIRECT_THRESHOLD": str(32 << 20), "VCCL_DIRECT_RSAG_THRESHOLD": str(256 << 20)}
 LL_DEFAULT = 1 << 20
 DIRECT_TEST = 4 << 20
 DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in chunks
@@ -251,8 +255,8 @@ def test_multi_process_ranks(n, geom):
         for ci, case in enumerate(RC.CASES):
             _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk,
                    nthreads, proto, chain)
-        _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot, ll_max,
-                     direct_max, chunk, nthreads, proto, chain)
+        _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot,
+                     [str(a) for a in res[0]["group_algos"]], nthreads, chain)
         # every geometry fuses the group's runs (LL, direct or ring batches)
         fused = int(res[0]["launch_stats"][1])
         assert fused > 0, f"fused group launches: {fused}"
@@ -295,17 +299,16 @@ def test_beyond_2gib_two_ranks():
     assert codes == [0] * n, f"worker exit codes {codes}\n" + "\n".join(logs)
 
 
-def _check_group(n, outs, nch, slot, ll_max, direct_max, chunk, nthreads=512, proto=2, chain=None):
+def _check_group(n, outs, nch, slot, algos, nthreads=512, chain=None):
     """Bit-exact against VCCL's GROUPED schedule on our rings and channels:
-    the calls on the ring / direct paths take their place in VCCL's
-    multi-task plan (oracle plan_schedule); fp sum / prod also
-    within the §8c tolerance of the exact value and of VCCL's grouped result
-    on its reference geometry."""
-    plan = RC.group_plan_works(n, nch, slot, ll_max, nthreads, proto)
+    every call takes its aggregate's path (`algos`, RC.group_algos) and its
+    place in VCCL's multi-task plan (oracle plan_schedule);
+    fp sum / prod also within the §8c tolerance of the exact value and of
+    VCCL's grouped result on its reference geometry."""
+    plan = RC.group_plan_works(n, nch, slot, nthreads, algos)
     vplan = RC.group_plan_works(n, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT)
     for gi, (name, op, dt, count) in enumerate(RC.GROUP_CASES):
-        exp = RC.expected_group(gi, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto, plan=plan,
-                                chain=chain)
+        exp = RC.expected_group(gi, n, nch, slot, nthreads, plan=plan, algos=algos, chain=chain)
         for r in range(n):
             assert_bitexact(dt, outs[r][name], exp, minmax=op in (2, 3),
                             what=f"group {name} n={n} rank {r}")
@@ -332,7 +335,8 @@ def test_group_fusion_single_process(monkeypatch):
         outs = RC.run_group(list(zip(comms, streams)), [0, 1], 2)
         for c in comms:
             assert c.async_error() == 0
-        _check_group(2, [outs[0], outs[1]], nch, slot, LL_DEFAULT, DIRECT_TEST, DIRECT_CHUNK_TEST)
+        algos = RC.group_algos(comms[0].coll_algo, 2)
+        _check_group(2, [outs[0], outs[1]], nch, slot, algos)
         n_coll, fused = comms[0].launch_stats()
         # GROUP_CASES: [f32 x3] [f16 x2] big [f32] [bf16 x2] [i32] [u8] [f32 min x20 -> 16 + 4]
         assert fused == 5, fused
@@ -429,10 +433,12 @@ def test_initall_single_process_worker():
 def test_group_zero_pattern(n, geom):
     """a group of 16 x 8 MiB bf16 reduce-scatters (a ZeRO
     bucket loop) launches ONCE, and a group of 8 mid-size fp32 all-reduces
-    once (vcclCommLaunchStats), each on the path the library picks for it —
-    the ring at 2 ranks and with NCCL_ALGO=Ring, the one-hop / two-shot
-    direct path at 4 ranks — and every output is bit-exact against the
-    oracle's fold in VCCL's ring order (tests/mp_group_worker.py)."""
+    once (vcclCommLaunchStats), each aggregate on the path the library picks
+    for its summed size (128 MiB of RS, 16 MiB of AR) — the ring at 2 ranks
+    and with NCCL_ALGO=Ring, the one-hop / two-shot direct path at 4 ranks
+    with the direct thresholds raised to cover the aggregates — and every
+    output is bit-exact against the oracle's fold in VCCL's grouped order
+    (tests/mp_group_worker.py)."""
     from tests import mp_group_worker as G
     uid = nccl.get_unique_id()
     hexid = nccl.unique_id_to_bytes(uid).hex()
@@ -440,6 +446,7 @@ def test_group_zero_pattern(n, geom):
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
     if geom in ("test", "ring_only"):
         env.update(TEST_GEOM)
+        env.update(GROUP_DIRECT)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
         if geom == "ring_only":
             env["NCCL_ALGO"] = "Ring"
@@ -461,9 +468,10 @@ def test_group_zero_pattern(n, geom):
     # VCCL's grouped plan of the 24 calls: bit-exact on our
     # rings and channels, within tolerance of VCCL's grouped result on its
     # reference geometry
-    calls = [("rs", 0, dt, count // n) for _, dt, count in G.GROUP_RS] + \
-            [("ar", 0, dt, count) for _, dt, count in G.GROUP_AR]
-    works = _ring.group_works(calls, n, nch, slot)
+    calls = G.call_list(G.GROUP_RS, G.GROUP_AR, 1, n)
+    algos = [str(a) for a in res[0]["group_algos"]]
+    assert len(set(algos[:16])) == 1 and len(set(algos[16:])) == 1, algos  # one aggregate each
+    works = _ring.group_works(calls, n, nch, slot, algos=algos)
     vworks = _ring.group_works(calls, n, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT)
     ident = [list(range(n))]
     for i, (name, dt, count) in enumerate(G.GROUP_RS):
@@ -491,12 +499,13 @@ def test_group_zero_pattern(n, geom):
 
 def test_group_mixed_direct_sizes():
     """a fused direct launch whose parts differ in size —
-    reduce-scatters of 5 MiB and 48 MiB buckets and all-reduces of 1.1 MiB
-    and 4 MiB, interleaved in one group, 4 ranks, direct path (test
-    geometry) — must not let one part's scatter overwrite inbox bytes a
-    peer's other workgroup still folds: every part of a batch uses one block
-    length.  The group runs 3 times (outputs NaN-filled before each) and
-    every run is bit-exact against VCCL's grouped plan."""
+    reduce-scatters of 5 MiB and 48 MiB buckets (two aggregates, both direct
+    under the raised thresholds, one run) and all-reduces of 1.1 MiB and
+    4 MiB, interleaved in one group, 4 ranks — must not let one part's
+    scatter overwrite inbox bytes a peer's other workgroup still folds: every
+    part of a batch uses one block length.  The group runs 3 times (outputs
+    NaN-filled before each) and every run is bit-exact against VCCL's
+    grouped plan."""
     from tests import mp_group_worker as G
     n = 4
     uid = nccl.get_unique_id()
@@ -504,6 +513,7 @@ def test_group_mixed_direct_sizes():
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
     env.update(TEST_GEOM)
+    env.update(GROUP_DIRECT)
     nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_group_worker.py"),
@@ -516,13 +526,10 @@ def test_group_mixed_direct_sizes():
     assert int(res[0]["fused"]) == 2, int(res[0]["fused"])
     for r in range(n):
         assert not [k for k in res[r] if k.endswith("_differs")], (r, [k for k in res[r] if k.endswith("_differs")])
-    calls = []
-    for i in range(max(len(G.MIXED_RS), len(G.MIXED_AR))):
-        if i < len(G.MIXED_RS):
-            calls.append(("rs", 0, G.MIXED_RS[i][1], G.MIXED_RS[i][2] // n))
-        if i < len(G.MIXED_AR):
-            calls.append(("ar", 0, G.MIXED_AR[i][1], G.MIXED_AR[i][2]))
-    works = iter(_ring.group_works(calls, n, nch, slot))
+    calls = G.call_list(G.MIXED_RS, G.MIXED_AR, 3, n)
+    algos = [str(a) for a in res[0]["group_algos"]]
+    assert set(algos) == {"direct"}, algos
+    works = iter(_ring.group_works(calls, n, nch, slot, algos=algos))
     for i in range(max(len(G.MIXED_RS), len(G.MIXED_AR))):
         for lst, coll in ((G.MIXED_RS, "rs"), (G.MIXED_AR, "ar")):
             if i >= len(lst):
@@ -545,9 +552,11 @@ def test_group_plan_stress(geom):
     """36 calls in one group (AR / RS / AG of f32 / bf16 / i32, sum and max,
     1 KiB - 6 MiB, two streams) at 4 ranks: several (func, op, type) bins,
     aggregates and batches of up to 16 parts with channels skipped per part.
-    Every output bit-exact: ring / direct calls against VCCL's grouped plan
-    (the path of each call read back with vcclCommCollAlgo), LL calls against
-    their own fold; a second run of the group is bitwise identical."""
+    Every call on its aggregate's path (vcclCommCollAlgo on the aggregate's
+    summed count) and its place in VCCL's grouped plan, LL calls included;
+    every output bit-exact (ring / direct: the ring fold on that place; LL
+    all-reduce: the chain fold; LL reduce-scatter: per channel of its LL
+    place); a second run of the group is bitwise identical."""
     from oracle import oracle as O
     from tests import mp_group_stress_worker as G
     n = 4
@@ -575,15 +584,13 @@ def test_group_plan_stress(geom):
         assert len(set(algos)) >= 2, algos  # the plan spans paths
     for r in range(n):
         assert not [k for k in res[r] if k.endswith("_differs")], r
-    planned = [i for i, a in enumerate(algos) if a in ("ring", "direct")]
-    works = dict(zip(planned, _ring.group_works([(calls[i][1], calls[i][3], calls[i][2], calls[i][4])
-                                                 for i in planned], n, nch, slot)))
+    works = _ring.group_works(G.group_calls(calls), n, nch, slot, algos=algos)
     for i, (name, coll, dt, op, count) in enumerate(calls):
         ins = [G.gen(name, dt, G.in_count(coll, count, n), r) for r in range(n)]
         if coll == "ag":
             exp = [np.concatenate(ins)] * n
         elif coll == "rs":
-            exp = _ring.expected_reducescatter(op, dt, ins, nch, slot, work=works.get(i))
+            exp = _ring.expected_reducescatter(op, dt, ins, nch, slot, work=works[i])
         elif algos[i] == "ll":
             dev_op, arg = O.host_to_dev_redop(op, dt, n)
             exp = [O.chain_fold(dev_op, dt, arg, dev_op == O.DEV_PREMULSUM, ins)] * n

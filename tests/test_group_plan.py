@@ -9,6 +9,11 @@
   currentTraffic);
 * a group too large for one kernel's argument budget splits into plans whose
   channel assignment restarts at channel 0 (enqueue.cc:535, :636);
+* the path per aggregate (vcclGroupPlanEx): every member of a 4x aggregate
+  takes the path of the summed count (enqueue.cc:387-427), an LL member's
+  traffic counts 4x (:418, :599) and LL calls move the channel cursor the
+  ring calls after them start from — library == oracle over random groups
+  and random path policies, plus hand-derived cases;
 * NCCL_ALGO / NCCL_PROTO list parsing (vcclAlgoSelection, graph/tuning.cc:
   53-116 parseList semantics).
 """
@@ -16,6 +21,7 @@ import numpy as np
 import pytest
 
 from oracle import vccl_sched as S
+from tests import _ring
 from vccl_amd import nccl
 
 COLL = {0: "ar", 1: "rs", 2: "ag"}
@@ -181,3 +187,119 @@ def test_algo_selection():
         with pytest.raises(nccl.VcclError) as e:
             nccl.algo_selection(algo, proto)
         assert e.value.code == nccl.ncclInvalidUsage
+
+
+def _random_policy(rng, n):
+    ll_max = int(rng.choice([0, 64 << 10, 128 << 10, 1 << 20]))
+    return dict(force=int(rng.choice([0, 0, 0, 0, 1, 2, 3, 4])),
+                ll_slot=int(rng.choice([0, 1 << 20, 1 << 20, 2 << 20])),
+                ll_max=ll_max, ll_rsag_max=int(rng.choice([n * ll_max, 0, 1 << 20])),
+                ll128=int(rng.integers(0, 2)), ll128_min=64 << 10,
+                ll128_max=int(rng.choice([0, 1 << 20, 8 << 20])),
+                direct=int(rng.integers(0, 2)), direct_max=int(rng.choice([0, 4 << 20, 8 << 20])),
+                direct_rsag_max=int(rng.choice([0, 8 << 20, 64 << 20])))
+
+
+def _check_equal_ex(calls, n, nch, policy, slot=512 << 10, nthreads=512):
+    """vcclGroupPlanEx == the oracle's plan with the same path per aggregate
+    (_ring.select_algo on the aggregate's count)."""
+    algos, order, plan_of, parts = nccl.group_plan_ex(calls, n, nch, policy, slot, nthreads)
+
+    def algo_of(i, agg):
+        coll, _, dt, _ = calls[i]
+        return _ring.select_algo(policy, COLL[coll], 1 if coll == 2 else ESZ[dt], agg, n)
+    o_algos = []
+    o_order, o_plan, o_works = S.plan_schedule(_oracle_calls(calls, n), n, nch, buff_size=slot * S.NCCL_STEPS,
+                                               nthreads=nthreads, algo_of=algo_of, algos_out=o_algos)
+    assert algos == o_algos, (calls, policy, algos, o_algos)
+    assert order == o_order and plan_of == o_plan, (calls, policy)
+    for i, (lib, w) in enumerate(zip(parts, o_works)):
+        ref = _as_tuple(w)
+        assert lib[:5] == ref[:5], (i, calls[i], algos[i], lib, ref)
+        for k, cnt in ((5, w.count_lo), (6, w.count_mid), (7, w.count_hi)):
+            if cnt:
+                assert lib[k] == ref[k], (i, calls[i], algos[i], k)
+    return algos, order, plan_of, parts
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_library_group_plan_ex_equals_oracle(n):
+    rng = np.random.default_rng(900 + n)
+    for trial in range(60):
+        k = int(rng.integers(1, 21))
+        calls = []
+        for _ in range(k):
+            coll = int(rng.integers(0, 3))
+            dt = int(rng.choice([7, 9, 6, 2, 0, 8]))
+            op = int(rng.choice([0, 1, 2, 3]))
+            count = int(rng.choice([1, 100, 4096, 16384, 40_000, 65_536, 300_000, 1 << 20, 3 << 20])) \
+                + int(rng.integers(0, 64))
+            calls.append((coll, count, dt, op))
+        nch = int(rng.choice([1, 2, 14, 16, 32, 56, 63, 64]))
+        _check_equal_ex(calls, n, nch, _random_policy(rng, n), nthreads=int(rng.choice([256, 512])))
+
+
+def test_group_plan_ex_without_policy_is_group_plan():
+    calls = [(0, 1 << 20, 7, 0), (1, 12_345, 9, 0), (2, 4096, 6, 0), (0, 3, 7, 2)]
+    algos, order, plan_of, parts = nccl.group_plan_ex(calls, 4, 56, None)
+    assert algos == ["ring"] * 4
+    assert (order, plan_of, parts) == nccl.group_plan(calls, 4, 56)
+
+
+DEFAULTS_8 = dict(force=0, ll_slot=1 << 20, ll_max=128 << 10, ll_rsag_max=8 * (128 << 10), ll128=0,
+                  ll128_min=64 << 10, ll128_max=0, direct=0, direct_max=0, direct_rsag_max=0)
+
+
+def test_hand_derived_ll_call_moves_the_cursor():
+    """A 64 KiB fp32 all-reduce (LL: VCCL's tree LL) planned with three 8 MiB
+    ones (ring) at 8 ranks on 56 channels, worked through enqueue.cc:387-427,
+    :549-681 by hand.  LL trafficBytes = 64 KiB x 2 x 4 = 512 KiB; nMaxChannels
+    LL (tree: threshold 8, 512 threads): 16; ring: 56.  trafficPerChannel =
+    (512 KiB + 3 x 16 MiB) / 56 = 908,141 B.  The LL call (first: its bin is
+    size-ascending) at (ch 0, 0): cells of 2 KiB (16 KiB traffic each, x4),
+    32 cells, all on ch 0 (lo = min(32, divUp(908,141, 16,384))), cursor (0,
+    524,288).  Ring call 1 at (0, 524,288): 8 KiB cells, 1024 cells,
+    cellsPerChannel 56, lo = divUp(908,141 - 524,288, 16,384) = 24, 17 mid,
+    hi 48 -> ch 0..18."""
+    calls = [(0, 16384, 7, 0)] + [(0, 2 << 20, 7, 0)] * 3
+    algos, order, plan_of, parts = _check_equal_ex(calls, 8, 56, DEFAULTS_8)
+    assert algos == ["ll", "ring", "ring", "ring"] and order == [0, 1, 2, 3]
+    assert parts[0][:5] == (0, 0, 16384, 0, 0)
+    assert parts[1][:5] == (0, 18, 24 * 2048, 56 * 2048, 48 * 2048)
+    # planned as a SIMPLE ring call the small bucket would leave call 1 on
+    # another partition: the LL protocol's 4x traffic is what moves it
+    _, _, _, ring_parts = nccl.group_plan_ex(calls, 8, 56, None)
+    assert ring_parts[1][:5] != parts[1][:5]
+
+
+def test_aggregate_takes_one_path():
+    """Two fp32 all-reduces of 48 KiB and 100 KiB at 8 ranks: each alone is
+    on the LL path (<= 128 KiB), but the second is within 4x of the first, so
+    they aggregate and the 148 KiB aggregate takes the ring — for both
+    (enqueue.cc:392-424: getAlgoInfo on the aggregate, its choice given to
+    every member).  A third call 4x larger starts its own aggregate (ring by
+    its own size); 16 KiB and 64 KiB calls stay apart and both on LL."""
+    calls = [(0, 12 * 1024, 7, 0), (0, 25 * 1024, 7, 0), (0, 100 * 1024, 7, 0)]
+    for coll, count, dt, _ in calls[:2]:
+        assert _ring.select_algo(DEFAULTS_8, "ar", 4, count, 8) == "ll"
+    algos, order, _, _ = _check_equal_ex(calls, 8, 56, DEFAULTS_8)
+    assert algos == ["ring", "ring", "ring"], algos
+    calls = [(0, 4096, 7, 0), (0, 16384, 7, 0)]  # 64 KiB is not < 4 x 16 KiB: two aggregates
+    algos, _, _, _ = _check_equal_ex(calls, 8, 56, DEFAULTS_8)
+    assert algos == ["ll", "ll"], algos
+
+
+def test_single_call_ll_partition():
+    """The one-hop LL reduce-scatter folds per channel of VCCL's LL ring
+    partition (LL cells: traffic x4; LL threshold x nRanks): library ==
+    oracle (vcclRingPartition with proto 0)."""
+    for n in (2, 4, 8):
+        for nch in (1, 14, 56):
+            for count, dt in ((1000, 7), (20_001, 9), (65_537, 7), (1_003, 0), (30_001, 6)):
+                for nt in (256, 512):
+                    lib = nccl.ring_partition(1, count, dt, n, nch, 8 * 512 * 16, nt, proto=0)
+                    w = S.cbd_schedule("rs", count, ESZ[dt], n, nch, proto=S.PROTO_LL, nthreads=nt)
+                    ref = _as_tuple(w)
+                    assert lib[:5] == ref[:5], (n, nch, count, dt, nt, lib, ref)
+                    assert lib[5] == ref[5] == 32768 // ESZ[dt]  # half a VCCL LL step
+

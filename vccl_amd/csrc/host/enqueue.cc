@@ -4,13 +4,15 @@
 // (collectives.cc:77-158 -> ncclEnqueueCheck enqueue.cc:2448-2525 -> ArgsCheck
 // misc/argcheck.cc:45-86 -> taskAppend enqueue.cc:2315-2442 with
 // hostToDevRedOp :2217-2310 and the nRanks==1 shortcut ncclLaunchOneRank
-// onerank.cu:47-83), re-implemented for one node: the planner picks one of
-// three algorithms per call (choose_algo: one-shot LL, two-shot direct, SIMPLE
+// onerank.cu:47-83), re-implemented for one node: the planner picks a path
+// per call (select_algo: one-shot LL, LL128 ring, two-shot direct, SIMPLE
 // ring over xGMI); the ring's channel partition is VCCL's own cbd split
-// (cbd_schedule below, ring.hpp cbd_part).  Group semantics (group.cc:92-110, :393-506): calls
-// between ncclGroupStart/End are queued per thread and launched at the
-// outermost ncclGroupEnd in call order, runs of small all-reduces fused into
-// one LL launch (launch_group).
+// (cbd_schedule below, ring.hpp cbd_part).  Group semantics (group.cc:92-110,
+// :393-506): calls between ncclGroupStart/End are queued per thread and, at
+// the outermost ncclGroupEnd, each comm's calls are laid out on VCCL's
+// multi-task plan (group_plan: aggregation, a path per aggregate, the shared
+// channel cursor) and launched in plan order, runs of one path fused into
+// one launch (launch_group).
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -47,11 +49,15 @@ struct Task {
   const void* argPtr;  // ncclScalarDevice PreMulSum scalar
   ncclComm* comm;
   hipStream_t stream;
-  // Set by the group planner (plan_group): this call's partition inside its
-  // group's VCCL plan; otherwise the call is planned alone (cbd_schedule).
+  // Set by the group planner (launch_planned): this call's partition inside
+  // its group's VCCL plan, under the protocol of the path its aggregate took;
+  // otherwise the call is planned alone (cbd_schedule).
   bool planned;
   CbdPlan plan;
 };
+
+// The paths a call can take (choose_algo / select_algo below).
+enum { kAlgoRing = 0, kAlgoLL = 1, kAlgoDirect = 2, kAlgoRingLL128 = 3 };
 
 static thread_local int tl_groupDepth = 0;
 static thread_local std::vector<Task> tl_tasks;
@@ -348,12 +354,16 @@ static int64_t traffic_per_byte(int coll, int nRanks) {  // ncclFuncTrafficPerBy
 }
 
 // nMaxChannels of a task (or of an aggregate of tasks, ncclPrepareTasks):
-// the ring channel tuning on nBytes = eltSize * ncclFuncMaxSendRecvCount
-// (enqueue.cc:1955, 1921-1924); thread thresholds (comm.h:38-40) SIMPLE 64,
-// LL128 8.
+// the ring / tree channel tuning on nBytes = eltSize * ncclFuncMaxSendRecvCount
+// (enqueue.cc:1955, 1921-1924); thread thresholds (comm.h:38-40,
+// tuning.cc:489-493) SIMPLE 64, LL128 8, LL 8 — times nRanks for the ring's
+// LL (reduce-scatter / all-gather), not for the all-reduce's LL, which VCCL
+// runs on its tree.  nThreads: maxThreads of the protocol (tuning.cc:198-211:
+// NCCL_NTHREADS for SIMPLE and LL, NCCL_LL128_NTHREADS for LL128).
 static int ring_nmax_channels(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
                               int proto, int64_t nThreads) {
-  const int64_t threshold = proto == kProtoLL128 ? 8 : 64;
+  const int64_t threshold = proto == kProtoSimple ? 64
+                            : proto == kProtoLL128 || coll == kAllReduce ? 8 : 8 * (int64_t)nRanks;
   const int64_t nBytes = eltSize * (coll == kAllReduce ? count : (int64_t)nRanks * count);
   int64_t nc = commChannels;
   while (nBytes < nc * nThreads * threshold && nc >= 2) nc--;
@@ -369,12 +379,17 @@ struct PlanCursor {
   int nMax;  // nMaxChannels[kind] = comm->nChannels
 };
 
-// The cbd cell split of one task at the cursor (enqueue.cc:597-644), then
-// the cursor advanced past it (:667-681).  Returns the task's channel count.
+// VCCL's LL step (the default LL buffer, init.cc:617: 8 lines x 512 threads
+// x NCCL_STEPS x 16 B, over NCCL_STEPS): only the chunk fields of an LL
+// task's plan use it, and the one-hop LL kernels ignore those.
+constexpr int64_t kLLStepBytes = 8 * 512 * 16;
+
+// The cbd cell split of one task at the cursor (enqueue.cc:597-644; LL
+// counts its traffic 4x, :599), then the cursor advanced past it (:667-681).
 static CbdPlan cbd_place(PlanCursor& pc, int coll, int64_t count, int64_t eltSize, int nRanks,
                          int proto, int64_t stepBytes) {
-  const bool ll128 = proto == kProtoLL128;
-  const uint64_t tpb = (uint64_t)traffic_per_byte(coll, nRanks);
+  const bool ll128 = proto == kProtoLL128, ll = proto == kProtoLL;
+  const uint64_t tpb = (uint64_t)traffic_per_byte(coll, nRanks) * (ll ? 4 : 1);
   const uint64_t cellSize = (uint64_t)div_up(div_up(kMinTraffic, tpb), 16) * 16;
   const uint64_t eltsPerCell = cellSize / (uint64_t)eltSize;
   const uint64_t cells = (uint64_t)div_up(count * eltSize, (int64_t)cellSize);
@@ -417,10 +432,11 @@ static CbdPlan cbd_place(PlanCursor& pc, int coll, int64_t count, int64_t eltSiz
   p.channelHi = pc.channelId + nCh - 1;
   // RING chunk (calcCollChunking, enqueue.cc:2027-2032, 2093): SIMPLE =
   // chunkSteps (4) FIFO steps of buffSize / NCCL_STEPS (= one slot here);
-  // LL128 = one step, 15/16 of it data; rounded down to the protocol grain
-  // (device.h:290-295: SIMPLE 512, LL128 1920); independent of size.
-  const int64_t grain = ll128 ? 1920 : 512;
-  const int64_t chunkBytes = ll128 ? stepBytes / 16 * 15 : 4 * stepBytes;
+  // LL128 = one step, 15/16 of it data; LL = half a step; rounded down to
+  // the protocol grain (device.h:290-295: SIMPLE 512, LL128 1920, LL 16);
+  // independent of size.
+  const int64_t grain = ll128 ? 1920 : ll ? 16 : 512;
+  const int64_t chunkBytes = ll128 ? stepBytes / 16 * 15 : ll ? stepBytes / 2 : 4 * stepBytes;
   const int64_t chunkElts = chunkBytes / grain * grain / eltSize;
   p.chunkLo = p.chunkMid = p.chunkHi = chunkElts;
   // advance the cursor (enqueue.cc:667-681)
@@ -444,16 +460,84 @@ static CbdPlan cbd_place(PlanCursor& pc, int coll, int64_t count, int64_t eltSiz
 static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks, int commChannels,
                             int proto, int64_t stepBytes, int64_t nThreads) {
   const int nc = ring_nmax_channels(coll, count, eltSize, nRanks, commChannels, proto, nThreads);
-  const uint64_t traffic = std::max<uint64_t>(kMinTraffic, (uint64_t)(count * eltSize) * traffic_per_byte(coll, nRanks));
+  const uint64_t traffic = std::max<uint64_t>(
+      kMinTraffic, (uint64_t)(count * eltSize) * traffic_per_byte(coll, nRanks) * (proto == kProtoLL ? 4 : 1));
   PlanCursor pc{std::max<uint64_t>(kMinTraffic, traffic / (uint64_t)std::min(nc, commChannels)), 0, 0,
                 commChannels};
   return cbd_place(pc, coll, count, eltSize, nRanks, proto, stepBytes);
 }
 
+// ---------------------------------------------------------------- paths
+// The path of a bucket (VCCL's topoGetAlgoInfo, enqueue.cc:1805-1945, reduced
+// to one node over a full xGMI mesh): buckets up to the LL threshold take the
+// one-hop LL path, the LL128 window (when enabled) the LL128 ring, up to the
+// direct threshold the direct path (all-reduce two-shot, reduce-scatter /
+// all-gather one-hop), larger ones the SIMPLE ring.  NCCL_ALGO / NCCL_PROTO
+// force one: Ring/SIMPLE -> ring; Tree/LL -> LL where it fits; Direct -> direct
+// where the mesh has it; LL128 -> the LL128 ring where its FIFOs exist;
+// anything that does not fit falls through to the ring.  A pure function of
+// the comm's thresholds (AlgoPolicy), so the group planner can ask it for an
+// aggregate of calls as ncclPrepareTasks asks getAlgoInfo (enqueue.cc:398).
+struct AlgoPolicy {
+  int nRanks = 1, algoForce = 0;
+  int64_t llSlotBytes = 0;                 // 0: no LL buffers
+  uint64_t llMax = 0, llRsAgMax = 0;
+  bool ll128 = false;                      // LL128 FIFOs mapped
+  uint64_t ll128Min = 0, ll128Max = 0;     // automatic LL128 window (max 0 = off)
+  bool direct = false;                     // every peer's inbox mapped
+  uint64_t directMax = 0, directRsAgMax = 0;
+};
+static AlgoPolicy policy_of(const ncclComm* c) {
+  AlgoPolicy p;
+  p.nRanks = c->nRanks;
+  p.algoForce = c->algoForce;
+  p.llSlotBytes = c->llBuf ? (int64_t)c->llLines * 8 : 0;
+  p.llMax = c->llMaxBytes;
+  p.llRsAgMax = c->llRsAgMaxBytes;
+  p.ll128 = c->ll128Buf != nullptr;
+  p.ll128Min = c->ll128MinBytes;
+  p.ll128Max = c->ll128MaxBytes;
+  p.direct = c->dPeers != nullptr;
+  p.directMax = c->directMaxBytes;
+  p.directRsAgMax = c->directRsAgMaxBytes;
+  return p;
+}
+// count in elements of eltSize (all-gather: any element type, or bytes)
+static int select_algo(const AlgoPolicy& p, int coll, int64_t eltSize, int64_t count) {
+  if (p.nRanks < 2 || p.algoForce == 1) return kAlgoRing;
+  // NCCL_PROTO=LL128 (or vcclCommSetAlgo): the LL128 ring for every size
+  if (p.algoForce == 4) return p.ll128 ? kAlgoRingLL128 : kAlgoRing;
+  const uint64_t block = (uint64_t)(count * eltSize);
+  // Reduce-scatter / all-gather: one rank's block must fit an LL slot; the
+  // thresholds are on the whole bucket (n blocks), as the reference's tuner
+  // sizes RS / AG (enqueue.cc:1955, ncclFuncMaxSendRecvCount).
+  const uint64_t bytes = coll == kAllReduce ? block : block * (uint64_t)p.nRanks;
+  const bool llFits = coll == kAllReduce
+                          ? p.llSlotBytes > 0 && bytes <= p.llMax
+                          : p.llSlotBytes > 0 && p.nRanks <= kOrderMaxRanks &&
+                                block <= (uint64_t)p.llSlotBytes && bytes <= p.llRsAgMax;
+  const bool directFits = p.direct && bytes <= (coll == kAllReduce ? p.directMax : p.directRsAgMax);
+  if (p.algoForce == 2) return llFits ? kAlgoLL : kAlgoRing;
+  // Forced direct: any bucket the inbox can stream (the size threshold only
+  // steers the automatic choice); needs every peer's inbox mapped (no net
+  // peers)
+  if (p.algoForce == 3) return p.direct && p.nRanks <= kDirectMaxRanks ? kAlgoDirect : kAlgoRing;
+  if (llFits) return kAlgoLL;
+  // the LL128 ring over its window (the bucket, as the tuner sizes it), ahead
+  // of the direct path
+  if (p.ll128 && p.ll128Max && bytes >= p.ll128Min && bytes <= p.ll128Max) return kAlgoRingLL128;
+  if (directFits) return kAlgoDirect;
+  return kAlgoRing;
+}
+// The protocol VCCL runs a path's calls with: the one-hop LL stands in for
+// VCCL's LL (tree for the all-reduce, ring otherwise), the direct path for a
+// SIMPLE ring call.
+static int proto_of_algo(int algo) {
+  return algo == kAlgoLL ? kProtoLL : algo == kAlgoRingLL128 ? kProtoLL128 : kProtoSimple;
+}
+
 // ---------------------------------------------------------------- group plan
-// VCCL's plan for a group's ring collectives of one comm (every call here
-// taken to run as RING / SIMPLE, the protocol VCCL's tuner picks for
-// bandwidth-bound buckets):
+// VCCL's plan for a group's collectives of one comm:
 //  * taskAppend: trafficBytes = count * eltSize * trafficPerByte, inserted
 //    into the size sorter (enqueue.cc:2405-2413; comm.h:294-343: 81 bins of
 //    u32fpEncode(min(bytes, 1 GiB) >> 10, 2 bits) in descending size, LIFO
@@ -461,25 +545,34 @@ static CbdPlan cbd_schedule(int coll, int64_t count, int64_t eltSize, int nRanks
 //  * ncclPrepareTasks (enqueue.cc:352-437): the sorted list binned by
 //    (func, devOp, type) in LIFO order — each bin size-ascending, bins in
 //    order of first appearance; runs within 4x of the run's first
-//    trafficBytes aggregated and nMaxChannels tuned on the aggregate's bytes;
+//    trafficBytes aggregated; the path (select_algo, standing in for
+//    getAlgoInfo's tuner) and nMaxChannels chosen on the aggregate's count
+//    and given to every member; an LL member's trafficBytes x4 (:418);
 //  * scheduleCollTasksToPlan (enqueue.cc:518-769): trafficPerChannel = the
 //    plan's traffic / min(sum nMaxChannels, comm channels), each task placed
-//    at the running channelId / currentTraffic; a task that would overflow
-//    the kernel-argument budget (testBudget :278-286: 16-byte work batches
-//    within 4 KiB - 32 B of kernel arguments, 96-byte works within half the
-//    1 MiB work FIFO; batches counted as addWorkBatchToPlan :91-156 does)
+//    at the running channelId / currentTraffic under its protocol; a task
+//    that would overflow the kernel-argument budget (testBudget :278-286:
+//    16-byte work batches within 4 KiB - 32 B of kernel arguments, 96-byte
+//    works within half the 1 MiB work FIFO; batches counted as
+//    addWorkBatchToPlan :91-156 does, per device function and protocol)
 //    starts the next plan.
-// Restated for the tests in oracle/vccl_sched.py (plan_schedule).
+// No policy: every call RING / SIMPLE.  Restated for the tests in
+// oracle/vccl_sched.py (plan_schedule).
 struct GroupTask {
   int coll;
   int64_t count, eltSize;  // AG in bytes
   int binKey;              // (func, devOp, type): ncclPrepareTasks' bins
   int funcKey;             // the device function (batches merge per function)
 };
+struct PlanGeometry {
+  int64_t stepBytes, nThreads;            // SIMPLE: FIFO step, NCCL_NTHREADS
+  int64_t ll128StepBytes, ll128Threads;   // LL128: step, NCCL_LL128_NTHREADS
+};
 struct GroupPlanOut {
   std::vector<int> order;        // tasks in execution (plan) order
   std::vector<int> planOf;       // per task: the plan (kernel) it lands in
-  std::vector<CbdPlan> cbd;      // per task
+  std::vector<int> algo;         // per task: the path of its aggregate
+  std::vector<CbdPlan> cbd;      // per task, under the path's protocol
 };
 static uint32_t u32fp_encode(uint32_t x, int bitsPerPow2) {  // bitops.h:252-262
   const int log2x = 31 - __builtin_clz(x | 1);
@@ -487,8 +580,8 @@ static uint32_t u32fp_encode(uint32_t x, int bitsPerPow2) {  // bitops.h:252-262
   const uint32_t exponent = log2x >= bitsPerPow2 ? log2x - (bitsPerPow2 - 1) : 0;
   return exponent << bitsPerPow2 | mantissa;
 }
-static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commChannels, int64_t stepBytes,
-                       int64_t nThreads, GroupPlanOut* out) {
+static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commChannels, const PlanGeometry& geo,
+                       const AlgoPolicy* pol, GroupPlanOut* out) {
   const int n = (int)ts.size();
   std::vector<uint64_t> traffic(n);
   for (int i = 0; i < n; i++)
@@ -513,15 +606,27 @@ static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commCha
     }
     byKey[k].insert(byKey[k].begin(), i);
   }
-  std::vector<int> nMax(n), queue;
+  auto step_of = [&](int proto) {
+    return proto == kProtoLL ? kLLStepBytes : proto == kProtoLL128 ? geo.ll128StepBytes : geo.stepBytes;
+  };
+  std::vector<int> nMax(n), proto(n), queue;
+  out->algo.assign(n, kAlgoRing);
   for (auto& lst : byKey) {
     for (size_t a = 0; a < lst.size();) {
       size_t e = a + 1;
       int64_t aggCount = ts[lst[a]].count;
       while (e < lst.size() && traffic[lst[e]] < 4 * traffic[lst[a]]) aggCount += ts[lst[e++]].count;
-      const int nc = ring_nmax_channels(ts[lst[a]].coll, aggCount, ts[lst[a]].eltSize, nRanks, commChannels,
-                                        kProtoSimple, nThreads);
-      for (size_t j = a; j < e; j++) nMax[lst[j]] = nc;
+      const GroupTask& h = ts[lst[a]];
+      const int algo = pol ? select_algo(*pol, h.coll, h.eltSize, aggCount) : kAlgoRing;
+      const int pr = proto_of_algo(algo);
+      const int nc = ring_nmax_channels(h.coll, aggCount, h.eltSize, nRanks, commChannels, pr,
+                                        pr == kProtoLL128 ? geo.ll128Threads : geo.nThreads);
+      for (size_t j = a; j < e; j++) {
+        nMax[lst[j]] = nc;
+        proto[lst[j]] = pr;
+        out->algo[lst[j]] = algo;
+        if (pr == kProtoLL) traffic[lst[j]] *= 4;
+      }
       a = e;
     }
     queue.insert(queue.end(), lst.begin(), lst.end());
@@ -556,12 +661,14 @@ static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commCha
     while (nPlanColls != 0 && head < queue.size()) {
       const int i = queue[head];
       PlanCursor trial = pc;
-      const CbdPlan p = cbd_place(trial, ts[i].coll, ts[i].count, ts[i].eltSize, nRanks, kProtoSimple, stepBytes);
+      const CbdPlan p = cbd_place(trial, ts[i].coll, ts[i].count, ts[i].eltSize, nRanks, proto[i],
+                                  step_of(proto[i]));
       const int nChTask = p.channelHi - p.channelLo + 1;
       if (!budget_ok(nWorkBatches + nChTask, workBytes + kWorkBytes)) break;  // the next plan
       pc = trial;
+      const int func = ts[i].funcKey * 4 + proto[i];  // devFuncId: (func, op, type, algo, proto)
       for (int c = p.channelLo; c <= p.channelHi && c < commChannels; c++) {
-        const bool fresh = lastFunc[c] < 0 || lastFunc[c] != ts[i].funcKey ||
+        const bool fresh = lastFunc[c] < 0 || lastFunc[c] != func ||
                            wipBytes[c] + kWorkBytes > 1024;  // NCCL_MAX_DEV_WORK_BATCH_BYTES
         const int64_t off = fresh ? 0 : workBytes - offsetBase[c];
         if (fresh || 63 * kWorkBytes < off) {
@@ -569,7 +676,7 @@ static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commCha
           if (fresh) wipBytes[c] = 0;
           nWorkBatches++;
         }
-        lastFunc[c] = ts[i].funcKey;
+        lastFunc[c] = func;
         wipBytes[c] += kWorkBytes;
       }
       workBytes += kWorkBytes;
@@ -581,19 +688,20 @@ static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commCha
   }
 }
 
-// A call's partition: its place in its group's plan (plan_group), else the
-// plan of the call alone.
+// A call's partition: its place in its group's plan (launch_planned, under
+// the protocol of the path its aggregate took — the caller asks for that
+// same protocol), else the plan of the call alone under `proto`.
 static CbdPlan task_plan(const Task& t, int proto) {
   const ncclComm* comm = t.comm;
-  if (t.planned && proto == kProtoSimple) return t.plan;
+  if (t.planned) return t.plan;
   const bool ag = t.coll == kAllGather;
   const int64_t esz = ag ? 1 : type_size(t.datatype);
   const int64_t count = ag ? (int64_t)t.count * type_size(t.datatype) : (int64_t)t.count;
-  return proto == kProtoLL128
-             ? cbd_schedule(t.coll, count, esz, comm->nRanks, comm->nChannels, kProtoLL128,
-                            comm->ll128StepBytes, comm->ll128Threads)
-             : cbd_schedule(t.coll, count, esz, comm->nRanks, comm->nChannels, kProtoSimple,
-                            comm->stepBytes, comm->nThreads);
+  if (proto == kProtoLL128)
+    return cbd_schedule(t.coll, count, esz, comm->nRanks, comm->nChannels, kProtoLL128, comm->ll128StepBytes,
+                        comm->ll128Threads);
+  return cbd_schedule(t.coll, count, esz, comm->nRanks, comm->nChannels, proto,
+                      proto == kProtoLL ? kLLStepBytes : comm->stepBytes, comm->nThreads);
 }
 
 // The ring work of one call (its kernel element type and device op too).
@@ -702,9 +810,10 @@ static int dev_coll(int coll) {
 }
 
 // The cbd partition of a reduce-scatter's block, for the one-hop LL / direct
-// reduce-scatters' per-channel fold order (the ring's own, cbd_schedule).
-static CbdLite rs_cbd(const Task& t) {
-  const CbdPlan p = task_plan(t, kProtoSimple);
+// reduce-scatters' per-channel fold order: the ring's, under VCCL's protocol
+// for the path (LL: the LL ring's cells, enqueue.cc:599; direct: SIMPLE).
+static CbdLite rs_cbd(const Task& t, int proto) {
+  const CbdPlan p = task_plan(t, proto);
   return CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)t.count};
 }
 
@@ -742,7 +851,7 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   }
   w.nParts = nTasks;
   w.nLines = lines;
-  if (t.coll == kReduceScatter) w.cbd = rs_cbd(t);
+  if (t.coll == kReduceScatter) w.cbd = rs_cbd(t, kProtoLL);
   if (lines > comm->llLines) return ncclInternalError;
   const int kt = t.coll == kAllGather ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
@@ -808,7 +917,7 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
     // (count elements) that fits a region; it is cut into blocks directly.
     w.chunkElts = std::min<int64_t>(count, regionElts / eltAlign * eltAlign);
     shard0 = w.chunkElts;
-    if (t.coll == kReduceScatter) w.cbd = rs_cbd(t);
+    if (t.coll == kReduceScatter) w.cbd = rs_cbd(t, kProtoSimple);
   }
   w.nChunks = (int)((count + w.chunkElts - 1) / w.chunkElts);
   // Blocks of >= 16 KiB (one 512-thread x 2-pack hunk), at most the cap.
@@ -876,49 +985,9 @@ static ncclResult_t launch_direct(const Task* ts, int nTasks) {
   return ncclSuccess;
 }
 
-// Algorithm choice (topoGetAlgoInfo, enqueue.cc:1805-1945, reduced to one
-// node over a full xGMI mesh): buckets up to the LL threshold take the
-// one-hop LL path, up to the direct threshold the direct path (LL128's
-// mid-range slot; all-reduce two-shot, reduce-scatter / all-gather one-hop),
-// larger ones the SIMPLE ring.  NCCL_ALGO / NCCL_PROTO force one: Ring/SIMPLE
-// -> ring; Tree/LL -> LL where it fits; LL128/Direct -> direct where it
-// fits; anything that does not fit falls through to the ring.
-enum { kAlgoRing = 0, kAlgoLL = 1, kAlgoDirect = 2, kAlgoRingLL128 = 3 };
+// A call's path: select_algo on the comm's thresholds.
 static int choose_algo(const Task& t) {
-  const ncclComm* c = t.comm;
-  if (c->nRanks < 2 || c->algoForce == 1) return kAlgoRing;
-  // NCCL_PROTO=LL128 (or vcclCommSetAlgo): the LL128 ring for every size
-  if (c->algoForce == 4) return c->ll128Buf ? kAlgoRingLL128 : kAlgoRing;
-  const size_t esz = (size_t)type_size(t.datatype);
-  bool llFits, directFits;
-  if (t.coll == kAllReduce) {
-    const size_t bytes = t.count * esz;
-    llFits = c->llBuf && bytes <= c->llMaxBytes;
-    directFits = c->dPeers && bytes <= c->directMaxBytes;
-  } else {
-    // Reduce-scatter / all-gather: one rank's block must fit an LL slot; the
-    // thresholds are on the whole bucket (n blocks), as the reference's tuner
-    // sizes RS / AG (enqueue.cc:1955, ncclFuncMaxSendRecvCount).
-    const size_t block = t.count * esz, bytes = block * (size_t)c->nRanks;
-    llFits = c->llBuf && c->nRanks <= kOrderMaxRanks && block <= (size_t)c->llLines * 8 &&
-             bytes <= c->llRsAgMaxBytes;
-    directFits = c->dPeers && bytes <= c->directRsAgMaxBytes;
-  }
-  if (c->algoForce == 2) return llFits ? kAlgoLL : kAlgoRing;
-  // Forced direct: any bucket the inbox can stream (the size threshold only
-  // steers the automatic choice); needs every peer's inbox mapped (no net
-  // peers)
-  if (c->algoForce == 3) return c->dPeers && c->nRanks <= kDirectMaxRanks ? kAlgoDirect : kAlgoRing;
-  if (llFits) return kAlgoLL;
-  // VCCL_LL128=1: the LL128 ring over its window (the bucket, as the tuner
-  // sizes it), ahead of the direct path
-  {
-    const size_t bytes = t.count * esz * (t.coll == kAllReduce ? 1 : (size_t)c->nRanks);
-    if (c->ll128Buf && c->ll128MaxBytes && bytes >= c->ll128MinBytes && bytes <= c->ll128MaxBytes)
-      return kAlgoRingLL128;
-  }
-  if (directFits) return kAlgoDirect;
-  return kAlgoRing;
+  return select_algo(policy_of(t.comm), t.coll, type_size(t.datatype), (int64_t)t.count);
 }
 
 static ncclResult_t launch_task(const Task& t) {
@@ -966,8 +1035,9 @@ static ncclResult_t launch_task(const Task& t) {
 // identically.  The fused launch runs on the first task's stream; the other
 // tasks' streams are joined before it and wait for it after.
 static int fuse_key_algo(const Task& t) { return t.comm->nRanks > 1 ? choose_algo(t) : -1; }
-static bool fusable(const Task& a, const Task& b, int algo) {
-  if (a.comm != b.comm || a.coll != b.coll || fuse_key_algo(b) != algo) return false;
+// Same comm, collective, kernel type and op (the caller compares the paths).
+static bool fusable(const Task& a, const Task& b) {
+  if (a.comm != b.comm || a.coll != b.coll) return false;
   if (a.coll == kAllGather) return true;  // byte copies: any type
   return a.datatype == b.datatype && a.devOp == b.devOp && a.arg == b.arg && a.argPtr == b.argPtr;
 }
@@ -1021,13 +1091,17 @@ static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, cons
   return r;
 }
 
-// The group's calls of one comm that take the SIMPLE ring or the direct path
-// (`idx`, in call order): placed on VCCL's plan for them (group_plan) — the
-// direct path folds every element in the order of its place in that plan,
-// as the ring does — and launched in plan order, consecutive calls of one
-// path with the same collective, type and op fused (<= max_parts).
-static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<int>& idx,
-                                   const std::vector<int>& algo) {
+// A group's calls of one comm (`idx`, in call order, nRanks > 1) on VCCL's
+// plan for them (group_plan): each (func, op, type) aggregate takes the path
+// select_algo gives its summed count, as ncclPrepareTasks gives getAlgoInfo's
+// choice to every member; every call is placed on the plan's channels under
+// its path's protocol — the ring, LL128 ring and direct path fold every
+// element in the order of that place, the LL reduce-scatter per channel of
+// it, and LL calls shift the running channel cursor as in VCCL — and the
+// calls launch in plan order, consecutive calls of one plan and path with the
+// same collective, type and op fused (<= max_parts; LL all-reduces while their
+// lines fit one slot, LL reduce-scatters / all-gathers one per launch).
+static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<int>& idx) {
   ncclComm* comm = tasks[idx[0]].comm;
   std::vector<GroupTask> g;
   for (int j : idx) {
@@ -1041,7 +1115,9 @@ static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<i
                           (t.coll * 16 + op) * 32 + dt, (t.coll * 16 + op) * 32 + kt});
   }
   GroupPlanOut plan;
-  group_plan(g, comm->nRanks, comm->nChannels, comm->stepBytes, comm->nThreads, &plan);
+  const AlgoPolicy pol = policy_of(comm);
+  group_plan(g, comm->nRanks, comm->nChannels,
+             PlanGeometry{comm->stepBytes, comm->nThreads, comm->ll128StepBytes, comm->ll128Threads}, &pol, &plan);
   for (size_t k = 0; k < idx.size(); k++) {
     if (plan.planOf[k] < 0) return ncclInternalError;
     tasks[idx[k]].planned = true;
@@ -1049,18 +1125,23 @@ static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<i
   }
   std::vector<std::vector<Task>> runs;
   std::vector<int> runAlgo, runPlan;
+  std::vector<int64_t> runLines;
   static const bool fusePlanned = param_int("GROUP_PLAN_FUSE", 1) != 0;
   for (int k : plan.order) {
     const Task& t = tasks[idx[k]];
-    const int a = algo[idx[k]];
+    const int a = plan.algo[k];
+    const int64_t lines = a == kAlgoLL ? ll_lines_of(t) : 0;
     if (fusePlanned && !runs.empty() && runPlan.back() == plan.planOf[k] && runAlgo.back() == a &&
-        runs.back().size() < (size_t)max_parts(a) && fusable(runs.back()[0], t, a)) {
+        runs.back().size() < (size_t)max_parts(a) && fusable(runs.back()[0], t) &&
+        (a != kAlgoLL || (t.coll == kAllReduce && runLines.back() + lines <= comm->llLines))) {
       runs.back().push_back(t);
+      runLines.back() += lines;
       continue;
     }
     runs.push_back({t});
     runAlgo.push_back(a);
     runPlan.push_back(plan.planOf[k]);
+    runLines.push_back(lines);
   }
   return launch_runs(runs, runAlgo);
 }
@@ -1070,28 +1151,28 @@ static ncclResult_t launch_group(std::vector<Task>& tasks) {
   const size_t n = tasks.size();
   std::vector<char> done(n, 0);
   const bool fuse = param_int("GROUP_FUSE", 1) != 0;
-  // VCCL_GROUP_PLAN=0: every call keeps the partition of a call planned alone
+  // VCCL_GROUP_PLAN=0: every call keeps its own path and the partition of a
+  // call planned alone (runs of consecutive fusable calls still fuse)
   const bool plan = fuse && param_int("GROUP_PLAN", 1) != 0;
   std::vector<int> algo(n, -1);
-  if (fuse)
+  if (fuse && !plan)
     for (size_t i = 0; i < n; i++) algo[i] = fuse_key_algo(tasks[i]);
-  auto planned_path = [&](size_t i) { return plan && (algo[i] == kAlgoRing || algo[i] == kAlgoDirect); };
   for (size_t i = 0; i < n; i++) {
     if (done[i]) continue;
     ncclResult_t r;
-    if (planned_path(i)) {
-      // every ring / direct call of this comm in the group, one VCCL plan
+    if (plan && tasks[i].comm->nRanks > 1) {
+      // every call of this comm in the group, one VCCL plan
       std::vector<int> idx;
       for (size_t j = i; j < n; j++)
-        if (!done[j] && tasks[j].comm == tasks[i].comm && planned_path(j)) idx.push_back((int)j);
+        if (!done[j] && tasks[j].comm == tasks[i].comm) idx.push_back((int)j);
       for (int j : idx) done[j] = 1;
-      r = launch_planned(tasks, idx, algo);
+      r = launch_planned(tasks, idx);
     } else if (algo[i] >= 0 && (algo[i] != kAlgoLL || tasks[i].coll == kAllReduce)) {
       std::vector<Task> batch{tasks[i]};
       int64_t lines = ll_lines_of(tasks[i]);
       for (size_t j = i + 1; j < n && batch.size() < (size_t)max_parts(algo[i]); j++) {
         if (done[j] || tasks[j].comm != tasks[i].comm) continue;
-        if (!fusable(tasks[i], tasks[j], algo[i])) break;
+        if (algo[j] != algo[i] || !fusable(tasks[i], tasks[j])) break;
         if (algo[i] == kAlgoLL) {
           if (lines + ll_lines_of(tasks[j]) > tasks[i].comm->llLines) break;
           lines += ll_lines_of(tasks[j]);
@@ -1355,7 +1436,7 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition
     size_t stepBytes, int nThreads, int64_t* out) {
   if (!out || coll < 0 || coll > 2 || type_size(datatype) < 1 || nRanks < 1 ||
       nChannels < 1 || nChannels > kMaxChannels || count == 0 || stepBytes < 4096 || nThreads < 64 ||
-      (proto != kProtoSimple && proto != kProtoLL128))
+      (proto != kProtoSimple && proto != kProtoLL128 && proto != kProtoLL))
     return ncclInvalidArgument;
   const int c = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : kAllGather;
   const int64_t esz = c == kAllGather ? 1 : type_size(datatype);
@@ -1385,11 +1466,13 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingChunkOf(
   return ncclSuccess;
 }
 
-extern "C" __attribute__((visibility("default"))) ncclResult_t vcclGroupPlan(
-    int nCalls, const int* colls, const size_t* counts, const int* datatypes, const int* ops, int nRanks,
-    int nChannels, size_t stepBytes, int nThreads, int* order, int* planOf, int64_t* cbd) {
+// vccl_ext.h: the group planner on explicit inputs (host only).
+static ncclResult_t group_plan_export(int nCalls, const int* colls, const size_t* counts, const int* datatypes,
+                                      const int* ops, int nRanks, int nChannels, const PlanGeometry& geo,
+                                      const AlgoPolicy* pol, int* algos, int* order, int* planOf, int64_t* cbd) {
   if (nCalls < 1 || !colls || !counts || !datatypes || !ops || !order || !planOf || !cbd || nRanks < 1 ||
-      nChannels < 1 || nChannels > kMaxChannels || stepBytes < 4096 || nThreads < 64)
+      nChannels < 1 || nChannels > kMaxChannels || geo.stepBytes < 4096 || geo.nThreads < 64 ||
+      geo.ll128StepBytes < 1920 * 16 || geo.ll128Threads < 64)
     return ncclInvalidArgument;
   std::vector<GroupTask> g;
   for (int i = 0; i < nCalls; i++) {
@@ -1407,15 +1490,53 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclGroupPlan(
                           (c * 16 + devOp) * 32 + (ag ? (int)ncclInt8 : (int)dt), (c * 16 + devOp) * 32 + kt});
   }
   GroupPlanOut p;
-  group_plan(g, nRanks, nChannels, (int64_t)stepBytes, nThreads, &p);
+  group_plan(g, nRanks, nChannels, geo, pol, &p);
   for (int i = 0; i < nCalls; i++) {
     order[i] = p.order[i];
     planOf[i] = p.planOf[i];
+    if (algos) {
+      const int a = p.algo[i];
+      algos[i] = a == kAlgoLL ? vcclAlgoLL : a == kAlgoDirect ? vcclAlgoDirect
+                 : a == kAlgoRingLL128 ? vcclAlgoLL128 : vcclAlgoRing;
+    }
     const CbdPlan& q = p.cbd[i];
     const int64_t v[8] = {q.channelLo, q.channelHi, q.countLo, q.countMid, q.countHi, q.chunkLo, q.chunkMid, q.chunkHi};
     memcpy(cbd + 8 * (size_t)i, v, sizeof(v));
   }
   return ncclSuccess;
+}
+
+extern "C" __attribute__((visibility("default"))) ncclResult_t vcclGroupPlan(
+    int nCalls, const int* colls, const size_t* counts, const int* datatypes, const int* ops, int nRanks,
+    int nChannels, size_t stepBytes, int nThreads, int* order, int* planOf, int64_t* cbd) {
+  const PlanGeometry geo{(int64_t)stepBytes, nThreads, 120 * 640 * 8, 640};
+  return group_plan_export(nCalls, colls, counts, datatypes, ops, nRanks, nChannels, geo, nullptr, nullptr, order,
+                           planOf, cbd);
+}
+
+extern "C" __attribute__((visibility("default"))) ncclResult_t vcclGroupPlanEx(
+    int nCalls, const int* colls, const size_t* counts, const int* datatypes, const int* ops, int nRanks,
+    int nChannels, const int64_t* geometry, const int64_t* policy, int* algos, int* order, int* planOf,
+    int64_t* cbd) {
+  if (!geometry) return ncclInvalidArgument;
+  const PlanGeometry geo{geometry[0], geometry[1], geometry[2], geometry[3]};
+  AlgoPolicy pol;
+  if (policy) {
+    if (policy[0] < 0 || policy[0] > 4) return ncclInvalidArgument;
+    pol.nRanks = nRanks;
+    pol.algoForce = (int)policy[0];
+    pol.llSlotBytes = policy[1];
+    pol.llMax = (uint64_t)policy[2];
+    pol.llRsAgMax = (uint64_t)policy[3];
+    pol.ll128 = policy[4] != 0;
+    pol.ll128Min = (uint64_t)policy[5];
+    pol.ll128Max = (uint64_t)policy[6];
+    pol.direct = policy[7] != 0;
+    pol.directMax = (uint64_t)policy[8];
+    pol.directRsAgMax = (uint64_t)policy[9];
+  }
+  return group_plan_export(nCalls, colls, counts, datatypes, ops, nRanks, nChannels, geo, policy ? &pol : nullptr,
+                           algos, order, planOf, cbd);
 }
 
 extern "C" ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo) {

@@ -41,7 +41,7 @@ EXPORTED = [
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
     "vcclCommRingTrace",
-    "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders", "vcclGroupPlan", "vcclAlgoSelection",
+    "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders", "vcclGroupPlan", "vcclGroupPlanEx", "vcclAlgoSelection",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
 ]
@@ -114,6 +114,10 @@ def lib() -> ctypes.CDLL:
         "vcclGroupPlan": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_size), ctypes.POINTER(c_int),
                           ctypes.POINTER(c_int), c_int, c_int, c_size, c_int, ctypes.POINTER(c_int),
                           ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_int64)],
+        "vcclGroupPlanEx": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_size), ctypes.POINTER(c_int),
+                            ctypes.POINTER(c_int), c_int, c_int, ctypes.POINTER(ctypes.c_int64),
+                            ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                            ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_int64)],
         "vcclAlgoSelection": [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int)],
     }
@@ -227,6 +231,29 @@ def group_plan(calls, nranks: int, nchannels: int, slot_bytes: int = 512 << 10,
     check(lib().vcclGroupPlan(n, colls, counts, dts, ops, nranks, nchannels, slot_bytes, nthreads, order,
                               plan_of, cbd), "vcclGroupPlan")
     return list(order), list(plan_of), [tuple(cbd[8 * i:8 * i + 8]) for i in range(n)]
+
+
+POLICY_FIELDS = ("force", "ll_slot", "ll_max", "ll_rsag_max", "ll128", "ll128_min", "ll128_max", "direct",
+                 "direct_max", "direct_rsag_max")
+
+
+def group_plan_ex(calls, nranks: int, nchannels: int, policy: dict | None, slot_bytes: int = 512 << 10,
+                  nthreads: int = 512, ll128_step: int = 120 * 640 * 8, ll128_threads: int = 640):
+    """vcclGroupPlanEx: the plan a comm lays a group out on — a path per
+    aggregate from `policy` (POLICY_FIELDS; None = every call on the SIMPLE
+    ring).  Returns (algos, order, plan_of, parts), algos as ALGO_NAMES."""
+    n = len(calls)
+    ci = ctypes.c_int * n
+    colls, dts, ops = ci(*[c[0] for c in calls]), ci(*[c[2] for c in calls]), ci(*[c[3] for c in calls])
+    counts = (ctypes.c_size_t * n)(*[c[1] for c in calls])
+    geo = (ctypes.c_int64 * 4)(slot_bytes, nthreads, ll128_step, ll128_threads)
+    pol = None if policy is None else (ctypes.c_int64 * 10)(*[int(policy[k]) for k in POLICY_FIELDS])
+    algos, order, plan_of = ci(), ci(), ci()
+    cbd = (ctypes.c_int64 * (8 * n))()
+    check(lib().vcclGroupPlanEx(n, colls, counts, dts, ops, nranks, nchannels, geo, pol, algos, order, plan_of,
+                                cbd), "vcclGroupPlanEx")
+    return ([ALGO_NAMES[a] for a in algos], list(order), list(plan_of),
+            [tuple(cbd[8 * i:8 * i + 8]) for i in range(n)])
 
 
 def algo_selection(algo: str | None, proto: str | None) -> tuple[int, int]:
