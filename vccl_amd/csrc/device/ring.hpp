@@ -172,11 +172,12 @@ struct RingCtx {
 // [16 (S - 1) 64 / S + 8 (l / S), +8).  The receiver polls its round's lines
 // (one 16-byte sc0 sc1 load per lane) until every flag lane shows the step,
 // and uses the data of that same load: the sender's wave store (sc0 sc1
-// write-through) must deliver a line whole — with 64-byte lines the flag
-// covers one 64-byte write request (the granule the PMC passes show); the
-// 128-byte line (VCCL's 15/16 NVLink line, -DVCCL_LL128_LINE=128) spans two
-// requests and relies on them landing together (0 tears in the intra-GPU
-// probe, tests/test_gpu_ll128.py).  No tail flag and no drain per step: the
+// write-through) must deliver a line whole — with 64-byte lines (default)
+// the flag covers one 64-byte write request (the granule the PMC passes
+// show); the 128-byte line (VCCL's 15/16 NVLink line, -DVCCL_LL128_LINE=128)
+// spans two requests with no order between them and tore in r04l (the first
+// 64 bytes stale under a fresh flag), so it is a probe build only.  No tail
+// flag and no drain per step: the
 // sender waits for the credit (head) like SIMPLE, the receiver posts the
 // head after the step.  Steps and credits are the channel's SIMPLE ones.
 template <class T>

@@ -208,15 +208,18 @@ enum : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2 };
 // per L/16 lanes — every lane but the line's last carries a 16-byte data
 // piece, the last an 8-byte data piece and the 8-byte flag — so one wave
 // instruction moves 1 KiB ("a round") of 1024/L lines.
-//   L = 128 (default): 8 lines, 960 data bytes per round (15/16, VCCL's
-//       NVLink line, device.h:82-83); VCCL's 576,000-byte LL128 chunk is
-//       exactly 600 rounds = its 614,400-byte step.  2-4 % faster than L = 64
-//       at 1-8 MiB, level at 256 KiB (2 ranks, interleaved A/B,
-//       profiles/r04e);
-//   L = 64 (-DVCCL_LL128_LINE=64): 16 lines, 896 data bytes per round (7/8),
-//       one flag per 64-byte write request (the granule the PMC passes show).
+//   L = 64 (default): 16 lines, 896 data bytes per round (7/8), one flag per
+//       64-byte write request — the unit a wave store reaches memory in
+//       (every TCC_EA0 write request is 64 B, profiles/r04f), so a line lands
+//       whole;
+//   L = 128 (-DVCCL_LL128_LINE=128, VCCL's 15/16 NVLink line, device.h:
+//       82-83): 8 lines, 960 data bytes per round, 2-4 % faster at 1-8 MiB
+//       (profiles/r04e) — but a line is TWO write requests with no order
+//       between them, and r04l caught the tear: 16 fp32 (the first 64 bytes
+//       of a line, data lanes 0-3) stale under a fresh flag in a 4-rank
+//       LL128 all-reduce (profiles/r04l).  Not safe; kept only for probes.
 #ifndef VCCL_LL128_LINE
-#define VCCL_LL128_LINE 128
+#define VCCL_LL128_LINE 64
 #endif
 static_assert(VCCL_LL128_LINE == 64 || VCCL_LL128_LINE == 128, "LL128 line: 64 or 128 bytes");
 constexpr int kLL128LineBytes = VCCL_LL128_LINE;
