@@ -3,7 +3,7 @@
 
 argv: rank nranks uid_hex outdir
 One ncclGroupStart/End of STRESS_CALLS — all-reduces, reduce-scatters and
-all-gathers of f32 / bf16 / i32 (sum, max) from 1 KiB to 6 MiB, issued on
+all-gathers of f32 / bf16 / i32 (sum, avg, max) from 1 KiB to 6 MiB, issued on
 two streams in turn — so the group plan spans several (func, op, type) bins,
 aggregates, and launches of up to 16 parts with channels skipped per part.
 Saves every output and the path the library chose for each call
@@ -36,7 +36,8 @@ def stress_calls(n, k=36, seed=4242):
     for i in range(k):
         coll = COLLS[int(rng.integers(0, 3))]
         dt = int(rng.choice([7, 9, 2]))
-        op = 2 if dt == 2 and rng.random() < 0.5 else 0
+        u = rng.random()
+        op = 2 if dt == 2 and u < 0.4 else 4 if u > 0.7 else 0  # max (i32), avg, sum
         nbytes = int(2 ** rng.uniform(10, np.log2(6 << 20)))
         esz = 2 if dt == 9 else 4
         count = max(1, nbytes // esz)

@@ -547,9 +547,9 @@ def test_group_mixed_direct_sizes():
                     assert_bitexact(dt, res[r][name], exp, what=f"{name} rank {r}")
 
 
-@pytest.mark.parametrize("geom", ["test", "ring_only"])
+@pytest.mark.parametrize("geom", ["test", "ring_only", "ll128_window"])
 def test_group_plan_stress(geom):
-    """36 calls in one group (AR / RS / AG of f32 / bf16 / i32, sum and max,
+    """36 calls in one group (AR / RS / AG of f32 / bf16 / i32, sum, avg, max,
     1 KiB - 6 MiB, two streams) at 4 ranks: several (func, op, type) bins,
     aggregates and batches of up to 16 parts with channels skipped per part.
     Every call on its aggregate's path (vcclCommCollAlgo on the aggregate's
@@ -567,6 +567,10 @@ def test_group_plan_stress(geom):
     env.update(TEST_GEOM)
     if geom == "ring_only":
         env["NCCL_ALGO"] = "Ring"
+    if geom == "ll128_window":
+        # every path in one plan: LL up to 64 KiB, the LL128 ring's window
+        # 64 KiB - 1 MiB, direct up to 4 MiB, the SIMPLE ring above
+        env.update(VCCL_LL128="1", VCCL_LL_THRESHOLD=str(64 << 10))
     nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_group_stress_worker.py"),
@@ -577,9 +581,11 @@ def test_group_plan_stress(geom):
         res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
     calls = G.stress_calls(n)
     algos = [str(a) for a in res[0]["algos"]]
-    assert set(algos) <= {"ll", "ring", "direct"}, algos
+    assert set(algos) <= {"ll", "ring", "direct", "ll128"}, algos
     if geom == "ring_only":
         assert set(algos) == {"ring"}
+    elif geom == "ll128_window":
+        assert set(algos) == {"ll", "ll128", "direct", "ring"}, algos  # all four paths in one plan
     else:
         assert len(set(algos)) >= 2, algos  # the plan spans paths
     for r in range(n):
