@@ -607,6 +607,28 @@ def test_group_plan_stress(geom):
                             what=f"{name} ({algos[i]}) {geom} rank {r}")
 
 
+@pytest.mark.parametrize("n,event", [(2, "1"), (4, "1"), (2, "0")])
+def test_calls_on_alternating_streams(n, event):
+    """Forty calls of one comm outside any group, back to back on three
+    streams in turn (LL, direct and ring all-reduces, reduce-scatters,
+    all-gathers of 64 B - 12 MiB): each launch must wait for the previous
+    one (shared FIFOs, LL slots, inbox regions) through the comm's ordering
+    event — bound to the kernel's completion (VCCL_LAUNCH_EVENT=1, the
+    default) or a recorded marker (0); every output exact
+    (tests/mp_stream_worker.py)."""
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    env.update(TEST_GEOM)
+    env["VCCL_LAUNCH_EVENT"] = event
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_stream_worker.py"),
+                               str(r), str(n), hexid], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+    outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+    assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_ring_trace_and_shared_cap(n):
     """The SIMPLE ring's slot timeline (VCCL_RING_TRACE, vcclCommRingTrace)

@@ -93,15 +93,14 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
 
 template <>
 hipError_t VCCL_RING_LAUNCH<VCCL_KT>(int coll, int devOp, const RingBatch& w, int nthreads,
-                                     hipStream_t stream) {
+                                     hipStream_t stream, hipEvent_t stop) {
   using T = typename KTypeOf<VCCL_KT>::T;
   hipError_t err = hipErrorInvalidValue;
   dim3 grid(w.w.nChannels), block(nthreads);
   if (coll == kCollAllGather) {
     if constexpr (VCCL_KT == K_U8) {
-      hipLaunchKernelGGL((k_ring<kCollAllGather, FnCopy<uint8_t>, VCCL_AG_UNROLL, kPartProto>), grid, block, 0,
-                         stream, w);
-      return hipGetLastError();
+      return launch_k(k_ring<kCollAllGather, FnCopy<uint8_t>, VCCL_AG_UNROLL, kPartProto>, grid, block, stream,
+                      stop, w);
     }
     return hipErrorInvalidValue;
   }
@@ -109,11 +108,10 @@ hipError_t VCCL_RING_LAUNCH<VCCL_KT>(int coll, int devOp, const RingBatch& w, in
     if constexpr (std::is_same<Fn, FnCopy<T>>::value) {
       err = hipErrorInvalidValue;
     } else if (coll == kCollAllReduce) {
-      hipLaunchKernelGGL((k_ring<kCollAllReduce, Fn, ring_unroll<Fn>(), kPartProto>), grid, block, 0, stream, w);
-      err = hipGetLastError();
+      err = launch_k(k_ring<kCollAllReduce, Fn, ring_unroll<Fn>(), kPartProto>, grid, block, stream, stop, w);
     } else if (coll == kCollReduceScatter) {
-      hipLaunchKernelGGL((k_ring<kCollReduceScatter, Fn, ring_unroll<Fn>(), kPartProto>), grid, block, 0, stream, w);
-      err = hipGetLastError();
+      err = launch_k(k_ring<kCollReduceScatter, Fn, ring_unroll<Fn>(), kPartProto>, grid, block, stream, stop,
+                     w);
     }
   });
   return err;
@@ -132,23 +130,20 @@ template <int K>  // instantiated in the K_U8 unit only (byte copies)
 __global__ __launch_bounds__(256) void k_ll_allgather(LLWork w) { ll_allgather(w); }
 
 template <>
-hipError_t ll_launch<VCCL_KT>(int coll, int devOp, const LLWork& w, int grid, hipStream_t stream) {
+hipError_t ll_launch<VCCL_KT>(int coll, int devOp, const LLWork& w, int grid, hipStream_t stream,
+                              hipEvent_t stop) {
   using T = typename KTypeOf<VCCL_KT>::T;
   if (coll == kCollAllGather) {
     if constexpr (VCCL_KT == K_U8) {
-      hipLaunchKernelGGL(k_ll_allgather<K_U8>, dim3(grid), dim3(256), 0, stream, w);
-      return hipGetLastError();
+      return launch_k(k_ll_allgather<K_U8>, dim3(grid), dim3(256), stream, stop, w);
     }
     return hipErrorInvalidValue;
   }
   hipError_t err = hipErrorInvalidValue;
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
-      if (coll == kCollAllReduce)
-        hipLaunchKernelGGL((k_ll_allreduce<Fn>), dim3(grid), dim3(256), 0, stream, w);
-      else
-        hipLaunchKernelGGL((k_ll_reducescatter<Fn>), dim3(grid), dim3(256), 0, stream, w);
-      err = hipGetLastError();
+      err = coll == kCollAllReduce ? launch_k(k_ll_allreduce<Fn>, dim3(grid), dim3(256), stream, stop, w)
+                                   : launch_k(k_ll_reducescatter<Fn>, dim3(grid), dim3(256), stream, stop, w);
     }
   });
   return err;
@@ -169,24 +164,21 @@ __global__ __launch_bounds__(kDirectThreads) void k_direct_allgather(DirectBatch
 }
 
 template <>
-hipError_t direct_launch<VCCL_KT>(int coll, int devOp, const DirectBatch& b, hipStream_t stream) {
+hipError_t direct_launch<VCCL_KT>(int coll, int devOp, const DirectBatch& b, hipStream_t stream,
+                                  hipEvent_t stop) {
   using T = typename KTypeOf<VCCL_KT>::T;
   const dim3 grid(b.w.nBlocks), block(kDirectThreads);
   if (coll == kCollAllGather) {
     if constexpr (VCCL_KT == K_U8) {
-      hipLaunchKernelGGL(k_direct_allgather<K_U8>, grid, block, 0, stream, b);
-      return hipGetLastError();
+      return launch_k(k_direct_allgather<K_U8>, grid, block, stream, stop, b);
     }
     return hipErrorInvalidValue;
   }
   hipError_t err = hipErrorInvalidValue;
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if constexpr (!std::is_same<Fn, FnCopy<T>>::value) {
-      if (coll == kCollAllReduce)
-        hipLaunchKernelGGL((k_direct_allreduce<Fn>), grid, block, 0, stream, b);
-      else
-        hipLaunchKernelGGL((k_direct_reducescatter<Fn>), grid, block, 0, stream, b);
-      err = hipGetLastError();
+      err = coll == kCollAllReduce ? launch_k(k_direct_allreduce<Fn>, grid, block, stream, stop, b)
+                                   : launch_k(k_direct_reducescatter<Fn>, grid, block, stream, stop, b);
     }
   });
   return err;

@@ -1,6 +1,7 @@
 // Host-side declarations for the ring kernels (one specialisation per kernel
 // element type, compiled in parallel).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "coll_types.hpp"
@@ -20,29 +21,43 @@ enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2 };
 constexpr int kRingUnroll = VCCL_RING_UNROLL;
 constexpr int kRingMaxThreads = 512;  // k_ring launch bound (ring_kernels.hip)
 
+// Every launcher takes `stop`: an event the kernel's own completion signal
+// records (hipExtLaunchKernel's stopEvent) — the comm's ordering event,
+// recorded without a separate marker packet; nullptr = none.
+//
 // w.w.nChannels workgroups (the largest part's channelHi + 1); the SIMPLE
 // ring, or the same schedules over LL128 FIFOs (separate objects).
 template <int K>
-hipError_t ring_launch(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream);
+hipError_t ring_launch(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream,
+                       hipEvent_t stop);
 template <int K>
-hipError_t ring_launch_ll128(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream);
+hipError_t ring_launch_ll128(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream,
+                             hipEvent_t stop);
 template <int K>
 inline hipError_t ring_launch_any(bool ll128, int coll, int devOp, const RingBatch& w, int nthreads,
-                                  hipStream_t stream) {
-  return ll128 ? ring_launch_ll128<K>(coll, devOp, w, nthreads, stream)
-               : ring_launch<K>(coll, devOp, w, nthreads, stream);
+                                  hipStream_t stream, hipEvent_t stop) {
+  return ll128 ? ring_launch_ll128<K>(coll, devOp, w, nthreads, stream, stop)
+               : ring_launch<K>(coll, devOp, w, nthreads, stream, stop);
 }
 
 // One-hop LL collectives (ll.hpp): 256-thread workgroups, `grid` of them.
 // All-gather only in the K_U8 unit (byte copies).
 template <int K>
-hipError_t ll_launch(int coll, int devOp, const LLWork& w, int grid, hipStream_t stream);
+hipError_t ll_launch(int coll, int devOp, const LLWork& w, int grid, hipStream_t stream, hipEvent_t stop);
 
 // Direct collectives over the full mesh (direct.hpp): two-shot all-reduce,
 // one-hop reduce-scatter / all-gather, 1 .. kDirectMaxWorks calls per launch;
 // b.w.nBlocks workgroups (the largest part's) of kDirectThreads threads.
 // All-gather only in the K_U8 unit.
 template <int K>
-hipError_t direct_launch(int coll, int devOp, const DirectBatch& b, hipStream_t stream);
+hipError_t direct_launch(int coll, int devOp, const DirectBatch& b, hipStream_t stream, hipEvent_t stop);
+
+// hipLaunchKernelGGL, or with `stop` bound to the kernel's completion.
+template <class F, class... A>
+inline hipError_t launch_k(F kernel, dim3 grid, dim3 block, hipStream_t stream, hipEvent_t stop, A... args) {
+  if (stop) hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, nullptr, stop, 0, args...);
+  else hipLaunchKernelGGL(kernel, grid, block, 0, stream, args...);
+  return hipGetLastError();
+}
 
 }  // namespace vccl

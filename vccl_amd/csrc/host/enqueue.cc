@@ -282,6 +282,16 @@ static ncclResult_t stream_order(ncclComm* comm, hipStream_t s, CaptureState* cs
     HIPCHECK(hipStreamWaitEvent(s, comm->lastLaunch, 0));
   return ncclSuccess;
 }
+// The event the launches of an eager call bind to their kernel's completion
+// (hipExtLaunchKernel stopEvent): the comm's ordering event, recorded by the
+// kernel's own completion signal instead of a separate marker packet — a
+// marker costs ~5 us of GPU time per call on MI355X (profiles/r04q: LL 8 B
+// 10.1 -> 5.7 us per call back to back, 1 MiB ring 17.5 -> 12.7).
+// VCCL_LAUNCH_EVENT=0: record markers.  Captures keep markers (graph edges).
+static hipEvent_t stop_event(ncclComm* comm, const CaptureState& cs) {
+  static const bool bind = param_int("LAUNCH_EVENT", 1) != 0;
+  return bind && !cs.active ? comm->lastLaunch : nullptr;
+}
 static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s, const CaptureState& cs) {
   if (cs.active) {
     ncclComm::CapOrder* c;
@@ -292,7 +302,11 @@ static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s, const CaptureStat
     c->has = true;
     return ncclSuccess;
   }
-  HIPCHECK(hipEventRecord(comm->lastLaunch, s));
+  // VCCL_DEBUG_NO_MARK=1: no ordering event (measurement only: correct for
+  // a comm driven from ONE stream, where stream order suffices)
+  static const bool noMark = param_int("DEBUG_NO_MARK", 0) != 0;
+  if (noMark) return ncclSuccess;
+  if (!stop_event(comm, cs)) HIPCHECK(hipEventRecord(comm->lastLaunch, s));  // else bound to the kernel
   comm->lastStream = s;
   comm->hasLastLaunch = true;
   return ncclSuccess;
@@ -750,7 +764,7 @@ static ncclResult_t ring_work_of(const Task& t, bool ll128, RingWork* out, int* 
 
 // 1 .. kRingMaxWorks ring calls of one comm with the same collective, kernel
 // type and op (fusable) in one launch on ts[0].stream; SIMPLE or LL128.
-static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128) {
+static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128, hipEvent_t stop) {
   const Task& t = ts[0];
   ncclComm* comm = t.comm;
   if (nTasks < 1 || nTasks > kRingMaxWorks) return ncclInternalError;
@@ -771,15 +785,15 @@ static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128) {
                    : t.coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
-    case K_U8: e = ring_launch_any<K_U8>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_U32: e = ring_launch_any<K_U32>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_U64: e = ring_launch_any<K_U64>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F16: e = ring_launch_any<K_F16>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F32: e = ring_launch_any<K_F32>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F64: e = ring_launch_any<K_F64>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_BF16: e = ring_launch_any<K_BF16>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F8E4M3: e = ring_launch_any<K_F8E4M3>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
-    case K_F8E5M2: e = ring_launch_any<K_F8E5M2>(ll128, coll, devOp, b, comm->nThreads, t.stream); break;
+    case K_U8: e = ring_launch_any<K_U8>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_U32: e = ring_launch_any<K_U32>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_U64: e = ring_launch_any<K_U64>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F16: e = ring_launch_any<K_F16>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F32: e = ring_launch_any<K_F32>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F64: e = ring_launch_any<K_F64>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_BF16: e = ring_launch_any<K_BF16>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F8E4M3: e = ring_launch_any<K_F8E4M3>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F8E5M2: e = ring_launch_any<K_F8E5M2>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
   }
   if (e != hipSuccess) {
     VWARN("ring kernel launch failed: %s", hipGetErrorString(e));
@@ -825,7 +839,7 @@ static CbdLite rs_cbd(const Task& t, int proto) {
 static int64_t ll_lines_of(const Task& t) {
   return ((int64_t)t.count * type_size(t.datatype) + 7) / 8;
 }
-static ncclResult_t launch_ll(const Task* ts, int nTasks) {
+static ncclResult_t launch_ll(const Task* ts, int nTasks, hipEvent_t stop) {
   const Task& t = ts[0];
   ncclComm* comm = t.comm;
   LLWork w{};
@@ -867,7 +881,7 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks) {
   grid = std::max(std::min(grid, comm->maxCTAs), comm->minCTAs);
   grid = std::max(1, std::min(grid, maxBlocks));
   const int coll = dev_coll(t.coll), devOp = t.coll == kAllGather ? OP_COPY : t.devOp;
-  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return ll_launch<K>(coll, devOp, w, grid, t.stream); });
+  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return ll_launch<K>(coll, devOp, w, grid, t.stream, stop); });
   if (e != hipSuccess) {
     VWARN("LL kernel launch failed: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
@@ -952,7 +966,7 @@ static ncclResult_t direct_work_of(const Task& t, DirectWork* out, int* ktOut, i
 // the next part's (a kernel boundary no longer separates them) — with
 // per-part lengths, workgroup b's next-part scatter could overwrite bytes a
 // peer's workgroup b' was still folding.
-static ncclResult_t launch_direct(const Task* ts, int nTasks) {
+static ncclResult_t launch_direct(const Task* ts, int nTasks, hipEvent_t stop) {
   const Task& t = ts[0];
   if (nTasks < 1 || nTasks > kDirectMaxWorks) return ncclInternalError;
   DirectBatch b{};
@@ -977,7 +991,7 @@ static ncclResult_t launch_direct(const Task* ts, int nTasks) {
   }
   b.nParts = nTasks;
   const int coll = dev_coll(t.coll);
-  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return direct_launch<K>(coll, devOp, b, t.stream); });
+  const hipError_t e = by_kernel_type(kt, [&]<int K>() { return direct_launch<K>(coll, devOp, b, t.stream, stop); });
   if (e != hipSuccess) {
     VWARN("direct kernel launch failed: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
@@ -1015,8 +1029,9 @@ static ncclResult_t launch_task(const Task& t) {
   ncclResult_t r = stream_order(t.comm, t.stream, &cs);
   if (r == ncclSuccess) {
     const int algo = choose_algo(t);
-    r = algo == kAlgoLL ? launch_ll(&t, 1)
-        : algo == kAlgoDirect ? launch_direct(&t, 1) : launch_ring(&t, 1, algo == kAlgoRingLL128);
+    const hipEvent_t stop = stop_event(t.comm, cs);
+    r = algo == kAlgoLL ? launch_ll(&t, 1, stop)
+        : algo == kAlgoDirect ? launch_direct(&t, 1, stop) : launch_ring(&t, 1, algo == kAlgoRingLL128, stop);
   }
   if (r == ncclSuccess) r = stream_mark(t.comm, t.stream, cs);
   t.comm->opCount++;
@@ -1076,9 +1091,10 @@ static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, cons
     std::vector<Task> run = runs[k];
     for (Task& t : run) t.stream = s0;
     const int n = (int)run.size(), algo = algos[k];
-    r = algo == kAlgoLL ? launch_ll(run.data(), n)
-        : algo == kAlgoDirect ? launch_direct(run.data(), n)
-                              : launch_ring(run.data(), n, algo == kAlgoRingLL128);
+    const hipEvent_t stop = stop_event(comm, cs);  // every launch: the last binding is the group's end
+    r = algo == kAlgoLL ? launch_ll(run.data(), n, stop)
+        : algo == kAlgoDirect ? launch_direct(run.data(), n, stop)
+                              : launch_ring(run.data(), n, algo == kAlgoRingLL128, stop);
     if (n > 1) comm->fusedLaunches++;
   }
   if (r == ncclSuccess) r = stream_mark(comm, s0, cs);

@@ -312,10 +312,19 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   HIPCHECK(hipHostMalloc((void**)&c->errorFlag, sizeof(int), hipHostMallocMapped));
   *c->abortFlag = 0;
   *c->errorFlag = 0;
-  HIPCHECK(hipEventCreateWithFlags(&c->lastLaunch, hipEventDisableTiming));
-  HIPCHECK(hipEventCreateWithFlags(&c->joinEvent, hipEventDisableTiming));
+  // Ordering events (stream_order / stream_mark): only ever waited on by
+  // other streams of this device, never by the host.  VCCL_EVENT_FENCE: 0 =
+  // HIP's default system-scope release when the event is recorded, 1 =
+  // device-scope release (hipEventReleaseToDevice), 2 = no system fence
+  // (hipEventDisableSystemFence).
+  const int64_t evMode = param_int("EVENT_FENCE", 0);
+  const unsigned evFlags = hipEventDisableTiming | (evMode == 1   ? hipEventReleaseToDevice
+                                                    : evMode == 2 ? hipEventDisableSystemFence
+                                                                  : 0u);
+  HIPCHECK(hipEventCreateWithFlags(&c->lastLaunch, evFlags));
+  HIPCHECK(hipEventCreateWithFlags(&c->joinEvent, evFlags));
   c->caps.resize(ncclComm::kMaxCaptures);
-  for (auto& cap : c->caps) HIPCHECK(hipEventCreateWithFlags(&cap.ev, hipEventDisableTiming));
+  for (auto& cap : c->caps) HIPCHECK(hipEventCreateWithFlags(&cap.ev, evFlags));
 
   PeerMap me{};
   me.pid = (int)getpid();
