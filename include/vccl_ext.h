@@ -62,7 +62,7 @@
  *                     loop (the chunk that finishes at ring position c,
  *                     src/device/all_reduce.h:32-64), out[2] = the end of that
  *                     chunk — the lookup the direct all-reduce folds by.
- *   vcclGroupPlan      the partition a GROUP of ring / direct calls of one
+ *   vcclGroupPlan      the partition a GROUP of calls of one
  *                     communicator gets (host only): VCCL's multi-task plan —
  *                     the size sorter and (func, op, type) bins with 4x
  *                     aggregation of ncclPrepareTasks (src/enqueue.cc:352-437)
