@@ -41,8 +41,19 @@ typedef struct ncclComm* ncclComm_t;
 #define NCCL_UNIQUE_ID_BYTES 128
 typedef struct { char internal[NCCL_UNIQUE_ID_BYTES]; } ncclUniqueId;
 
+/* The enums below are int-sized as in the reference; C++ translation units
+ * see that as a fixed underlying type, so a caller's out-of-range value (an
+ * invalid datatype or op, which the library must reject with
+ * ncclInvalidArgument) is a well-defined int there, not undefined behaviour
+ * (found by `make sanitize`, UBSan's enum check). */
+#ifdef __cplusplus
+#define VCCL_ENUM_INT : int
+#else
+#define VCCL_ENUM_INT
+#endif
+
 /* nccl.h.in:40-48 */
-typedef enum {
+typedef enum VCCL_ENUM_INT {
   ncclSuccess = 0,
   ncclUnhandledCudaError = 1, /* a HIP runtime call failed */
   ncclSystemError = 2,
@@ -83,7 +94,7 @@ typedef struct ncclConfig_v21700 {
 
 /* nccl.h.in:220-236 */
 typedef enum { ncclNumOps_dummy = 5 } ncclRedOp_dummy_t;
-typedef enum {
+typedef enum VCCL_ENUM_INT {
   ncclSum = 0,
   ncclProd = 1,
   ncclMax = 2,
@@ -94,7 +105,7 @@ typedef enum {
 } ncclRedOp_t;
 
 /* nccl.h.in:239-252 */
-typedef enum {
+typedef enum VCCL_ENUM_INT {
   ncclInt8 = 0, ncclChar = 0,
   ncclUint8 = 1,
   ncclInt32 = 2, ncclInt = 2,
@@ -111,7 +122,7 @@ typedef enum {
 } ncclDataType_t;
 
 /* nccl.h.in:255-262 */
-typedef enum {
+typedef enum VCCL_ENUM_INT {
   ncclScalarDevice = 0,
   ncclScalarHostImmediate = 1
 } ncclScalarResidence_t;
