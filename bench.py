@@ -1011,7 +1011,9 @@ def _group_row(dist, comm, rank, world, S, k, steps=20, warmup=3):
     return {"bytes": S, "calls": k, "us_separate": round(t_sep / steps * 1e6, 2),
             "us_grouped": round(t_grp / steps * 1e6, 2),
             "fused_launches_per_group": (comm.launch_stats()[1] - f0) / (steps + warmup),
-            "algo": comm.coll_algo(0, n, nccl.ncclFloat32)}
+            "algo": comm.coll_algo(0, n, nccl.ncclFloat32),
+            # grouped, the calls take the path of their aggregate (VCCL's plan)
+            "algo_grouped": comm.group_algos([(0, n, nccl.ncclFloat32, nccl.ncclSum)] * k)[0]}
 
 
 ZERO_BUCKET = 8 << 20  # bytes per bucket of the ZeRO reduce-scatter group row
@@ -1045,7 +1047,9 @@ def _zero_group_row(dist, comm, rank, world, S=ZERO_BUCKET, k=16, steps=10, warm
             "us_grouped": round(t_grp / steps * 1e6, 2), "busbw_separate": bw(t_sep),
             "busbw_grouped": bw(t_grp),
             "fused_launches_per_group": (comm.launch_stats()[1] - f0) / (steps + warmup),
-            "algo": comm.coll_algo(1, rc, nccl.ncclBfloat16)}
+            "algo": comm.coll_algo(1, rc, nccl.ncclBfloat16),
+            # grouped, the k buckets aggregate and take the aggregate's path
+            "algo_grouped": comm.group_algos([(1, rc, nccl.ncclBfloat16, nccl.ncclSum)] * k)[0]}
 
 
 def bench_extras(dist, comm, rank, world, args):

@@ -121,6 +121,11 @@ typedef enum {
 ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count, ncclDataType_t datatype,
                               int* algo);
 ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo);
+/* The vcclAlgo_t every call of a group would take on this comm: the path of
+ * its 4x aggregate in VCCL's plan (see vcclGroupPlanEx); nothing launched.
+ * colls / counts / datatypes / ops as in vcclGroupPlan. */
+ncclResult_t vcclCommGroupAlgos(ncclComm_t comm, int nCalls, const int* colls, const size_t* counts,
+                                const int* datatypes, const int* ops, int* algos);
 ncclResult_t vcclCommLaunchStats(ncclComm_t comm, unsigned long long* collectives,
                                  unsigned long long* fusedLaunches);
 ncclResult_t vcclCommRingTrace(ncclComm_t comm, void* hostBuf, size_t bytes, int* nChannels, int* cap);

@@ -84,6 +84,7 @@ def main():
         bufs[name] = (xb, yb, x.dtype)
     # every call's path: its aggregate's (ncclPrepareTasks, _ring.group_algos)
     algos = _ring.group_algos(group_calls(calls), n, comm.coll_algo)
+    lib_algos = comm.group_algos([(COLLS.index(c), cnt, dt, op) for _, c, dt, op, cnt in calls])
     res = {}
     for rep in range(2):
         for xb, yb, _ in bufs.values():
@@ -108,6 +109,7 @@ def main():
             elif not np.array_equal(out.view(np.uint8), res[name].view(np.uint8)):
                 res[name + "_differs"] = np.array(rep)
     res["algos"] = np.array(algos)
+    res["lib_algos"] = np.array(lib_algos)
     err = comm.async_error()
     comm.destroy()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)

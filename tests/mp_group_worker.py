@@ -108,6 +108,8 @@ def main():
     res["algo_rs"] = np.array(algos["rs"])
     res["algo_ar"] = np.array(algos["ar"])
     res["group_algos"] = np.array(group_algos)
+    codes = {"ar": 0, "rs": 1, "ag": 2}
+    res["lib_group_algos"] = np.array(comm.group_algos([(codes[c], cnt, dt, op) for c, op, dt, cnt in calls]))
     err = comm.async_error()
     comm.destroy()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)

@@ -59,6 +59,8 @@ def main():
     res.update(g)
     # every call's path in the group: its aggregate's (RC.group_algos)
     res["group_algos"] = np.array(RC.group_algos(comm.coll_algo, nranks))
+    # ... and as the library reports it (vcclCommGroupAlgos)
+    res["lib_group_algos"] = np.array(comm.group_algos([(0, c, dt, op) for _, op, dt, c in RC.GROUP_CASES]))
     before = comm.launch_stats()
     res["launch_stats"] = np.array(before, dtype=np.int64)
     res["net_stats"] = np.array(comm.net_stats(), dtype=np.int64)

@@ -255,6 +255,7 @@ def test_multi_process_ranks(n, geom):
         for ci, case in enumerate(RC.CASES):
             _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk,
                    nthreads, proto, chain)
+        assert [str(a) for a in res[0]["group_algos"]] == [str(a) for a in res[0]["lib_group_algos"]]
         _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot,
                      [str(a) for a in res[0]["group_algos"]], nthreads, chain)
         # every geometry fuses the group's runs (LL, direct or ring batches)
@@ -336,6 +337,7 @@ def test_group_fusion_single_process(monkeypatch):
         for c in comms:
             assert c.async_error() == 0
         algos = RC.group_algos(comms[0].coll_algo, 2)
+        assert algos == comms[0].group_algos([(0, c, dt, op) for _, op, dt, c in RC.GROUP_CASES])
         _check_group(2, [outs[0], outs[1]], nch, slot, algos)
         n_coll, fused = comms[0].launch_stats()
         # GROUP_CASES: [f32 x3] [f16 x2] big [f32] [bf16 x2] [i32] [u8] [f32 min x20 -> 16 + 4]
@@ -470,6 +472,7 @@ def test_group_zero_pattern(n, geom):
     # reference geometry
     calls = G.call_list(G.GROUP_RS, G.GROUP_AR, 1, n)
     algos = [str(a) for a in res[0]["group_algos"]]
+    assert algos == [str(a) for a in res[0]["lib_group_algos"]]  # oracle aggregation == library's
     assert len(set(algos[:16])) == 1 and len(set(algos[16:])) == 1, algos  # one aggregate each
     works = _ring.group_works(calls, n, nch, slot, algos=algos)
     vworks = _ring.group_works(calls, n, RC.VCCL_REF_CHANNELS, RC.VCCL_REF_SLOT)
@@ -528,6 +531,7 @@ def test_group_mixed_direct_sizes():
         assert not [k for k in res[r] if k.endswith("_differs")], (r, [k for k in res[r] if k.endswith("_differs")])
     calls = G.call_list(G.MIXED_RS, G.MIXED_AR, 3, n)
     algos = [str(a) for a in res[0]["group_algos"]]
+    assert algos == [str(a) for a in res[0]["lib_group_algos"]]
     assert set(algos) == {"direct"}, algos
     works = iter(_ring.group_works(calls, n, nch, slot, algos=algos))
     for i in range(max(len(G.MIXED_RS), len(G.MIXED_AR))):
@@ -581,6 +585,7 @@ def test_group_plan_stress(geom):
         res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
     calls = G.stress_calls(n)
     algos = [str(a) for a in res[0]["algos"]]
+    assert algos == [str(a) for a in res[0]["lib_algos"]]  # oracle aggregation == library's
     assert set(algos) <= {"ll", "ring", "direct", "ll128"}, algos
     if geom == "ring_only":
         assert set(algos) == {"ring"}

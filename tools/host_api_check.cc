@@ -134,6 +134,11 @@ int main() {
   for (int e = -1; e < 12; e++) EXPECT(ncclGetErrorString((ncclResult_t)e) != nullptr);
   int v = 0;
   EXPECT(ncclCommCount(nullptr, &v) == ncclInvalidArgument);
+  {
+    int c = 0, d = ncclFloat32, o = 0, a = -1;
+    size_t cnt = 4;
+    EXPECT(vcclCommGroupAlgos(nullptr, 1, &c, &cnt, &d, &o, &a) == ncclInvalidArgument);
+  }
   EXPECT(ncclAllReduce(nullptr, nullptr, 4, ncclFloat32, ncclSum, nullptr, nullptr) == ncclInvalidArgument);
   EXPECT(ncclGroupStart() == ncclSuccess);
   EXPECT(ncclAllGather(nullptr, nullptr, 4, ncclFloat32, nullptr, nullptr) == ncclInvalidArgument);

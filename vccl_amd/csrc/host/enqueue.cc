@@ -1555,6 +1555,24 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t vcclGroupPlanEx(
                            algos, order, planOf, cbd);
 }
 
+// vccl_ext.h: the path every call of a group would take on this comm (its
+// aggregate's, as launch_planned lays the group out); no launch.
+extern "C" ncclResult_t vcclCommGroupAlgos(ncclComm_t comm, int nCalls, const int* colls, const size_t* counts,
+                                           const int* datatypes, const int* ops, int* algos) {
+  NCCLCHECK(comm_check(comm, "vcclCommGroupAlgos"));
+  if (nCalls < 1 || !algos) return ncclInvalidArgument;
+  if (comm->nRanks == 1) {
+    for (int i = 0; i < nCalls; i++) algos[i] = vcclAlgoOneRank;
+    return ncclSuccess;
+  }
+  std::vector<int> order(nCalls), planOf(nCalls);
+  std::vector<int64_t> cbd(8 * (size_t)nCalls);
+  const AlgoPolicy pol = policy_of(comm);
+  return group_plan_export(nCalls, colls, counts, datatypes, ops, comm->nRanks, comm->nChannels,
+                           PlanGeometry{comm->stepBytes, comm->nThreads, comm->ll128StepBytes, comm->ll128Threads},
+                           &pol, algos, order.data(), planOf.data(), cbd.data());
+}
+
 extern "C" ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo) {
   NCCLCHECK(comm_check(comm, "vcclCommSetAlgo"));
   switch (algo) {

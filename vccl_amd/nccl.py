@@ -40,7 +40,7 @@ EXPORTED = [
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
-    "vcclCommRingTrace",
+    "vcclCommRingTrace", "vcclCommGroupAlgos",
     "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders", "vcclGroupPlan", "vcclGroupPlanEx", "vcclAlgoSelection",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
@@ -118,6 +118,8 @@ def lib() -> ctypes.CDLL:
                             ctypes.POINTER(c_int), c_int, c_int, ctypes.POINTER(ctypes.c_int64),
                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                             ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_int64)],
+        "vcclCommGroupAlgos": [vp, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_size), ctypes.POINTER(c_int),
+                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)],
         "vcclAlgoSelection": [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int)],
     }
@@ -337,6 +339,17 @@ class Comm:
         check(lib().vcclCommCollAlgo(self.handle, coll, ctypes.c_size_t(count), dtype,
                                      ctypes.byref(a)), "vcclCommCollAlgo")
         return ALGO_NAMES[a.value]
+
+    def group_algos(self, calls) -> list[str]:
+        """vcclCommGroupAlgos: the path of every call of a group on this comm
+        (its aggregate's); calls = [(coll 0 AR / 1 RS / 2 AG, count, dtype, op)]."""
+        n = len(calls)
+        ci = ctypes.c_int * n
+        out = ci()
+        check(lib().vcclCommGroupAlgos(self.handle, n, ci(*[c[0] for c in calls]),
+                                       (ctypes.c_size_t * n)(*[c[1] for c in calls]), ci(*[c[2] for c in calls]),
+                                       ci(*[c[3] for c in calls]), out), "vcclCommGroupAlgos")
+        return [ALGO_NAMES[a] for a in out]
 
     def set_algo(self, algo: str | None):
         """vcclCommSetAlgo: force "ring" | "ll" | "direct" | "ll128" for later calls; None = automatic."""
