@@ -1568,9 +1568,12 @@ extern "C" ncclResult_t vcclCommGroupAlgos(ncclComm_t comm, int nCalls, const in
   std::vector<int> order(nCalls), planOf(nCalls);
   std::vector<int64_t> cbd(8 * (size_t)nCalls);
   const AlgoPolicy pol = policy_of(comm);
-  return group_plan_export(nCalls, colls, counts, datatypes, ops, comm->nRanks, comm->nChannels,
-                           PlanGeometry{comm->stepBytes, comm->nThreads, comm->ll128StepBytes, comm->ll128Threads},
-                           &pol, algos, order.data(), planOf.data(), cbd.data());
+  // without LL128 FIFOs no call takes the LL128 ring: its geometry is moot
+  const PlanGeometry geo{comm->stepBytes, comm->nThreads,
+                         comm->ll128StepBytes > 0 ? comm->ll128StepBytes : 120 * 640 * 8,
+                         comm->ll128StepBytes > 0 ? comm->ll128Threads : 640};
+  return group_plan_export(nCalls, colls, counts, datatypes, ops, comm->nRanks, comm->nChannels, geo, &pol, algos,
+                           order.data(), planOf.data(), cbd.data());
 }
 
 extern "C" ncclResult_t vcclCommSetAlgo(ncclComm_t comm, int algo) {
