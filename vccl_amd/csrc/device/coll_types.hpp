@@ -13,11 +13,17 @@ namespace vccl {
 // ------------------------------------------------------------------- LL
 constexpr int kLLMaxParts = 16;
 
+// One call of an LL launch.  All-reduce: nbytes = count * sizeof(T).
+// Reduce-scatter / all-gather: nbytes = the bytes of ONE rank's block (send
+// holds n blocks for a reduce-scatter, recv n blocks for an all-gather); the
+// reduce-scatter folds each line on the ring of its channel (VCCL's cbd
+// partition of the block, `cbd`, DevComm::rsOrder).
 struct LLPart {
   const char* send;
   char* recv;
-  int64_t nbytes;          // count * sizeof(T)
+  int64_t nbytes;
   int64_t line0;           // first line of this part in the slot
+  CbdLite cbd;             // reduce-scatter only
 };
 
 struct LLWork {
@@ -28,16 +34,11 @@ struct LLWork {
   int preOp;
   int nRanks, rank;
   int linesPerSlot;        // capacity of one (parity, source) slot
-  int nParts;              // 1 .. kLLMaxParts all-reduces in this launch
+  int nParts;              // 1 .. kLLMaxParts calls of one collective in this launch
   int64_t nLines;          // lines of all parts (<= linesPerSlot)
   char* localBuf;          // my LL buffer: [2 parities][nRanks sources][linesPerSlot] lines
   char* peerBuf[kMaxRanks];  // every rank's LL buffer mapped here (peerBuf[rank] = local)
   LLPart parts[kLLMaxParts];
-  // Reduce-scatter / all-gather (one part): parts[0] = {input, output, bytes
-  // of ONE rank's block, 0}; nLines = lines of one block.  Reduce-scatter
-  // folds each line on the ring of its channel (VCCL's cbd partition of the
-  // block, DevComm::rsOrder).
-  CbdLite cbd;
 };
 
 // Byte offset of the (parity, source rank) slot inside an LL buffer.

@@ -222,22 +222,28 @@ __device__ void ll_allreduce(const LLWork& w) {
 // to p's slot (parity, me); p folds its block line by line from the n-1 slots
 // and its own input, in the order of the line's ring (lines never straddle a
 // channel part: parts are 16-byte multiples of the block, lines 8 bytes).
+// Up to kLLMaxParts calls per launch (a group's run): part i's block lines
+// sit at [line0_i, line0_i + ceil(nbytes_i / 8)) of every slot.
 template <class Fn>
 __device__ void ll_reducescatter(const LLWork& w) {
   using T = typename Fn::EltType;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
+  __shared__ LLParts sh;
+  ll_load_parts(w, &sh);
   const uint32_t e = ll_epoch_of(w.comm);
   const int parity = (int)(e & 1);
-  const int n = w.nRanks, me = w.rank;
-  const int64_t nLines = w.nLines, nb = w.parts[0].nbytes;
-  const char* in = w.parts[0].send;
-  char* out = w.parts[0].recv;
+  const int n = w.nRanks, me = w.rank, nParts = w.nParts;
+  const int64_t nLines = w.nLines;
   const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t gthreads = (int64_t)gridDim.x * blockDim.x;
+  int pc = 0;
   for (int64_t l = gtid; l < nLines; l += gthreads) {
+    pc = ll_advance(sh, nParts, pc, l);
+    const LLPart& part = sh.p[pc];
+    const int64_t nb = part.nbytes, pl = l - part.line0;
     for (int k = 1; k < n; k++) {
       const int p = me + k < n ? me + k : me + k - n;
-      const uint64_t v = ll_load8(in + (int64_t)p * nb, l, nb);
+      const uint64_t v = ll_load8(part.send + (int64_t)p * nb, pl, nb);
       u32x4 line;
       line.x = (uint32_t)v;
       line.y = e;
@@ -248,9 +254,13 @@ __device__ void ll_reducescatter(const LLWork& w) {
     }
   }
   bool ok = true;
+  pc = 0;
   for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
+    pc = ll_advance(sh, nParts, pc, l);
+    const LLPart& part = sh.p[pc];
+    const int64_t nb = part.nbytes, pl = l - part.line0;
     int64_t end;
-    const int ch = cbd_channel_of(w.cbd, l * 8 / (int64_t)sizeof(T), &end);
+    const int ch = cbd_channel_of(part.cbd, pl * 8 / (int64_t)sizeof(T), &end);
     const int8_t* order = w.comm->rsOrder[ch % w.comm->nRings];
     u32x4 v[kOrderMaxRanks];
 #pragma unroll
@@ -269,7 +279,7 @@ __device__ void ll_reducescatter(const LLWork& w) {
       const int q = order[j];
       uint64_t x;
       if (q == me) {
-        x = ll_load8(in + (int64_t)me * nb, l, nb);
+        x = ll_load8(part.send + (int64_t)me * nb, pl, nb);
       } else if (v[j].y == e && v[j].w == e) {
         x = (uint64_t)v[j].x | ((uint64_t)v[j].z << 32);
       } else {
@@ -282,7 +292,7 @@ __device__ void ll_reducescatter(const LLWork& w) {
     }
     if (!ok) break;
     if (Fn::kPostOp) acc = ll_apply(fn, acc, 0, 2);
-    ll_store8(out, l, nb, acc);
+    ll_store8(part.recv, pl, nb, acc);
   }
   ll_epoch_retire(w.comm, e);
 }
@@ -290,18 +300,25 @@ __device__ void ll_reducescatter(const LLWork& w) {
 // ---------------------------------------------------------------- all-gather
 // One-hop LL all-gather (bytes): my block's lines go to every peer's slot
 // (parity, me); every rank copies each rank's block out of its slots (its own
-// from its input) to output + rank * bytes.
+// from its input) to output + rank * bytes.  Up to kLLMaxParts calls per
+// launch, as the reduce-scatter.
 __device__ inline void ll_allgather(const LLWork& w) {
+  __shared__ LLParts sh;
+  ll_load_parts(w, &sh);
   const uint32_t e = ll_epoch_of(w.comm);
   const int parity = (int)(e & 1);
-  const int n = w.nRanks, me = w.rank;
-  const int64_t nLines = w.nLines, nb = w.parts[0].nbytes;
-  const char* in = w.parts[0].send;
-  char* out = w.parts[0].recv;
+  const int n = w.nRanks, me = w.rank, nParts = w.nParts;
+  const int64_t nLines = w.nLines;
   const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t gthreads = (int64_t)gridDim.x * blockDim.x;
+  int pc = 0;
   for (int64_t l = gtid; l < nLines; l += gthreads) {
-    const uint64_t v = ll_load8(in, l, nb);
+    pc = ll_advance(sh, nParts, pc, l);
+    const LLPart& part = sh.p[pc];
+    const int64_t nb = part.nbytes, pl = l - part.line0;
+    const char* in = part.send;
+    char* out = part.recv;
+    const uint64_t v = ll_load8(in, pl, nb);
     u32x4 line;
     line.x = (uint32_t)v;
     line.y = e;
@@ -312,16 +329,20 @@ __device__ inline void ll_allgather(const LLWork& w) {
       const SysAddr d = sys_addr(w.peerBuf[p] + ll_slot_off(parity, me, n, w.linesPerSlot) + l * 16);
       __builtin_amdgcn_raw_buffer_store_b128(line, d.r, d.voff, 0, kSysAux);
     }
-    if (out + (int64_t)me * nb != in) ll_store8(out + (int64_t)me * nb, l, nb, v);
+    if (out + (int64_t)me * nb != in) ll_store8(out + (int64_t)me * nb, pl, nb, v);
   }
   bool ok = true;
+  pc = 0;
   for (int64_t l = gtid; l < nLines && ok; l += gthreads) {
+    pc = ll_advance(sh, nParts, pc, l);
+    const LLPart& part = sh.p[pc];
+    const int64_t nb = part.nbytes, pl = l - part.line0;
     for (int k = 1; k < n; k++) {
       const int q = me + k < n ? me + k : me + k - n;
       uint64_t x;
       ok = ll_read_line(w.localBuf + ll_slot_off(parity, q, n, w.linesPerSlot) + l * 16, e, w.comm, &x);
       if (!ok) break;
-      ll_store8(out + (int64_t)q * nb, l, nb, x);
+      ll_store8(part.recv + (int64_t)q * nb, pl, nb, x);
     }
   }
   ll_epoch_retire(w.comm, e);

@@ -831,11 +831,11 @@ static CbdLite rs_cbd(const Task& t, int proto) {
   return CbdLite{p.channelLo, p.channelHi, p.countLo, p.countMid, (int64_t)t.count};
 }
 
-// One-hop LL collectives.  All-reduce: `ts` holds 1 .. kLLMaxParts calls of
-// one comm with the same type and op (fusable) whose lines fit one slot;
+// One-hop LL collectives: `ts` holds 1 .. kLLMaxParts calls of one comm with
+// the same collective, type and op (fusable) whose lines — all-reduce: the
+// bucket's, reduce-scatter / all-gather: one rank's block's — fit one slot;
 // they run as one launch on ts[0].stream (the caller orders the other
-// streams around it).  Reduce-scatter / all-gather: one call; a slot holds
-// one rank's block.
+// streams around it).
 static int64_t ll_lines_of(const Task& t) {
   return ((int64_t)t.count * type_size(t.datatype) + 7) / 8;
 }
@@ -853,19 +853,19 @@ static ncclResult_t launch_ll(const Task* ts, int nTasks, hipEvent_t stop) {
   w.linesPerSlot = comm->llLines;
   w.localBuf = comm->llBuf;
   for (int r = 0; r < comm->nRanks; r++) w.peerBuf[r] = comm->llPeer[r];
-  if (nTasks < 1 || nTasks > kLLMaxParts || (t.coll != kAllReduce && nTasks != 1))
-    return ncclInternalError;
+  if (nTasks < 1 || nTasks > kLLMaxParts) return ncclInternalError;
   int64_t lines = 0;
   for (int i = 0; i < nTasks; i++) {
+    if (ts[i].coll != t.coll) return ncclInternalError;
     w.parts[i].send = (const char*)ts[i].sendbuff;
     w.parts[i].recv = (char*)ts[i].recvbuff;
     w.parts[i].nbytes = (int64_t)ts[i].count * type_size(ts[i].datatype);
     w.parts[i].line0 = lines;
+    if (t.coll == kReduceScatter) w.parts[i].cbd = rs_cbd(ts[i], kProtoLL);
     lines += ll_lines_of(ts[i]);
   }
   w.nParts = nTasks;
   w.nLines = lines;
-  if (t.coll == kReduceScatter) w.cbd = rs_cbd(t, kProtoLL);
   if (lines > comm->llLines) return ncclInternalError;
   const int kt = t.coll == kAllGather ? K_U8 : kernel_type_of(t.devOp, (int)t.datatype);
   if (kt < 0) return ncclInvalidArgument;
@@ -1115,8 +1115,8 @@ static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, cons
 // element in the order of that place, the LL reduce-scatter per channel of
 // it, and LL calls shift the running channel cursor as in VCCL — and the
 // calls launch in plan order, consecutive calls of one plan and path with the
-// same collective, type and op fused (<= max_parts; LL all-reduces while their
-// lines fit one slot, LL reduce-scatters / all-gathers one per launch).
+// same collective, type and op fused (<= max_parts; LL calls while their lines
+// fit one slot).
 static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<int>& idx) {
   ncclComm* comm = tasks[idx[0]].comm;
   std::vector<GroupTask> g;
@@ -1149,7 +1149,7 @@ static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<i
     const int64_t lines = a == kAlgoLL ? ll_lines_of(t) : 0;
     if (fusePlanned && !runs.empty() && runPlan.back() == plan.planOf[k] && runAlgo.back() == a &&
         runs.back().size() < (size_t)max_parts(a) && fusable(runs.back()[0], t) &&
-        (a != kAlgoLL || (t.coll == kAllReduce && runLines.back() + lines <= comm->llLines))) {
+        (a != kAlgoLL || runLines.back() + lines <= comm->llLines)) {
       runs.back().push_back(t);
       runLines.back() += lines;
       continue;
@@ -1183,7 +1183,7 @@ static ncclResult_t launch_group(std::vector<Task>& tasks) {
         if (!done[j] && tasks[j].comm == tasks[i].comm) idx.push_back((int)j);
       for (int j : idx) done[j] = 1;
       r = launch_planned(tasks, idx);
-    } else if (algo[i] >= 0 && (algo[i] != kAlgoLL || tasks[i].coll == kAllReduce)) {
+    } else if (algo[i] >= 0) {
       std::vector<Task> batch{tasks[i]};
       int64_t lines = ll_lines_of(tasks[i]);
       for (size_t j = i + 1; j < n && batch.size() < (size_t)max_parts(algo[i]); j++) {
