@@ -348,6 +348,59 @@ def test_group_fusion_single_process(monkeypatch):
             c.destroy()
 
 
+def test_group_ll_rs_ag_fused(monkeypatch):
+    """A group's small reduce-scatters and all-gathers on the one-hop LL path
+    fuse like LL all-reduces: 6 f32 reduce-scatters then 6 all-gathers of
+    mixed types (each 0.25-3 KiB per block; one 4x aggregate per collective,
+    still LL) launch as ONE LL kernel per collective (vcclCommLaunchStats), each
+    part on its own slot lines and partition; every output exact (two comms
+    driven from one thread, 2 ranks)."""
+    import bench
+    for k, v in TEST_GEOM.items():
+        monkeypatch.setenv(k, v)
+    comms = nccl.Comm.init_all([0, 0])
+    try:
+        n = 2
+        streams = [torch.cuda.Stream() for _ in comms]
+        rs_counts = [64 * (1 + i) for i in range(6)]           # recvcount (f32)
+        ag = [(torch.float32, 7, 100 + 37 * i) if i % 2 == 0 else (torch.bfloat16, 9, 300 + 11 * i)
+              for i in range(6)]
+        xs, ys = {}, {}
+        for r in range(n):
+            for i, rc in enumerate(rs_counts):
+                x = torch.empty(rc * n, device="cuda")
+                bench.pattern_fill(x, r, n, base=i << 12)
+                xs[r, "rs", i] = x
+                ys[r, "rs", i] = torch.full((rc,), float("nan"), device="cuda")
+            for i, (tdt, code, c) in enumerate(ag):
+                xs[r, "ag", i] = torch.full((c,), float(r * 100 + i), device="cuda").to(tdt)
+                ys[r, "ag", i] = torch.full((c * n,), float("nan"), device="cuda").to(tdt)
+        torch.cuda.synchronize()
+        assert comms[0].group_algos([(1, rc, 7, 0) for rc in rs_counts]) == ["ll"] * 6
+        f0 = comms[0].launch_stats()[1]
+        nccl.group_start()
+        for r, c in enumerate(comms):
+            sp = streams[r].cuda_stream
+            for i, rc in enumerate(rs_counts):
+                c.reduce_scatter(xs[r, "rs", i].data_ptr(), ys[r, "rs", i].data_ptr(), rc, 7, 0, sp)
+            for i, (tdt, code, cnt) in enumerate(ag):
+                c.all_gather(xs[r, "ag", i].data_ptr(), ys[r, "ag", i].data_ptr(), cnt, code, sp)
+        nccl.group_end()
+        torch.cuda.synchronize()
+        for c in comms:
+            assert c.async_error() == 0
+        assert comms[0].launch_stats()[1] - f0 == 2  # one LL RS launch + one LL AG launch
+        for r in range(n):
+            for i, rc in enumerate(rs_counts):
+                assert bench.pattern_ok(ys[r, "rs", i], n, base=(i << 12) + r * rc), ("rs", r, i)
+            for i, (tdt, code, cnt) in enumerate(ag):
+                want = torch.cat([torch.full((cnt,), float(q * 100 + i), device="cuda").to(tdt) for q in range(n)])
+                assert torch.equal(ys[r, "ag", i], want), ("ag", r, i)
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_graph_capture_replay():
     """Collectives captured into a HIP graph replay correctly (device-resident
     LL epoch and ring step counters; no host state baked into the graph)."""
