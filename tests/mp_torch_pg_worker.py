@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""One rank of the PyTorch drop-in test (tests/test_gpu_collectives.py).
+
+Run with LD_PRELOAD = torch's libamdhip64.so (so one HIP runtime serves
+both) then libvccl.so: torch.distributed's "nccl" backend (ProcessGroupNCCL,
+the reference's own caller) then resolves ncclCommInitRank*,
+ncclAllReduce, ncclReduceScatter, ncclAllGather, ncclGroupStart/End, ... to
+this library instead of RCCL.  Both ranks share cuda:0, which RCCL itself
+refuses; VCCL_ALLOW_SHARED_DEVICE=1 lets this library run it.  Checks
+all_reduce (sum, avg, max), reduce_scatter_tensor and all_gather_into_tensor
+exactly; exit 0 on success.  Rendezvous: RANK, WORLD_SIZE, MASTER_ADDR /
+MASTER_PORT (TCPStore carries ncclUniqueId)."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    bad = []
+    # integer-valued inputs: exact in any fold order
+    for n in (3, 4096, 1 << 20, 3 << 20):
+        x = torch.arange(n, device="cuda", dtype=torch.float32) % 97 + rank
+        want = (torch.arange(n, device="cuda", dtype=torch.float32) % 97) * world + world * (world - 1) / 2
+        dist.all_reduce(x)
+        if not torch.equal(x, want):
+            bad.append(("all_reduce", n))
+    y = torch.full((1000,), float(4 * (rank + 1)), device="cuda", dtype=torch.bfloat16)
+    dist.all_reduce(y, op=dist.ReduceOp.AVG)
+    if not torch.equal(y, torch.full_like(y, 2.0 * (world + 1))):
+        bad.append(("avg", 1000))
+    z = torch.full((777,), rank, device="cuda", dtype=torch.int32)
+    dist.all_reduce(z, op=dist.ReduceOp.MAX)
+    if not torch.equal(z, torch.full_like(z, world - 1)):
+        bad.append(("max", 777))
+    blk = 1 << 16
+    src = torch.arange(blk * world, device="cuda", dtype=torch.float32) % 13 + rank
+    out = torch.empty(blk, device="cuda")
+    dist.reduce_scatter_tensor(out, src)
+    ref = (torch.arange(blk * world, device="cuda", dtype=torch.float32) % 13)[rank * blk:(rank + 1) * blk]
+    if not torch.equal(out, ref * world + world * (world - 1) / 2):
+        bad.append(("reduce_scatter", blk))
+    part = torch.full((blk,), float(rank), device="cuda")
+    full = torch.empty(blk * world, device="cuda")
+    dist.all_gather_into_tensor(full, part)
+    if not torch.equal(full, torch.arange(world, device="cuda", dtype=torch.float32).repeat_interleave(blk)):
+        bad.append(("all_gather", blk))
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+    if bad:
+        print(f"rank {rank}: wrong {bad}", flush=True)
+        sys.exit(1)
+    print(f"rank {rank}: ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

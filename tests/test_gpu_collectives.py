@@ -401,6 +401,39 @@ def test_group_ll_rs_ag_fused(monkeypatch):
             c.destroy()
 
 
+def test_torch_process_group_dropin():
+    """The drop-in boundary from the reference's own caller:
+    torch.distributed's "nccl" backend with libvccl.so preloaded — its
+    ncclCommInitRankConfig / ncclAllReduce / ncclReduceScatter /
+    ncclAllGather calls land in this library — runs all_reduce (sum, avg,
+    max), reduce_scatter_tensor and all_gather_into_tensor exactly on 2 ranks
+    sharing cuda:0 (which RCCL refuses); the library's own INFO lines
+    (VCCL_DEBUG=INFO) prove it served the calls (tests/mp_torch_pg_worker.py)."""
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    vlib = os.path.join(ROOT, "vccl_amd", "lib", "libvccl.so")
+    port = str(29700 + os.getpid() % 200)
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, LD_PRELOAD=f"{tlib}:{vlib}", VCCL_ALLOW_SHARED_DEVICE="1",
+                   VCCL_SPIN_TIMEOUT_S="20", VCCL_DEBUG="INFO", TORCH_NCCL_ASYNC_ERROR_HANDLING="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_torch_pg_worker.py")],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=240)[0].decode(errors="replace"))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    tails = "\n".join(o[-2500:] for o in outs)
+    assert [p.returncode for p in procs] == [0, 0], tails
+    for o in outs:
+        assert "ok" in o.splitlines()[-1], tails
+        assert "[vccl" in o and "AllReduce: opCount" in o, tails  # served by this library
+
+
 def test_graph_capture_replay():
     """Collectives captured into a HIP graph replay correctly (device-resident
     LL epoch and ring step counters; no host state baked into the graph)."""
