@@ -428,6 +428,10 @@ def test_torch_process_group_dropin():
                 q.kill()
             raise
     tails = "\n".join(o[-2500:] for o in outs)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    for r, o in enumerate(outs):  # the evidence: this library's own log lines per rank
+        with open(os.path.join(ROOT, "gpurun_out", f"torch_dropin_rank{r}.txt"), "w") as f:
+            f.write("\n".join(o.splitlines()[:300]))
     assert [p.returncode for p in procs] == [0, 0], tails
     for o in outs:
         assert "ok" in o.splitlines()[-1], tails
