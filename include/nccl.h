@@ -186,7 +186,42 @@ ncclResult_t pncclGroupStart(void);
 ncclResult_t  ncclGroupEnd(void);
 ncclResult_t pncclGroupEnd(void);
 
+/* ---- memory, registration and scalable init (nccl.h.in:104-111, :178-181,
+ * :208-217): exported so a caller linked against libnccl (PyTorch's nccl
+ * backend imports all of them) never reaches another library with this
+ * library's communicator.  ncclMemAlloc / Free = hipMalloc / hipFree;
+ * registration is a no-op (zero-copy registration is out of scope, buffers
+ * work unregistered; *handle = buff); ncclCommInitRankScalable = InitRankConfig
+ * on commIds[0]'s root. ---- */
+ncclResult_t  ncclMemAlloc(void** ptr, size_t size);
+ncclResult_t pncclMemAlloc(void** ptr, size_t size);
+ncclResult_t  ncclMemFree(void* ptr);
+ncclResult_t pncclMemFree(void* ptr);
+ncclResult_t  ncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
+    ncclUniqueId* commIds, ncclConfig_t* config);
+ncclResult_t pncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
+    ncclUniqueId* commIds, ncclConfig_t* config);
+ncclResult_t  ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
+ncclResult_t pncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
+ncclResult_t  ncclCommDeregister(const ncclComm_t comm, void* handle);
+ncclResult_t pncclCommDeregister(const ncclComm_t comm, void* handle);
+
+/* nccl.h.in:87-102 */
+typedef struct ncclSimInfo_v22200 {
+  size_t size;
+  unsigned int magic;
+  unsigned int version;
+  float estimatedTime;
+} ncclSimInfo_t;
+#define NCCL_SIM_INFO_INITIALIZER {                                         \
+  sizeof(ncclSimInfo_t), 0x74685283,                                        \
+  NCCL_VERSION(NCCL_MAJOR, NCCL_MINOR, NCCL_PATCH), NCCL_UNDEF_FLOAT }
+
 /* ---- out of scope: WARN + ncclInvalidUsage ---- */
+/* nccl.h.in:472-473: ends the group (nothing launched) without an estimate
+ * (the tuner's cost model is out of scope) */
+ncclResult_t  ncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
+ncclResult_t pncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
 /* nccl.h.in:312-315 */
 ncclResult_t  ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
     ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
@@ -215,6 +250,18 @@ ncclResult_t pncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, in
 /* nccl.h.in:173-174 */
 ncclResult_t  ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
 ncclResult_t pncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
+/* RCCL's all-to-all extensions (not VCCL API; PyTorch's ROCm build imports
+ * them): out of scope too */
+ncclResult_t  ncclAllToAll(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclAllToAll(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    ncclComm_t comm, hipStream_t stream);
+ncclResult_t  ncclAllToAllv(const void* sendbuff, const size_t sendcounts[], const size_t sdispls[],
+    void* recvbuff, const size_t recvcounts[], const size_t rdispls[], ncclDataType_t datatype,
+    ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclAllToAllv(const void* sendbuff, const size_t sendcounts[], const size_t sdispls[],
+    void* recvbuff, const size_t recvcounts[], const size_t rdispls[], ncclDataType_t datatype,
+    ncclComm_t comm, hipStream_t stream);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -85,6 +85,37 @@ def test_out_of_scope_calls_are_invalid_usage():
     assert L.ncclCommSplit(None, 0, 0, ctypes.byref(out), None) == nccl.ncclInvalidUsage
     assert out.value is None
     assert L.pncclSend(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage
+    # RCCL's all-to-all extensions (imported by PyTorch's ROCm build)
+    assert L.ncclAllToAll(vp(0x10), vp(0x10), ctypes.c_size_t(4), 7, None, None) == nccl.ncclInvalidUsage
+    assert L.ncclAllToAllv(vp(0x10), None, None, vp(0x10), None, None, 7, None, None) == nccl.ncclInvalidUsage
+
+
+def test_group_simulate_end_and_registration():
+    """ncclGroupSimulateEnd ends the group (nothing launched, no estimate:
+    out of scope); the next group is clean.  Registration needs a comm
+    (no-op otherwise); ncclCommInitRankScalable refuses an empty id list;
+    ncclMemAlloc of 0 bytes is a null pointer (no GPU needed for these)."""
+    L = nccl.lib()
+
+    class SimInfo(ctypes.Structure):
+        _fields_ = [("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
+                    ("estimatedTime", ctypes.c_float)]
+    info = SimInfo(ctypes.sizeof(SimInfo), 0x74685283, nccl.get_version(), 0.0)
+    assert L.ncclGroupSimulateEnd(ctypes.byref(info)) == nccl.ncclInvalidUsage  # not in a group
+    nccl.group_start()
+    assert L.ncclGroupSimulateEnd(ctypes.byref(info)) == nccl.ncclInvalidUsage
+    assert info.estimatedTime == -1.0
+    nccl.group_start()
+    nccl.group_end()  # the thread is out of the first group
+    h = ctypes.c_void_p()
+    assert L.ncclCommRegister(None, ctypes.c_void_p(0x10), ctypes.c_size_t(16), ctypes.byref(h)) == \
+        nccl.ncclInvalidArgument
+    assert L.ncclCommDeregister(None, None) == nccl.ncclInvalidArgument
+    out = ctypes.c_void_p(0x1234)
+    assert L.ncclCommInitRankScalable(ctypes.byref(out), 2, 0, 0, None, None) == nccl.ncclInvalidArgument
+    p = ctypes.c_void_p(0x1234)
+    assert L.ncclMemAlloc(ctypes.byref(p), ctypes.c_size_t(0)) == nccl.ncclSuccess and p.value is None
+    assert L.ncclMemFree(None) == nccl.ncclSuccess
 
 
 def test_group_with_failing_call_launches_nothing():

@@ -1286,6 +1286,13 @@ VCCL_EXPORT ncclResult_t ncclCommSplit(ncclComm_t, int, int, ncclComm_t* newcomm
   if (newcomm) *newcomm = nullptr;
   return out_of_scope("ncclCommSplit");
 }
+VCCL_EXPORT ncclResult_t ncclAllToAll(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) {
+  return out_of_scope("ncclAllToAll");
+}
+VCCL_EXPORT ncclResult_t ncclAllToAllv(const void*, const size_t[], const size_t[], void*, const size_t[],
+                                       const size_t[], ncclDataType_t, ncclComm_t, hipStream_t) {
+  return out_of_scope("ncclAllToAllv");
+}
 
 #define VCCL_ALIAS(name) __attribute__((alias(#name), visibility("default")))
 
@@ -1331,6 +1338,20 @@ VCCL_EXPORT ncclResult_t ncclGroupEnd(void) {
     return err;
   }
   return launch_group(tasks);
+}
+
+// nccl.h.in:472-473: ends the group like ncclGroupEnd but launches nothing;
+// the run-time estimate needs the tuner's cost model (out of scope).
+VCCL_EXPORT ncclResult_t ncclGroupSimulateEnd(ncclSimInfo_t* simInfo) {
+  if (tl_groupDepth == 0) {
+    VWARN("ncclGroupSimulateEnd: not in a group call.");
+    return ncclInvalidUsage;
+  }
+  if (--tl_groupDepth > 0) return ncclSuccess;
+  tl_groupError = ncclSuccess;
+  tl_tasks.clear();
+  if (simInfo) simInfo->estimatedTime = NCCL_UNDEF_FLOAT;
+  return out_of_scope("ncclGroupSimulateEnd");
 }
 
 VCCL_EXPORT ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar,
@@ -1411,6 +1432,11 @@ ncclResult_t pncclAllGather(const void*, void*, size_t, ncclDataType_t, ncclComm
     VCCL_ALIAS(ncclAllGather);
 ncclResult_t pncclGroupStart(void) VCCL_ALIAS(ncclGroupStart);
 ncclResult_t pncclGroupEnd(void) VCCL_ALIAS(ncclGroupEnd);
+ncclResult_t pncclGroupSimulateEnd(ncclSimInfo_t*) VCCL_ALIAS(ncclGroupSimulateEnd);
+ncclResult_t pncclAllToAll(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t)
+    VCCL_ALIAS(ncclAllToAll);
+ncclResult_t pncclAllToAllv(const void*, const size_t[], const size_t[], void*, const size_t[], const size_t[],
+                            ncclDataType_t, ncclComm_t, hipStream_t) VCCL_ALIAS(ncclAllToAllv);
 ncclResult_t pncclRedOpCreatePreMulSum(ncclRedOp_t*, void*, ncclDataType_t, ncclScalarResidence_t,
                                        ncclComm_t) VCCL_ALIAS(ncclRedOpCreatePreMulSum);
 ncclResult_t pncclRedOpDestroy(ncclRedOp_t, ncclComm_t) VCCL_ALIAS(ncclRedOpDestroy);

@@ -853,6 +853,47 @@ VCCL_EXPORT ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks,
   return comm_init_rank(comm, nranks, &commId, rank, dev, config);
 }
 
+// nccl.h.in:178-181: several roots spread the bootstrap of very large jobs;
+// one node needs one, so every rank joins the root of commIds[0] (the same
+// array on every rank).
+VCCL_EXPORT ncclResult_t ncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
+                                                  ncclUniqueId* commIds, ncclConfig_t* config) {
+  if (nId < 1 || !commIds) {
+    VWARN("ncclCommInitRankScalable: nId %d, commIds %p", nId, (void*)commIds);
+    return ncclInvalidArgument;
+  }
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  return comm_init_rank(newcomm, nranks, &commIds[0], myrank, dev, config);
+}
+
+// nccl.h.in:104-111: device memory for any buffer the library is handed.
+VCCL_EXPORT ncclResult_t ncclMemAlloc(void** ptr, size_t size) {
+  if (!ptr) return ncclInvalidArgument;
+  *ptr = nullptr;
+  if (size == 0) return ncclSuccess;
+  HIPCHECK(hipMalloc(ptr, size));
+  return ncclSuccess;
+}
+VCCL_EXPORT ncclResult_t ncclMemFree(void* ptr) {
+  if (ptr) HIPCHECK(hipFree(ptr));
+  return ncclSuccess;
+}
+
+// nccl.h.in:208-217: buffer registration enables zero-copy in the reference;
+// that is out of scope here and every collective works on
+// unregistered buffers, so registration is accepted and does nothing.
+VCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t, void** handle) {
+  NCCLCHECK(comm_check(comm, "ncclCommRegister"));
+  if (!handle) return ncclInvalidArgument;
+  *handle = buff;
+  return ncclSuccess;
+}
+VCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void*) {
+  NCCLCHECK(comm_check(comm, "ncclCommDeregister"));
+  return ncclSuccess;
+}
+
 VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
   if (!comms || ndev < 1) return ncclInvalidArgument;
   int ndevices = 0;
@@ -1001,6 +1042,12 @@ ncclResult_t pncclCommInitRank(ncclComm_t*, int, ncclUniqueId, int) VCCL_ALIAS(n
 ncclResult_t pncclCommInitRankConfig(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*)
     VCCL_ALIAS(ncclCommInitRankConfig);
 ncclResult_t pncclCommInitAll(ncclComm_t*, int, const int*) VCCL_ALIAS(ncclCommInitAll);
+ncclResult_t pncclCommInitRankScalable(ncclComm_t*, int, int, int, ncclUniqueId*, ncclConfig_t*)
+    VCCL_ALIAS(ncclCommInitRankScalable);
+ncclResult_t pncclMemAlloc(void**, size_t) VCCL_ALIAS(ncclMemAlloc);
+ncclResult_t pncclMemFree(void*) VCCL_ALIAS(ncclMemFree);
+ncclResult_t pncclCommRegister(const ncclComm_t, void*, size_t, void**) VCCL_ALIAS(ncclCommRegister);
+ncclResult_t pncclCommDeregister(const ncclComm_t, void*) VCCL_ALIAS(ncclCommDeregister);
 ncclResult_t pncclCommFinalize(ncclComm_t) VCCL_ALIAS(ncclCommFinalize);
 ncclResult_t pncclCommDestroy(ncclComm_t) VCCL_ALIAS(ncclCommDestroy);
 ncclResult_t pncclCommAbort(ncclComm_t) VCCL_ALIAS(ncclCommAbort);

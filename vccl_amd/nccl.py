@@ -44,6 +44,10 @@ EXPORTED = [
     "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders", "vcclGroupPlan", "vcclGroupPlanEx", "vcclAlgoSelection",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
+    "ncclGroupSimulateEnd", "ncclAllToAll", "ncclAllToAllv",
+    # memory / registration / scalable init (what a libnccl caller such as
+    # PyTorch's nccl backend imports)
+    "ncclMemAlloc", "ncclMemFree", "ncclCommInitRankScalable", "ncclCommRegister", "ncclCommDeregister",
 ]
 ALGO_NAMES = {0: "ring", 1: "ll", 2: "direct", 3: "one_rank", 4: "ll128"}
 
