@@ -8,7 +8,7 @@ ncclAllReduce, ncclReduceScatter, ncclAllGather, ncclGroupStart/End, ... to
 this library instead of RCCL.  Both ranks share cuda:0, which RCCL itself
 refuses; VCCL_ALLOW_SHARED_DEVICE=1 lets this library run it.  Checks
 all_reduce (sum, avg, max), reduce_scatter_tensor and all_gather_into_tensor
-exactly; exit 0 on success.  Rendezvous: RANK, WORLD_SIZE, MASTER_ADDR /
+exactly, and an all_reduce on a sub-group (new_group); exit 0 on success.  Rendezvous: RANK, WORLD_SIZE, MASTER_ADDR /
 MASTER_PORT (TCPStore carries ncclUniqueId)."""
 import os
 import sys
@@ -20,7 +20,9 @@ import torch.distributed as dist
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    # lazy communicator init (no device_id=): sub-groups then get their own
+    # ncclCommInitRankConfig instead of ncclCommSplit (out of scope)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
     bad = []
     # integer-valued inputs: exact in any fold order
     for n in (3, 4096, 1 << 20, 3 << 20):
@@ -49,6 +51,12 @@ def main():
     dist.all_gather_into_tensor(full, part)
     if not torch.equal(full, torch.arange(world, device="cuda", dtype=torch.float32).repeat_interleave(blk)):
         bad.append(("all_gather", blk))
+    # a sub-group (its own communicator; reversed rank order inside it)
+    sub = dist.new_group(list(range(world))[::-1])
+    w = torch.full((4099,), float(rank + 1), device="cuda")
+    dist.all_reduce(w, group=sub)
+    if not torch.equal(w, torch.full_like(w, world * (world + 1) / 2)):
+        bad.append(("sub_group", 4099))
     torch.cuda.synchronize()
     dist.destroy_process_group()
     if bad:
