@@ -205,6 +205,11 @@ ncclResult_t  ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, v
 ncclResult_t pncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
 ncclResult_t  ncclCommDeregister(const ncclComm_t comm, void* handle);
 ncclResult_t pncclCommDeregister(const ncclComm_t comm, void* handle);
+/* nccl.h.in:173-174: ranks of one color form a new communicator ordered by
+ * (key, parent rank); NCCL_SPLIT_NOCOLOR joins none (*newcomm = NULL).
+ * Collective over `comm`; config NULL = defaults. */
+ncclResult_t  ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
+ncclResult_t pncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
 
 /* nccl.h.in:87-102 */
 typedef struct ncclSimInfo_v22200 {
@@ -247,9 +252,6 @@ ncclResult_t  ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, in
     ncclComm_t comm, hipStream_t stream);
 ncclResult_t pncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int peer,
     ncclComm_t comm, hipStream_t stream);
-/* nccl.h.in:173-174 */
-ncclResult_t  ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
-ncclResult_t pncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config);
 /* RCCL's all-to-all extensions (not VCCL API; PyTorch's ROCm build imports
  * them): out of scope too */
 ncclResult_t  ncclAllToAll(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,

@@ -20,9 +20,12 @@ import torch.distributed as dist
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
-    # lazy communicator init (no device_id=): sub-groups then get their own
-    # ncclCommInitRankConfig instead of ncclCommSplit (out of scope)
-    dist.init_process_group("nccl", rank=rank, world_size=world)
+    # lazy communicator init: sub-groups get their own ncclCommInitRankConfig;
+    # eager (device_id=): torch splits the default communicator (ncclCommSplit)
+    if os.environ.get("VCCL_TEST_TORCH_INIT", "lazy") == "eager":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("nccl", rank=rank, world_size=world)
     bad = []
     # integer-valued inputs: exact in any fold order
     for n in (3, 4096, 1 << 20, 3 << 20):

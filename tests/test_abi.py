@@ -72,7 +72,7 @@ def test_null_comm_queries():
 
 
 def test_out_of_scope_calls_are_invalid_usage():
-    """ncclReduce / Bcast / Broadcast / Send / Recv / CommSplit are exported
+    """ncclReduce / Bcast / Broadcast / Send / Recv / AllToAll(v) are exported
     (include/nccl.h) so a libnccl-linked binary loads, and refuse loudly."""
     L = nccl.lib()
     vp = ctypes.c_void_p
@@ -81,8 +81,8 @@ def test_out_of_scope_calls_are_invalid_usage():
     assert L.ncclBroadcast(vp(0x10), vp(0x10), ctypes.c_size_t(4), 7, 0, None, None) == nccl.ncclInvalidUsage
     assert L.ncclSend(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage
     assert L.ncclRecv(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage
-    out = vp(0x1234)
-    assert L.ncclCommSplit(None, 0, 0, ctypes.byref(out), None) == nccl.ncclInvalidUsage
+    out = vp(0x1234)  # ncclCommSplit is implemented: a NULL parent is an invalid argument
+    assert L.ncclCommSplit(None, 0, 0, ctypes.byref(out), None) == nccl.ncclInvalidArgument
     assert out.value is None
     assert L.pncclSend(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage
     # RCCL's all-to-all extensions (imported by PyTorch's ROCm build)

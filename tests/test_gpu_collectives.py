@@ -401,14 +401,36 @@ def test_group_ll_rs_ag_fused(monkeypatch):
             c.destroy()
 
 
-def test_torch_process_group_dropin():
+@pytest.mark.parametrize("n", [2, 4])
+def test_comm_split(n):
+    """ncclCommSplit (nccl.h.in:173-174): by color with reversed keys, and
+    with NCCL_SPLIT_NOCOLOR on one rank — sub-communicator sizes and ranks as
+    the reference orders them, an exact all-reduce on each, the parent intact
+    (tests/mp_split_worker.py; n ranks sharing the GPU)."""
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    env.update(TEST_GEOM)
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_split_worker.py"),
+                               str(r), str(n), hexid], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+    outs = [p.communicate(timeout=240)[0].decode(errors="replace")[-2000:] for p in procs]
+    assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+
+
+@pytest.mark.parametrize("init", ["lazy", "eager"])
+def test_torch_process_group_dropin(init):
     """The drop-in boundary from the reference's own caller:
     torch.distributed's "nccl" backend with libvccl.so preloaded — its
     ncclCommInitRankConfig / ncclAllReduce / ncclReduceScatter /
     ncclAllGather calls land in this library — runs all_reduce (sum, avg,
     max), reduce_scatter_tensor and all_gather_into_tensor exactly on 2 ranks
-    sharing cuda:0 (which RCCL refuses); the library's own INFO lines
-    (VCCL_DEBUG=INFO) prove it served the calls (tests/mp_torch_pg_worker.py)."""
+    sharing cuda:0 (which RCCL refuses), and a sub-group — created with its
+    own ncclCommInitRankConfig (lazy init) or split from the default group's
+    communicator with ncclCommSplit (eager init, device_id=); the library's
+    own INFO lines (VCCL_DEBUG=INFO) prove it served the calls
+    (tests/mp_torch_pg_worker.py)."""
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
     vlib = os.path.join(ROOT, "vccl_amd", "lib", "libvccl.so")
     port = str(29700 + os.getpid() % 200)
@@ -416,7 +438,8 @@ def test_torch_process_group_dropin():
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=port, LD_PRELOAD=f"{tlib}:{vlib}", VCCL_ALLOW_SHARED_DEVICE="1",
-                   VCCL_SPIN_TIMEOUT_S="20", VCCL_DEBUG="INFO", TORCH_NCCL_ASYNC_ERROR_HANDLING="1")
+                   VCCL_SPIN_TIMEOUT_S="20", VCCL_DEBUG="INFO", TORCH_NCCL_ASYNC_ERROR_HANDLING="1",
+                   VCCL_TEST_TORCH_INIT=init)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_torch_pg_worker.py")],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = []
@@ -430,7 +453,7 @@ def test_torch_process_group_dropin():
     tails = "\n".join(o[-2500:] for o in outs)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     for r, o in enumerate(outs):  # the evidence: this library's own log lines per rank
-        with open(os.path.join(ROOT, "gpurun_out", f"torch_dropin_rank{r}.txt"), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", f"torch_dropin_{init}_rank{r}.txt"), "w") as f:
             f.write("\n".join(o.splitlines()[:300]))
     assert [p.returncode for p in procs] == [0, 0], tails
     for o in outs:

@@ -1282,10 +1282,6 @@ VCCL_EXPORT ncclResult_t ncclSend(const void*, size_t, ncclDataType_t, int, nccl
 VCCL_EXPORT ncclResult_t ncclRecv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) {
   return out_of_scope("ncclRecv");
 }
-VCCL_EXPORT ncclResult_t ncclCommSplit(ncclComm_t, int, int, ncclComm_t* newcomm, ncclConfig_t*) {
-  if (newcomm) *newcomm = nullptr;
-  return out_of_scope("ncclCommSplit");
-}
 VCCL_EXPORT ncclResult_t ncclAllToAll(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) {
   return out_of_scope("ncclAllToAll");
 }
@@ -1450,8 +1446,6 @@ ncclResult_t pncclSend(const void*, size_t, ncclDataType_t, int, ncclComm_t, hip
     VCCL_ALIAS(ncclSend);
 ncclResult_t pncclRecv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t)
     VCCL_ALIAS(ncclRecv);
-ncclResult_t pncclCommSplit(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*)
-    VCCL_ALIAS(ncclCommSplit);
 }
 
 extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count,

@@ -894,6 +894,50 @@ VCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void*) {
   return ncclSuccess;
 }
 
+// nccl.h.in:173-174 (src/init.cc ncclCommSplit): the ranks of `comm` with
+// one color form a new communicator, ranked by (key, parent rank); color
+// NCCL_SPLIT_NOCOLOR joins none (*newcomm = NULL).  Collective over the
+// parent: its bootstrap carries every rank's (color, key), then the new
+// roots' ids — the first member of each color hosts its group's root — and
+// the members initialise as with ncclCommInitRankConfig on the parent's
+// device (config NULL: the defaults).
+VCCL_EXPORT ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm,
+                                       ncclConfig_t* config) {
+  if (newcomm) *newcomm = nullptr;
+  NCCLCHECK(comm_check(comm, "ncclCommSplit"));
+  if (!newcomm) return ncclInvalidArgument;
+  if (color < NCCL_SPLIT_NOCOLOR) {
+    VWARN("ncclCommSplit: invalid color %d", color);
+    return ncclInvalidArgument;
+  }
+  const int n = comm->nRanks, me = comm->rank;
+  struct Entry {
+    int color, key;
+  };
+  std::vector<Entry> ents((size_t)n);
+  ents[me] = Entry{color, key};
+  if (n > 1) NCCLCHECK(bootstrap_allgather(comm->bootstrap, ents.data(), sizeof(Entry)));
+  std::vector<int> members;
+  if (color != NCCL_SPLIT_NOCOLOR)
+    for (int r = 0; r < n; r++)
+      if (ents[r].color == color) members.push_back(r);
+  std::stable_sort(members.begin(), members.end(),
+                   [&](int a, int b) { return ents[a].key < ents[b].key; });  // ties: parent rank
+  std::vector<ncclUniqueId> ids((size_t)n);
+  memset(ids.data(), 0, ids.size() * sizeof(ncclUniqueId));
+  if (!members.empty() && members[0] == me) NCCLCHECK(bootstrap_get_unique_id(&ids[me]));
+  if (n > 1) NCCLCHECK(bootstrap_allgather(comm->bootstrap, ids.data(), sizeof(ncclUniqueId)));
+  if (members.empty()) return ncclSuccess;
+  const int newRank = (int)(std::find(members.begin(), members.end(), me) - members.begin());
+  int old = -1;
+  HIPCHECK(hipGetDevice(&old));
+  if (old != comm->device) HIPCHECK(hipSetDevice(comm->device));
+  const ncclResult_t r =
+      comm_init_rank(newcomm, (int)members.size(), &ids[members[0]], newRank, comm->device, config);
+  if (old != comm->device) (void)hipSetDevice(old);
+  return r;
+}
+
 VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
   if (!comms || ndev < 1) return ncclInvalidArgument;
   int ndevices = 0;
@@ -1042,6 +1086,7 @@ ncclResult_t pncclCommInitRank(ncclComm_t*, int, ncclUniqueId, int) VCCL_ALIAS(n
 ncclResult_t pncclCommInitRankConfig(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*)
     VCCL_ALIAS(ncclCommInitRankConfig);
 ncclResult_t pncclCommInitAll(ncclComm_t*, int, const int*) VCCL_ALIAS(ncclCommInitAll);
+ncclResult_t pncclCommSplit(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*) VCCL_ALIAS(ncclCommSplit);
 ncclResult_t pncclCommInitRankScalable(ncclComm_t*, int, int, int, ncclUniqueId*, ncclConfig_t*)
     VCCL_ALIAS(ncclCommInitRankScalable);
 ncclResult_t pncclMemAlloc(void**, size_t) VCCL_ALIAS(ncclMemAlloc);

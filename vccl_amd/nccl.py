@@ -355,6 +355,13 @@ class Comm:
                                        ci(*[c[3] for c in calls]), out), "vcclCommGroupAlgos")
         return [ALGO_NAMES[a] for a in out]
 
+    def split(self, color: int, key: int):
+        """ncclCommSplit: the new communicator of this rank's color (None for
+        NCCL_SPLIT_NOCOLOR = -1).  Collective over this comm."""
+        h = ctypes.c_void_p()
+        check(lib().ncclCommSplit(self.handle, color, key, ctypes.byref(h), None), "ncclCommSplit")
+        return Comm(h.value) if h.value else None
+
     def set_algo(self, algo: str | None):
         """vcclCommSetAlgo: force "ring" | "ll" | "direct" | "ll128" for later calls; None = automatic."""
         code = -1 if algo is None else {v: k for k, v in ALGO_NAMES.items()}[algo]
