@@ -459,6 +459,8 @@ def test_torch_process_group_dropin(init):
     for o in outs:
         assert "ok" in o.splitlines()[-1], tails
         assert "[vccl" in o and "AllReduce: opCount" in o, tails  # served by this library
+        if init == "eager":  # torch split the default communicator for the sub-group
+            assert "ncclCommSplit: comm" in o, tails
 
 
 def test_graph_capture_replay():

@@ -927,6 +927,8 @@ VCCL_EXPORT ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, nccl
   memset(ids.data(), 0, ids.size() * sizeof(ncclUniqueId));
   if (!members.empty() && members[0] == me) NCCLCHECK(bootstrap_get_unique_id(&ids[me]));
   if (n > 1) NCCLCHECK(bootstrap_allgather(comm->bootstrap, ids.data(), sizeof(ncclUniqueId)));
+  VINFO("ncclCommSplit: comm %p rank %d color %d key %d -> %zu ranks", (void*)comm, me, color, key,
+        members.size());
   if (members.empty()) return ncclSuccess;
   const int newRank = (int)(std::find(members.begin(), members.end(), me) - members.begin());
   int old = -1;
