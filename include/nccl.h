@@ -9,11 +9,11 @@
  *
  * Scope: AllReduce / ReduceScatter / AllGather over the
  * repo's own transport (xGMI peer memory, no RCCL) and the comm lifecycle they
- * need.  The calls of the "out of scope" block at the end (Reduce, Bcast,
- * Broadcast, Send, Recv, CommSplit) are declared and exported so a binary
- * linked against libnccl still loads; each logs a WARN and returns
- * ncclInvalidUsage.  Other reference entry points (Register, MemAlloc,
- * InitRankScalable, ...) are not exported.
+ * need, including CommSplit, MemAlloc / MemFree, Register / Deregister (a
+ * no-op) and InitRankScalable.  The calls of the "out of scope" block at the
+ * end (Reduce, Bcast, Broadcast, Send, Recv, GroupSimulateEnd, RCCL's
+ * AllToAll / AllToAllv) are declared and exported so a binary linked against
+ * libnccl still loads; each logs a WARN and returns ncclInvalidUsage.
  */
 #ifndef VCCL_NCCL_H_
 #define VCCL_NCCL_H_
