@@ -9,10 +9,10 @@
  *
  * Scope: AllReduce / ReduceScatter / AllGather over the
  * repo's own transport (xGMI peer memory, no RCCL) and the comm lifecycle they
- * need, including CommSplit, MemAlloc / MemFree, Register / Deregister (a
- * no-op) and InitRankScalable.  The calls of the "out of scope" block at the
- * end (Reduce, Bcast, Broadcast, Send, Recv, GroupSimulateEnd, RCCL's
- * AllToAll / AllToAllv) are declared and exported so a binary linked against
+ * need, Broadcast / Bcast (the byte-copy ring), CommSplit, MemAlloc /
+ * MemFree, Register / Deregister (a no-op) and InitRankScalable.  The calls
+ * of the "out of scope" block at the end (Reduce, Send, Recv,
+ * GroupSimulateEnd, RCCL's AllToAll / AllToAllv) are declared and exported so a binary linked against
  * libnccl still loads; each logs a WARN and returns ncclInvalidUsage.
  */
 #ifndef VCCL_NCCL_H_
@@ -186,6 +186,20 @@ ncclResult_t pncclGroupStart(void);
 ncclResult_t  ncclGroupEnd(void);
 ncclResult_t pncclGroupEnd(void);
 
+/* ---- broadcast: the ring broadcast (src/device/broadcast.h), the byte-copy
+ * ring of the all-gather from one root (torch's DDP broadcasts its module
+ * state with it) ---- */
+/* nccl.h.in:326-329 (in place) */
+ncclResult_t  ncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root,
+    ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root,
+    ncclComm_t comm, hipStream_t stream);
+/* nccl.h.in:340-343 */
+ncclResult_t  ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    int root, ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    int root, ncclComm_t comm, hipStream_t stream);
+
 /* ---- memory, registration and scalable init (nccl.h.in:104-111, :178-181,
  * :208-217): exported so a caller linked against libnccl (PyTorch's nccl
  * backend imports all of them) never reaches another library with this
@@ -232,16 +246,6 @@ ncclResult_t  ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncc
     ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
 ncclResult_t pncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
     ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
-/* nccl.h.in:326-329 */
-ncclResult_t  ncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root,
-    ncclComm_t comm, hipStream_t stream);
-ncclResult_t pncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root,
-    ncclComm_t comm, hipStream_t stream);
-/* nccl.h.in:340-343 */
-ncclResult_t  ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
-    int root, ncclComm_t comm, hipStream_t stream);
-ncclResult_t pncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
-    int root, ncclComm_t comm, hipStream_t stream);
 /* nccl.h.in:403-406 */
 ncclResult_t  ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer,
     ncclComm_t comm, hipStream_t stream);

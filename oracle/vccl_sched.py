@@ -88,18 +88,20 @@ class CbdWork:
 
 
 def traffic_per_byte(coll, nranks):
-    return 2 if coll == "ar" else nranks
+    """ncclFuncTrafficPerByte (enqueue.cc:67-74): AR 2, RS / AG nRanks, else 1."""
+    return 2 if coll == "ar" else 1 if coll == "bc" else nranks
 
 
 def max_send_recv_count(coll, nranks, count):
-    return nranks * count if coll in ("ag", "rs") else count
+    return nranks * count if coll in ("ag", "rs") else count  # AR / broadcast: count
 
 
-def chunk_size(proto, buff_size=None):
-    """calcCollChunking for the RING algorithm (enqueue.cc:2027-2032, 2093)."""
+def chunk_size(proto, buff_size=None, coll="ar"):
+    """calcCollChunking for the RING algorithm (enqueue.cc:2027-2032, 2093);
+    broadcast: BROADCAST_CHUNKSTEPS 1 (collectives.h:23-24)."""
     buff = DEFAULT_BUFFSIZE[proto] if buff_size is None else buff_size
     step = buff // NCCL_STEPS
-    cs = step * (CHUNK_STEPS if proto == PROTO_SIMPLE else 1)
+    cs = step * (CHUNK_STEPS if proto == PROTO_SIMPLE and coll != "bc" else 1)
     if proto == PROTO_LL:
         cs //= 2
     if proto == PROTO_LL128:
@@ -130,9 +132,10 @@ def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPL
                  buff_size=None, nthreads=None) -> CbdWork:
     """scheduleCollTasksToPlan for a plan of one ring collective.
 
-    coll: "ar" | "rs" | "ag"; count: AR count, RS recvcount, AG sendcount (in
-    elements of elt_size; AG is rewritten to bytes here as taskAppend does)."""
-    if coll == "ag":
+    coll: "ar" | "rs" | "ag" | "bc"; count: AR count, RS recvcount, AG
+    sendcount, broadcast count (in elements of elt_size; AG and broadcast are
+    rewritten to bytes here as taskAppend does)."""
+    if coll in ("ag", "bc"):
         count, elt_size = count * elt_size, 1
     tpb = traffic_per_byte(coll, nranks)
     task_traffic = count * elt_size * tpb * (4 if proto == PROTO_LL else 1)   # enqueue.cc:418
@@ -180,7 +183,7 @@ def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPL
         count_lo -= excess
     n_channels = (1 if count_lo else 0) + n_mid + (1 if cells_hi else 0)
     g = grain_size(proto)
-    cs = chunk_size(proto, buff_size)  # ring: independent of nBytes (enqueue.cc:2034-2082)
+    cs = chunk_size(proto, buff_size, coll)  # ring: independent of nBytes (enqueue.cc:2034-2082)
     grains = cs // g
     return CbdWork(channel_id, channel_id + n_channels - 1, count_lo, count_mid, count_hi,
                    grains if count_lo else 0, grains if n_mid else 0, grains if count_hi else 0,
@@ -273,7 +276,7 @@ def _place(cur, coll, count, elt_size, nranks, proto, buff_size):
     else:
         c_lo -= excess
     n_ch = (1 if c_lo else 0) + n_mid + (1 if hi else 0)
-    grains = chunk_size(proto, buff_size) // grain_size(proto)
+    grains = chunk_size(proto, buff_size, coll) // grain_size(proto)
     work = CbdWork(ch, ch + n_ch - 1, c_lo, c_mid, c_hi, grains if c_lo else 0, grains if n_mid else 0,
                    grains if c_hi else 0, proto, elt_size)
     if c_hi:
@@ -302,7 +305,7 @@ def plan_schedule(calls, nranks, comm_channels, buff_size=None, nthreads=None, a
     ring call, "ll" as VCCL's LL (tree for the all-reduce, ring otherwise),
     "ll128" as the LL128 ring (ll128_buff / ll128_threads: VCCL's defaults).
     algos_out (a list) receives every call's path."""
-    calls = [GroupCall(c.coll, c.count * c.elt_size, 1, c.key, c.func) if c.coll == "ag" else c
+    calls = [GroupCall(c.coll, c.count * c.elt_size, 1, c.key, c.func) if c.coll in ("ag", "bc") else c
              for c in calls]
     traffic = [c.count * c.elt_size * traffic_per_byte(c.coll, nranks) for c in calls]
     bins = [[] for _ in range(SORTER_BINS)]

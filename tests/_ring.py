@@ -101,8 +101,8 @@ def _group_calls(calls, n):
     gc = []
     for coll, op, dt, count in calls:
         esz = np.dtype(O.NP_DTYPE[dt]).itemsize
-        if coll == "ag":
-            key = func = ("ag", 0, 0)
+        if coll in ("ag", "bc"):  # byte copies
+            key = func = (coll, 0, 0)
         else:
             dev_op, _ = O.host_to_dev_redop(op, dt, n)
             key = (coll, dev_op, dt)
@@ -121,7 +121,7 @@ def group_works(calls, n, nch, slot_bytes=512 << 10, nthreads=512, algos=None):
                            nthreads=nthreads, algo_of=algo_of)[2]
 
 
-_COLL_CODE = {"ar": 0, "rs": 1, "ag": 2}
+_COLL_CODE = {"ar": 0, "rs": 1, "ag": 2, "bc": 3}
 
 
 def group_algos(calls, n, coll_algo):
@@ -133,7 +133,7 @@ def group_algos(calls, n, coll_algo):
     out = []
     def algo_of(i, agg):
         coll, op, dt, count = calls[i]
-        return coll_algo(_COLL_CODE[coll], agg, 0 if coll == "ag" else dt)
+        return coll_algo(_COLL_CODE[coll], agg, 0 if coll in ("ag", "bc") else dt)
     S.plan_schedule(_group_calls(calls, n), n, 1, nthreads=512, algo_of=algo_of, algos_out=out)
     return out
 
@@ -146,6 +146,10 @@ def select_algo(policy, coll, esz, count, n):
         return "ring"
     if policy["force"] == 4:
         return "ll128" if policy["ll128"] else "ring"
+    if coll == "bc":  # the ring broadcast: SIMPLE, or the LL128 window
+        nb = count * esz
+        return "ll128" if policy["ll128"] and policy["ll128_max"] and policy["ll128_min"] <= nb <= policy["ll128_max"] \
+            else "ring"
     block = count * esz
     nbytes = block if coll == "ar" else block * n
     if coll == "ar":

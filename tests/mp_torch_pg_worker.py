@@ -8,7 +8,9 @@ ncclAllReduce, ncclReduceScatter, ncclAllGather, ncclGroupStart/End, ... to
 this library instead of RCCL.  Both ranks share cuda:0, which RCCL itself
 refuses; VCCL_ALLOW_SHARED_DEVICE=1 lets this library run it.  Checks
 all_reduce (sum, avg, max), reduce_scatter_tensor and all_gather_into_tensor
-exactly, and an all_reduce on a sub-group (new_group); exit 0 on success.  Rendezvous: RANK, WORLD_SIZE, MASTER_ADDR /
+exactly, broadcast, a DistributedDataParallel step (state broadcast at
+construction, gradient-bucket all-reduce in backward) and an all_reduce on a
+sub-group (new_group); exit 0 on success.  Rendezvous: RANK, WORLD_SIZE, MASTER_ADDR /
 MASTER_PORT (TCPStore carries ncclUniqueId)."""
 import os
 import sys
@@ -54,6 +56,25 @@ def main():
     dist.all_gather_into_tensor(full, part)
     if not torch.equal(full, torch.arange(world, device="cuda", dtype=torch.float32).repeat_interleave(blk)):
         bad.append(("all_gather", blk))
+    # broadcast (ncclBroadcast) and DDP: construction broadcasts rank 0's
+    # module state, backward all-reduces the gradient buckets (the path this
+    # library is built for); grads of sum(model(x_r)) with x_r = r + 1 average
+    # to exact values
+    b = torch.full((1234,), float(rank * 10 + 1), device="cuda")
+    dist.broadcast(b, src=world - 1)
+    if not torch.equal(b, torch.full_like(b, float((world - 1) * 10 + 1))):
+        bad.append(("broadcast", 1234))
+    torch.manual_seed(rank)
+    model = torch.nn.Linear(64, 32).cuda()
+    torch.manual_seed(0)
+    ref = torch.nn.Linear(64, 32).cuda()  # rank 0's initial state
+    ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0])
+    if not (torch.equal(ddp.module.weight, ref.weight) and torch.equal(ddp.module.bias, ref.bias)):
+        bad.append(("ddp broadcast", 0))
+    ddp(torch.full((8, 64), float(rank + 1), device="cuda")).sum().backward()
+    gw = torch.full((32, 64), 8.0 * (world + 1) / 2, device="cuda")
+    if not (torch.equal(ddp.module.weight.grad, gw) and torch.equal(ddp.module.bias.grad, torch.full((32,), 8.0, device="cuda"))):
+        bad.append(("ddp grads", 0))
     # a sub-group (its own communicator; reversed rank order inside it)
     sub = dist.new_group(list(range(world))[::-1])
     w = torch.full((4099,), float(rank + 1), device="cuda")

@@ -401,6 +401,32 @@ def test_group_ll_rs_ag_fused(monkeypatch):
             c.destroy()
 
 
+@pytest.mark.parametrize("n,geom", [(2, "test"), (3, "test"), (4, "test"), (4, "ll128"), (2, "default")])
+def test_broadcast(n, geom):
+    """ncclBroadcast / ncclBcast (broadcast.h ring, bytes): 1 B - 24 MiB,
+    every root, out of place and in place, and a group of broadcasts from
+    different roots fused with an all-reduce; every byte exact
+    (tests/mp_bcast_worker.py; n ranks sharing the GPU; "ll128": the LL128
+    ring)."""
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    if geom == "default":
+        for k in TEST_GEOM:
+            env.pop(k, None)
+        env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
+    else:
+        env.update(TEST_GEOM)
+        if geom == "ll128":
+            env["NCCL_PROTO"] = "LL128"
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_bcast_worker.py"),
+                               str(r), str(n), hexid], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+    outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+    assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_comm_split(n):
     """ncclCommSplit (nccl.h.in:173-174): by color with reversed keys, and

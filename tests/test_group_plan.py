@@ -24,7 +24,7 @@ from oracle import vccl_sched as S
 from tests import _ring
 from vccl_amd import nccl
 
-COLL = {0: "ar", 1: "rs", 2: "ag"}
+COLL = {0: "ar", 1: "rs", 2: "ag", 3: "bc"}
 ESZ = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2, 10: 1, 11: 1}
 
 
@@ -34,8 +34,8 @@ def _oracle_calls(calls, n):
     equivalence (generate.py:129-137)."""
     out = []
     for coll, count, dt, op in calls:
-        if coll == 2:
-            key = func = (2, 0, 0)
+        if coll in (2, 3):  # byte copies (AG, broadcast)
+            key = func = (coll, 0, 0)
         else:
             dev_op, _ = nccl.host_to_dev_redop(op, dt, n)
             key = (coll, dev_op, dt)
@@ -207,7 +207,7 @@ def _check_equal_ex(calls, n, nch, policy, slot=512 << 10, nthreads=512):
 
     def algo_of(i, agg):
         coll, _, dt, _ = calls[i]
-        return _ring.select_algo(policy, COLL[coll], 1 if coll == 2 else ESZ[dt], agg, n)
+        return _ring.select_algo(policy, COLL[coll], 1 if coll in (2, 3) else ESZ[dt], agg, n)
     o_algos = []
     o_order, o_plan, o_works = S.plan_schedule(_oracle_calls(calls, n), n, nch, buff_size=slot * S.NCCL_STEPS,
                                                nthreads=nthreads, algo_of=algo_of, algos_out=o_algos)
@@ -229,7 +229,7 @@ def test_library_group_plan_ex_equals_oracle(n):
         k = int(rng.integers(1, 21))
         calls = []
         for _ in range(k):
-            coll = int(rng.integers(0, 3))
+            coll = int(rng.integers(0, 4))  # incl. broadcast
             dt = int(rng.choice([7, 9, 6, 2, 0, 8]))
             op = int(rng.choice([0, 1, 2, 3]))
             count = int(rng.choice([1, 100, 4096, 16384, 40_000, 65_536, 300_000, 1 << 20, 3 << 20])) \
@@ -303,3 +303,17 @@ def test_single_call_ll_partition():
                     assert lib[:5] == ref[:5], (n, nch, count, dt, nt, lib, ref)
                     assert lib[5] == ref[5] == 32768 // ESZ[dt]  # half a VCCL LL step
 
+
+
+def test_broadcast_partition():
+    """The ring broadcast's partition (traffic 1 per byte, one FIFO step per
+    chunk, BROADCAST_CHUNKSTEPS, collectives.h:23-24; bytes on the wire):
+    library (vcclRingPartition coll 3) == oracle."""
+    for n in (2, 4, 8):
+        for nch in (1, 14, 56, 64):
+            for count, dt in ((1, 7), (1000, 7), (300_001, 9), (1 << 22, 0), ((1 << 24) + 3, 6)):
+                for nt in (256, 512):
+                    lib = nccl.ring_partition(3, count, dt, n, nch, 512 << 10, nt)
+                    w = S.cbd_schedule("bc", count, ESZ[dt], n, nch, buff_size=(512 << 10) * 8, nthreads=nt)
+                    ref = _as_tuple(w)
+                    assert lib[:5] == ref[:5] and lib[5] == ref[5] == 512 << 10, (n, nch, count, dt, lib, ref)

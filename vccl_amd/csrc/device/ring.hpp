@@ -510,4 +510,37 @@ __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
   }
 }
 
+// ----------------------------------------------------------------- Broadcast
+// broadcast.h:12-60 (runRing): byte copies along the ring from the root —
+// the root sends (copying to its output when out of place), every other
+// rank receives into its output and forwards, the root's predecessor only
+// receives.  One FIFO step per chunk (BROADCAST_CHUNKSTEPS 1).
+template <int UNROLL, int PROTO = kProtoSimple>
+__device__ void ring_broadcast(RingCtx& r, const RingWork& w, int c) {
+  using Fn = FnCopy<uint8_t>;
+  const Fn fn(0);
+  int64_t partOff, partCount, chunkCount;
+  if (!cbd_part(w, c, &partOff, &partCount, &chunkCount)) return;
+  const uint8_t* in = (const uint8_t*)w.sendbuff;
+  uint8_t* out = (uint8_t*)w.recvbuff;
+  const int me = r.ch->ringRanks[0], next = r.ch->ringRanks[1];
+  for (int64_t eo = 0; eo < partCount; eo += chunkCount) {
+    const int64_t nelem = partCount - eo < chunkCount ? partCount - eo : chunkCount;
+    const int64_t off = partOff + eo;
+    // the chunk travels at its offset's misalignment inside the slots (the
+    // same on every rank, so sender and receiver agree)
+    const int m = (int)(off & 15);
+    if (me == w.root) {
+      if (in == out)
+        ring_step<Fn, false, true, true, false, UNROLL, PROTO>(r, fn, in + off, nullptr, nelem, false, 0, m);
+      else
+        ring_step<Fn, false, true, true, true, UNROLL, PROTO>(r, fn, in + off, out + off, nelem, false, 0, m);
+    } else if (next == w.root) {
+      ring_step<Fn, true, false, false, true, UNROLL, PROTO>(r, fn, nullptr, out + off, nelem, false, m, 0);
+    } else {
+      ring_step<Fn, true, true, false, true, UNROLL, PROTO>(r, fn, nullptr, out + off, nelem, false, m, m);
+    }
+  }
+}
+
 }  // namespace vccl

@@ -52,7 +52,8 @@ __device__ __forceinline__ void ring_run(RingCtx& r, const Fn& fn, const RingWor
   if constexpr (COLL == kCollAllReduce) ring_allreduce<Fn, UNROLL, PROTO>(r, fn, w, blockIdx.x);
   else if constexpr (COLL == kCollReduceScatter)
     ring_reducescatter<Fn, UNROLL, PROTO>(r, fn, w, blockIdx.x);
-  else ring_allgather<UNROLL, PROTO>(r, w, blockIdx.x);
+  else if constexpr (COLL == kCollAllGather) ring_allgather<UNROLL, PROTO>(r, w, blockIdx.x);
+  else ring_broadcast<UNROLL, PROTO>(r, w, blockIdx.x);
 }
 
 // One launch = 1 .. kRingMaxWorks calls (RingBatch, group aggregation): the
@@ -97,8 +98,11 @@ hipError_t VCCL_RING_LAUNCH<VCCL_KT>(int coll, int devOp, const RingBatch& w, in
   using T = typename KTypeOf<VCCL_KT>::T;
   hipError_t err = hipErrorInvalidValue;
   dim3 grid(w.w.nChannels), block(nthreads);
-  if (coll == kCollAllGather) {
+  if (coll == kCollAllGather || coll == kCollBroadcast) {  // byte copies: the K_U8 unit only
     if constexpr (VCCL_KT == K_U8) {
+      if (coll == kCollBroadcast)
+        return launch_k(k_ring<kCollBroadcast, FnCopy<uint8_t>, VCCL_AG_UNROLL, kPartProto>, grid, block, stream,
+                        stop, w);
       return launch_k(k_ring<kCollAllGather, FnCopy<uint8_t>, VCCL_AG_UNROLL, kPartProto>, grid, block, stream,
                       stop, w);
     }

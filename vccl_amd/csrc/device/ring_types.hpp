@@ -180,7 +180,7 @@ struct RingWork {
   DevChannel* channels;              // device-resident, nChannels entries
   const void* sendbuff;
   void* recvbuff;
-  uint64_t count;                    // AR: count; RS: recvcount; AG: bytes per rank
+  uint64_t count;                    // AR: count; RS: recvcount; AG: bytes per rank; BC: bytes
   uint64_t redArg;                   // device op argument (also the preOp scalar)
   const void* redArgPtr;             // ncclScalarDevice scalar (read on device)
   int redArgBytes;
@@ -200,6 +200,7 @@ struct RingWork {
   int64_t chunkLo, chunkMid, chunkHi;
   // LL128 ring (proto = kProtoLL128): bytes per LL128 FIFO slot
   int64_t ll128SlotBytes;
+  int root;                          // broadcast: the root's rank
 };
 
 // Protocols of the ring kernels (nccl_common.h ids).
@@ -240,6 +241,7 @@ struct RingPart {
   const void* sendbuff;
   void* recvbuff;
   uint64_t count;
+  int root;
   int channelLo, channelHi;
   int64_t countLo, countMid, countHi;
   int64_t chunkLo, chunkMid, chunkHi;
@@ -250,13 +252,14 @@ struct RingBatch {
   RingPart more[kRingMaxWorks - 1];  // parts 1 .. nParts-1
 };
 __host__ __device__ inline RingPart ring_part_of(const RingWork& w) {
-  return RingPart{w.sendbuff, w.recvbuff, w.count, w.channelLo, w.channelHi, w.countLo,
+  return RingPart{w.sendbuff, w.recvbuff, w.count, w.root, w.channelLo, w.channelHi, w.countLo,
                   w.countMid, w.countHi, w.chunkLo, w.chunkMid, w.chunkHi};
 }
 __host__ __device__ inline RingWork ring_work_with(RingWork w, const RingPart& p) {
   w.sendbuff = p.sendbuff;
   w.recvbuff = p.recvbuff;
   w.count = p.count;
+  w.root = p.root;
   w.channelLo = p.channelLo;
   w.channelHi = p.channelHi;
   w.countLo = p.countLo;

@@ -26,7 +26,9 @@
 
 namespace vccl {
 
-enum Coll { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2 };
+enum Coll { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2, kBroadcast = 3 };
+// Byte-copy collectives: the host rewrites them as int8 (enqueue.cc:2400-2404).
+static inline bool is_copy_coll(int coll) { return coll == kAllGather || coll == kBroadcast; }
 
 // One call's part of VCCL's channel partition (ncclDevWorkColl channelLo /
 // channelHi + cbd, device.h:258-287): channels [channelLo, channelHi] carry
@@ -47,6 +49,7 @@ struct Task {
   int devOp;
   uint64_t arg;
   const void* argPtr;  // ncclScalarDevice PreMulSum scalar
+  int root;            // broadcast
   ncclComm* comm;
   hipStream_t stream;
   // Set by the group planner (launch_planned): this call's partition inside
@@ -319,7 +322,7 @@ static hipEvent_t stream_last_event(ncclComm* comm, const CaptureState& cs) {
 // ncclLaunchOneRank (onerank.cu:47-83): a copy, or the PreMulSum kernel.
 static ncclResult_t launch_one_rank(const Task& t) {
   const size_t bytes = t.count * (size_t)type_size(t.datatype);
-  if (t.coll == kAllGather || t.devOp != OP_PREMULSUM) {  // AG: a plain copy
+  if (is_copy_coll(t.coll) || t.devOp != OP_PREMULSUM) {  // AG: a plain copy
     if (t.recvbuff == t.sendbuff) return ncclSuccess;
     // Small buckets: the library's own byte-copy kernel (one launch) — a
     // hipMemcpyAsync D2D costs more host time than the whole 1 KiB copy
@@ -364,7 +367,7 @@ static ncclResult_t launch_one_rank(const Task& t) {
 constexpr uint64_t kMinTraffic = 16 << 10;  // MinTrafficPerChannel, enqueue.cc:528
 static int64_t div_up(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static int64_t traffic_per_byte(int coll, int nRanks) {  // ncclFuncTrafficPerByte (enqueue.cc:67-74)
-  return coll == kAllReduce ? 2 : nRanks;
+  return coll == kAllReduce ? 2 : coll == kBroadcast ? 1 : nRanks;
 }
 
 // nMaxChannels of a task (or of an aggregate of tasks, ncclPrepareTasks):
@@ -378,7 +381,8 @@ static int ring_nmax_channels(int coll, int64_t count, int64_t eltSize, int nRan
                               int proto, int64_t nThreads) {
   const int64_t threshold = proto == kProtoSimple ? 64
                             : proto == kProtoLL128 || coll == kAllReduce ? 8 : 8 * (int64_t)nRanks;
-  const int64_t nBytes = eltSize * (coll == kAllReduce ? count : (int64_t)nRanks * count);
+  // ncclFuncMaxSendRecvCount (enqueue.h:36-38): RS / AG move n blocks
+  const int64_t nBytes = eltSize * (coll == kAllReduce || coll == kBroadcast ? count : (int64_t)nRanks * count);
   int64_t nc = commChannels;
   while (nBytes < nc * nThreads * threshold && nc >= 2) nc--;
   return (int)nc;
@@ -449,8 +453,10 @@ static CbdPlan cbd_place(PlanCursor& pc, int coll, int64_t count, int64_t eltSiz
   // LL128 = one step, 15/16 of it data; LL = half a step; rounded down to
   // the protocol grain (device.h:290-295: SIMPLE 512, LL128 1920, LL 16);
   // independent of size.
+  // (broadcast: BROADCAST_CHUNKSTEPS 1, collectives.h:23-24)
   const int64_t grain = ll128 ? 1920 : ll ? 16 : 512;
-  const int64_t chunkBytes = ll128 ? stepBytes / 16 * 15 : ll ? stepBytes / 2 : 4 * stepBytes;
+  const int64_t chunkBytes =
+      ll128 ? stepBytes / 16 * 15 : ll ? stepBytes / 2 : (coll == kBroadcast ? 1 : 4) * stepBytes;
   const int64_t chunkElts = chunkBytes / grain * grain / eltSize;
   p.chunkLo = p.chunkMid = p.chunkHi = chunkElts;
   // advance the cursor (enqueue.cc:667-681)
@@ -521,6 +527,10 @@ static int select_algo(const AlgoPolicy& p, int coll, int64_t eltSize, int64_t c
   if (p.nRanks < 2 || p.algoForce == 1) return kAlgoRing;
   // NCCL_PROTO=LL128 (or vcclCommSetAlgo): the LL128 ring for every size
   if (p.algoForce == 4) return p.ll128 ? kAlgoRingLL128 : kAlgoRing;
+  if (coll == kBroadcast) {  // the ring broadcast (broadcast.h), SIMPLE or the LL128 window
+    const uint64_t bytes = (uint64_t)(count * eltSize);
+    return p.ll128 && p.ll128Max && bytes >= p.ll128Min && bytes <= p.ll128Max ? kAlgoRingLL128 : kAlgoRing;
+  }
   const uint64_t block = (uint64_t)(count * eltSize);
   // Reduce-scatter / all-gather: one rank's block must fit an LL slot; the
   // thresholds are on the whole bucket (n blocks), as the reference's tuner
@@ -702,13 +712,19 @@ static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commCha
   }
 }
 
+static int dev_coll(int coll) {
+  return coll == kAllReduce ? kCollAllReduce
+         : coll == kReduceScatter ? kCollReduceScatter
+         : coll == kBroadcast ? kCollBroadcast : kCollAllGather;
+}
+
 // A call's partition: its place in its group's plan (launch_planned, under
 // the protocol of the path its aggregate took — the caller asks for that
 // same protocol), else the plan of the call alone under `proto`.
 static CbdPlan task_plan(const Task& t, int proto) {
   const ncclComm* comm = t.comm;
   if (t.planned) return t.plan;
-  const bool ag = t.coll == kAllGather;
+  const bool ag = is_copy_coll(t.coll);
   const int64_t esz = ag ? 1 : type_size(t.datatype);
   const int64_t count = ag ? (int64_t)t.count * type_size(t.datatype) : (int64_t)t.count;
   if (proto == kProtoLL128)
@@ -732,7 +748,7 @@ static ncclResult_t ring_work_of(const Task& t, bool ll128, RingWork* out, int* 
   w.slotBytes = comm->slotBytes;
   w.nRanks = comm->nRanks;
   int kt, devOp = t.devOp;
-  if (t.coll == kAllGather) {
+  if (is_copy_coll(t.coll)) {
     w.count = t.count * (uint64_t)type_size(t.datatype);  // bytes (enqueue.cc:2400-2404)
     kt = K_U8;
     devOp = OP_COPY;
@@ -743,6 +759,7 @@ static ncclResult_t ring_work_of(const Task& t, bool ll128, RingWork* out, int* 
   }
   w.redArgPtr = t.argPtr;  // ncclScalarDevice: dereferenced by the kernel (nccl.h.in:255-262)
   w.redArgBytes = type_size(t.datatype);
+  w.root = t.root;
   const CbdPlan p = ll128 ? task_plan(t, kProtoLL128) : task_plan(t, kProtoSimple);
   if (p.channelHi >= comm->nChannels || p.channelLo < 0 || p.channelLo > p.channelHi)
     return ncclInternalError;
@@ -781,8 +798,7 @@ static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128, hipEvent
     b.w.nChannels = std::max(b.w.nChannels, wi.nChannels);
   }
   b.nParts = nTasks;
-  const int coll = t.coll == kAllReduce ? kCollAllReduce
-                   : t.coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
+  const int coll = dev_coll(t.coll);
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
     case K_U8: e = ring_launch_any<K_U8>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
@@ -819,9 +835,6 @@ static hipError_t by_kernel_type(int kt, F&& f) {
   return hipErrorInvalidValue;
 }
 
-static int dev_coll(int coll) {
-  return coll == kAllReduce ? kCollAllReduce : coll == kReduceScatter ? kCollReduceScatter : kCollAllGather;
-}
 
 // The cbd partition of a reduce-scatter's block, for the one-hop LL / direct
 // reduce-scatters' per-channel fold order: the ring's, under VCCL's protocol
@@ -1011,7 +1024,7 @@ static ncclResult_t launch_task(const Task& t) {
   // A one-rank in-place call without a preOp enqueues nothing (onerank.cu:
   // 47-83): no stream bookkeeping either.
   if (t.comm->nRanks == 1 && t.sendbuff == t.recvbuff &&
-      (t.coll == kAllGather || t.devOp != OP_PREMULSUM)) {
+      (is_copy_coll(t.coll) || t.devOp != OP_PREMULSUM)) {
     t.comm->opCount++;
     if (old != t.comm->device) (void)hipSetDevice(old);
     return ncclSuccess;
@@ -1053,7 +1066,7 @@ static int fuse_key_algo(const Task& t) { return t.comm->nRanks > 1 ? choose_alg
 // Same comm, collective, kernel type and op (the caller compares the paths).
 static bool fusable(const Task& a, const Task& b) {
   if (a.comm != b.comm || a.coll != b.coll) return false;
-  if (a.coll == kAllGather) return true;  // byte copies: any type
+  if (is_copy_coll(a.coll)) return true;  // byte copies: any type
   return a.datatype == b.datatype && a.devOp == b.devOp && a.arg == b.arg && a.argPtr == b.argPtr;
 }
 static int max_parts(int algo) {
@@ -1122,7 +1135,7 @@ static ncclResult_t launch_planned(std::vector<Task>& tasks, const std::vector<i
   std::vector<GroupTask> g;
   for (int j : idx) {
     const Task& t = tasks[j];
-    const bool ag = t.coll == kAllGather;
+    const bool ag = is_copy_coll(t.coll);
     const int tsz = type_size(t.datatype);
     const int op = ag ? OP_SUM : t.devOp;  // AG: int8 copies (enqueue.cc:2400-2404)
     const int dt = ag ? (int)ncclInt8 : (int)t.datatype;
@@ -1207,14 +1220,19 @@ static ncclResult_t launch_group(std::vector<Task>& tasks) {
 
 static ncclResult_t enqueue_check_impl(int coll, const char* name, const void* sendbuff,
                                        void* recvbuff, size_t count, ncclDataType_t dt,
-                                       ncclRedOp_t op, ncclComm* comm, hipStream_t stream) {
+                                       ncclRedOp_t op, ncclComm* comm, hipStream_t stream, int root) {
   NCCLCHECK(comm_check(comm, name));
-  NCCLCHECK(args_check(comm, name, dt, op, coll != kAllGather));
+  if (coll == kBroadcast && (root < 0 || root >= comm->nRanks)) {  // argcheck.cc:66-69
+    VWARN("%s : invalid root %d (root should be in the 0..%d range)", name, root, comm->nRanks);
+    return ncclInvalidArgument;
+  }
+  NCCLCHECK(args_check(comm, name, dt, op, !is_copy_coll(coll)));
   VINFO("%s: opCount %lx sendbuff %p recvbuff %p count %zu datatype %d op %d comm %p [nranks=%d] stream %p",
         name, (unsigned long)comm->opCount, sendbuff, recvbuff, count, (int)dt, (int)op,
         (void*)comm, comm->nRanks, (void*)stream);
   if (count == 0) return ncclSuccess;  // enqueue.cc:2372
-  if (!sendbuff || !recvbuff) {
+  // broadcast: a non-root's sendbuff is never read (argcheck.cc:76-78)
+  if (!recvbuff || (!sendbuff && !(coll == kBroadcast && comm->rank != root))) {
     VWARN("%s : NULL buffer", name);
     return ncclInvalidArgument;
   }
@@ -1226,8 +1244,9 @@ static ncclResult_t enqueue_check_impl(int coll, const char* name, const void* s
   t.datatype = dt;
   t.comm = comm;
   t.stream = stream;
-  if (coll != kAllGather) NCCLCHECK(resolve_op(comm, op, dt, &t.devOp, &t.arg, &t.argPtr));
+  if (!is_copy_coll(coll)) NCCLCHECK(resolve_op(comm, op, dt, &t.devOp, &t.arg, &t.argPtr));
   else t.devOp = OP_COPY;
+  t.root = root;
   if (*(volatile int*)comm->errorFlag) {
     comm->asyncError = ncclRemoteError;
     return ncclRemoteError;
@@ -1244,9 +1263,9 @@ static ncclResult_t enqueue_check_impl(int coll, const char* name, const void* s
 // group and returns that error (group.cc:528, :591).
 static ncclResult_t enqueue_check(int coll, const char* name, const void* sendbuff, void* recvbuff,
                                   size_t count, ncclDataType_t dt, ncclRedOp_t op, ncclComm* comm,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, int root = 0) {
   const ncclResult_t r =
-      enqueue_check_impl(coll, name, sendbuff, recvbuff, count, dt, op, comm, stream);
+      enqueue_check_impl(coll, name, sendbuff, recvbuff, count, dt, op, comm, stream, root);
   if (r != ncclSuccess && tl_groupDepth > 0 && tl_groupError == ncclSuccess) tl_groupError = r;
   return r;
 }
@@ -1268,13 +1287,7 @@ VCCL_EXPORT ncclResult_t ncclReduce(const void*, void*, size_t, ncclDataType_t, 
                                     ncclComm_t, hipStream_t) {
   return out_of_scope("ncclReduce");
 }
-VCCL_EXPORT ncclResult_t ncclBcast(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) {
-  return out_of_scope("ncclBcast");
-}
-VCCL_EXPORT ncclResult_t ncclBroadcast(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
-                                       hipStream_t) {
-  return out_of_scope("ncclBroadcast");
-}
+
 VCCL_EXPORT ncclResult_t ncclSend(const void*, size_t, ncclDataType_t, int, ncclComm_t,
                                   hipStream_t) {
   return out_of_scope("ncclSend");
@@ -1311,6 +1324,19 @@ VCCL_EXPORT ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, siz
                                        hipStream_t stream) {
   return enqueue_check(kAllGather, "AllGather", sendbuff, recvbuff, sendcount, datatype, ncclSum,
                        comm, stream);
+}
+
+// broadcast.h / collectives.cc:125-158: the ring broadcast, count elements of
+// datatype from root's sendbuff to every rank's recvbuff (bytes on the wire).
+VCCL_EXPORT ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count,
+                                       ncclDataType_t datatype, int root, ncclComm_t comm, hipStream_t stream) {
+  return enqueue_check(kBroadcast, "Broadcast", sendbuff, recvbuff, count, datatype, ncclSum, comm, stream,
+                       root);
+}
+// collectives.cc:112-123: the in-place broadcast
+VCCL_EXPORT ncclResult_t ncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root, ncclComm_t comm,
+                                   hipStream_t stream) {
+  return ncclBroadcast(buff, buff, count, datatype, root, comm, stream);
 }
 
 VCCL_EXPORT ncclResult_t ncclGroupStart(void) {
@@ -1451,14 +1477,14 @@ ncclResult_t pncclRecv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream
 extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count,
                                          ncclDataType_t datatype, int* algo) {
   NCCLCHECK(comm_check(comm, "vcclCommCollAlgo"));
-  if (!algo || coll < 0 || coll > 2 || type_size(datatype) < 1) return ncclInvalidArgument;
+  if (!algo || coll < 0 || coll > 3 || type_size(datatype) < 1) return ncclInvalidArgument;
   if (comm->nRanks == 1) {
     *algo = vcclAlgoOneRank;
     return ncclSuccess;
   }
   Task t{};
   t.comm = comm;
-  t.coll = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : kAllGather;
+  t.coll = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : coll == 2 ? kAllGather : kBroadcast;
   t.count = count;
   t.datatype = datatype;
   const int a = choose_algo(t);
@@ -1470,13 +1496,13 @@ extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count
 extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition(
     int coll, size_t count, ncclDataType_t datatype, int nRanks, int nChannels, int proto,
     size_t stepBytes, int nThreads, int64_t* out) {
-  if (!out || coll < 0 || coll > 2 || type_size(datatype) < 1 || nRanks < 1 ||
+  if (!out || coll < 0 || coll > 3 || type_size(datatype) < 1 || nRanks < 1 ||
       nChannels < 1 || nChannels > kMaxChannels || count == 0 || stepBytes < 4096 || nThreads < 64 ||
       (proto != kProtoSimple && proto != kProtoLL128 && proto != kProtoLL))
     return ncclInvalidArgument;
-  const int c = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : kAllGather;
-  const int64_t esz = c == kAllGather ? 1 : type_size(datatype);
-  const int64_t cnt = c == kAllGather ? (int64_t)count * type_size(datatype) : (int64_t)count;
+  const int c = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : coll == 2 ? kAllGather : kBroadcast;
+  const int64_t esz = is_copy_coll(c) ? 1 : type_size(datatype);
+  const int64_t cnt = is_copy_coll(c) ? (int64_t)count * type_size(datatype) : (int64_t)count;
   const CbdPlan p = cbd_schedule(c, cnt, esz, nRanks, nChannels, proto, (int64_t)stepBytes, nThreads);
   const int64_t v[8] = {p.channelLo, p.channelHi, p.countLo, p.countMid,
                         p.countHi,   p.chunkLo,   p.chunkMid, p.chunkHi};
@@ -1514,9 +1540,10 @@ static ncclResult_t group_plan_export(int nCalls, const int* colls, const size_t
   for (int i = 0; i < nCalls; i++) {
     const ncclDataType_t dt = (ncclDataType_t)datatypes[i];
     const int tsz = type_size(dt);
-    if (colls[i] < 0 || colls[i] > 2 || tsz < 1 || counts[i] == 0) return ncclInvalidArgument;
-    const int c = colls[i] == 0 ? kAllReduce : colls[i] == 1 ? kReduceScatter : kAllGather;
-    const bool ag = c == kAllGather;
+    if (colls[i] < 0 || colls[i] > 3 || tsz < 1 || counts[i] == 0) return ncclInvalidArgument;
+    const int c = colls[i] == 0 ? kAllReduce : colls[i] == 1 ? kReduceScatter : colls[i] == 2 ? kAllGather
+                                                                                            : kBroadcast;
+    const bool ag = is_copy_coll(c);
     int devOp = OP_SUM;
     uint64_t arg = 0;
     if (!ag) NCCLCHECK(host_to_dev_redop((ncclRedOp_t)ops[i], dt, nRanks, &devOp, &arg));

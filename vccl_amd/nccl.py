@@ -99,6 +99,7 @@ def lib() -> ctypes.CDLL:
         "ncclAllReduce": [vp, vp, c_size, c_int, c_int, vp, vp],
         "ncclReduceScatter": [vp, vp, c_size, c_int, c_int, vp, vp],
         "ncclAllGather": [vp, vp, c_size, c_int, vp, vp],
+        "ncclBroadcast": [vp, vp, c_size, c_int, c_int, vp, vp],
         "ncclGroupStart": [],
         "ncclGroupEnd": [],
         "vcclReduceCopy": [c_int, c_int, u64, c_int, c_int, c_int, ctypes.POINTER(vp), c_int,
@@ -336,6 +337,9 @@ class Comm:
 
     def all_gather(self, send: int, recv: int, sendcount: int, dtype: int, stream: int = 0):
         check(lib().ncclAllGather(send, recv, sendcount, dtype, self.handle, stream), "ncclAllGather")
+
+    def broadcast(self, send: int, recv: int, count: int, dtype: int, root: int, stream: int = 0):
+        check(lib().ncclBroadcast(send, recv, count, dtype, root, self.handle, stream), "ncclBroadcast")
 
     def coll_algo(self, coll: int, count: int, dtype: int) -> str:
         """vcclCommCollAlgo: "ring" | "ll" | "direct" | "one_rank" (coll 0 AR, 1 RS, 2 AG)."""
