@@ -1102,6 +1102,10 @@ def bench_extras(dist, comm, rank, world, args):
         ex["rs_ag_error"] = repr(e)
     finally:
         comm.set_algo(None)
+    try:  # the ring broadcast (DDP's construction-time state broadcast), root 0
+        ex["broadcast_f32"] = [_bcast_row(dist, comm, rank, world, S) for S in BCAST_SIZES]
+    except Exception as e:  # noqa: BLE001
+        ex["broadcast_error"] = repr(e)
     try:  # small / mid buckets: the one-hop LL / direct RS + AG vs the ring
         ex["rs_ag_f32_sizes"] = []
         for S in EXTRA_RSAG_SIZES:
@@ -1128,6 +1132,30 @@ def bench_extras(dist, comm, rank, world, args):
         ex["graph_error"] = repr(e)
     ex["async_error"] = comm.async_error()
     return ex
+
+
+BCAST_SIZES = (64 << 10, 8 << 20, 256 << 20)
+
+
+def _bcast_row(dist, comm, rank, world, S, root=0):
+    """ncclBroadcast of S bytes (f32) from `root`: us per call and busbw
+    (nccl-tests: busbw = algbw = S / t for broadcast); output checked."""
+    sp = torch.cuda.current_stream().cuda_stream
+    n = S // 4
+    x = torch.empty(n, device="cuda")
+    pattern_fill(x, root, world)
+    y = x if rank == root else torch.full((n,), float("nan"), device="cuda")
+    steps = 20 if S <= (8 << 20) else 5
+
+    def call():
+        comm.broadcast(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, root, sp)
+    t = _time_coll(dist, call, steps, 2)
+    ref = torch.empty(n, device="cuda")
+    pattern_fill(ref, root, world)
+    ok = bool(_all_ok(dist, torch.equal(y, ref)))
+    del x, y, ref
+    return {"bytes": S, "us": round(t / steps * 1e6, 2), "busbw": round(S / (t / steps) / 1e9, 3),
+            "correct": ok, "algo": comm.coll_algo(3, S, nccl.ncclUint8)}
 
 
 def _rs_ag(dist, comm, rank, world, S, steps, warmup, dtype="bf16"):
