@@ -9,9 +9,9 @@
  *
  * Scope: AllReduce / ReduceScatter / AllGather over the
  * repo's own transport (xGMI peer memory, no RCCL) and the comm lifecycle they
- * need, Broadcast / Bcast (the byte-copy ring), CommSplit, MemAlloc /
- * MemFree, Register / Deregister (a no-op) and InitRankScalable.  The calls
- * of the "out of scope" block at the end (Reduce, Send, Recv,
+ * need, Broadcast / Bcast (the byte-copy ring), Reduce (the reduce ring),
+ * CommSplit, MemAlloc / MemFree, Register / Deregister (a no-op) and
+ * InitRankScalable.  The calls of the "out of scope" block at the end (Send, Recv,
  * GroupSimulateEnd, RCCL's AllToAll / AllToAllv) are declared and exported so a binary linked against
  * libnccl still loads; each logs a WARN and returns ncclInvalidUsage.
  */
@@ -199,6 +199,12 @@ ncclResult_t  ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, 
     int root, ncclComm_t comm, hipStream_t stream);
 ncclResult_t pncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
     int root, ncclComm_t comm, hipStream_t stream);
+/* nccl.h.in:312-315: the ring reduce (reduce.h) into root's recvbuff; a
+ * non-root's recvbuff is never written and may be NULL */
+ncclResult_t  ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
+ncclResult_t pncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
 
 /* ---- memory, registration and scalable init (nccl.h.in:104-111, :178-181,
  * :208-217): exported so a caller linked against libnccl (PyTorch's nccl
@@ -241,11 +247,6 @@ typedef struct ncclSimInfo_v22200 {
  * (the tuner's cost model is out of scope) */
 ncclResult_t  ncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
 ncclResult_t pncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
-/* nccl.h.in:312-315 */
-ncclResult_t  ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
-    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
-ncclResult_t pncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
-    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream);
 /* nccl.h.in:403-406 */
 ncclResult_t  ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer,
     ncclComm_t comm, hipStream_t stream);

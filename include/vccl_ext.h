@@ -109,13 +109,19 @@
 extern "C" {
 #endif
 
-typedef enum { vcclCollAllReduce = 0, vcclCollReduceScatter = 1, vcclCollAllGather = 2 } vcclColl_t;
+typedef enum {
+  vcclCollAllReduce = 0,
+  vcclCollReduceScatter = 1,
+  vcclCollAllGather = 2,
+  vcclCollBroadcast = 3,
+  vcclCollReduce = 4
+} vcclColl_t;
 typedef enum {
   vcclAlgoRing = 0,     /* SIMPLE ring over arc-balanced ring sets */
   vcclAlgoLL = 1,       /* one-shot LL all-reduce, chain-tree fold */
   vcclAlgoDirect = 2,   /* two-shot direct all-reduce over the full mesh */
   vcclAlgoOneRank = 3,  /* nRanks == 1: copy / PreMulSum kernel */
-  vcclAlgoLL128 = 4     /* ring over LL128 FIFOs (128-byte lines, in-line flags) */
+  vcclAlgoLL128 = 4     /* ring over LL128 FIFOs (64-byte lines by default, in-line flags) */
 } vcclAlgo_t;
 
 ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count, ncclDataType_t datatype,

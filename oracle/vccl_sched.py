@@ -88,20 +88,22 @@ class CbdWork:
 
 
 def traffic_per_byte(coll, nranks):
-    """ncclFuncTrafficPerByte (enqueue.cc:67-74): AR 2, RS / AG nRanks, else 1."""
-    return 2 if coll == "ar" else 1 if coll == "bc" else nranks
+    """ncclFuncTrafficPerByte (enqueue.cc:67-74): AR 2, RS / AG nRanks, else
+    (broadcast "bc", reduce "red") 1."""
+    return 2 if coll == "ar" else 1 if coll in ("bc", "red") else nranks
 
 
 def max_send_recv_count(coll, nranks, count):
-    return nranks * count if coll in ("ag", "rs") else count  # AR / broadcast: count
+    return nranks * count if coll in ("ag", "rs") else count  # AR / broadcast / reduce: count
 
 
 def chunk_size(proto, buff_size=None, coll="ar"):
     """calcCollChunking for the RING algorithm (enqueue.cc:2027-2032, 2093);
-    broadcast: BROADCAST_CHUNKSTEPS 1 (collectives.h:23-24)."""
+    broadcast / reduce: BROADCAST_CHUNKSTEPS / REDUCE_CHUNKSTEPS 1
+    (collectives.h:23-26)."""
     buff = DEFAULT_BUFFSIZE[proto] if buff_size is None else buff_size
     step = buff // NCCL_STEPS
-    cs = step * (CHUNK_STEPS if proto == PROTO_SIMPLE and coll != "bc" else 1)
+    cs = step * (CHUNK_STEPS if proto == PROTO_SIMPLE and coll not in ("bc", "red") else 1)
     if proto == PROTO_LL:
         cs //= 2
     if proto == PROTO_LL128:
@@ -132,8 +134,8 @@ def cbd_schedule(coll, count, elt_size, nranks, comm_channels, proto=PROTO_SIMPL
                  buff_size=None, nthreads=None) -> CbdWork:
     """scheduleCollTasksToPlan for a plan of one ring collective.
 
-    coll: "ar" | "rs" | "ag" | "bc"; count: AR count, RS recvcount, AG
-    sendcount, broadcast count (in elements of elt_size; AG and broadcast are
+    coll: "ar" | "rs" | "ag" | "bc" | "red"; count: AR count, RS recvcount, AG
+    sendcount, broadcast / reduce count (in elements of elt_size; AG and broadcast are
     rewritten to bytes here as taskAppend does)."""
     if coll in ("ag", "bc"):
         count, elt_size = count * elt_size, 1
@@ -229,8 +231,8 @@ def u32fp_encode(x, bits):
 
 @dataclass
 class GroupCall:
-    """One queued collective: coll "ar"|"rs"|"ag", count (AR count, RS
-    recvcount, AG sendcount) in elements of elt_size; key = (func, devOp,
+    """One queued collective: coll "ar"|"rs"|"ag"|"bc"|"red", count (AR /
+    broadcast / reduce count, RS recvcount, AG sendcount) in elements of elt_size; key = (func, devOp,
     type) of ncclPrepareTasks' bins; func = the device function (batches of a
     channel merge while it is the same)."""
     coll: str

@@ -121,7 +121,7 @@ def group_works(calls, n, nch, slot_bytes=512 << 10, nthreads=512, algos=None):
                            nthreads=nthreads, algo_of=algo_of)[2]
 
 
-_COLL_CODE = {"ar": 0, "rs": 1, "ag": 2, "bc": 3}
+_COLL_CODE = {"ar": 0, "rs": 1, "ag": 2, "bc": 3, "red": 4}
 
 
 def group_algos(calls, n, coll_algo):
@@ -146,7 +146,7 @@ def select_algo(policy, coll, esz, count, n):
         return "ring"
     if policy["force"] == 4:
         return "ll128" if policy["ll128"] else "ring"
-    if coll == "bc":  # the ring broadcast: SIMPLE, or the LL128 window
+    if coll in ("bc", "red"):  # the broadcast / reduce rings: SIMPLE, or the LL128 window
         nb = count * esz
         return "ll128" if policy["ll128"] and policy["ll128_max"] and policy["ll128_min"] <= nb <= policy["ll128_max"] \
             else "ring"
@@ -222,6 +222,31 @@ def expected_reducescatter(op, dtype, inputs, nch, slot_bytes=512 << 10, rings=N
             own = np.full(idx.size, ring.index(r), np.int32)
             outs[r][idx] = O.ring_fold(dev_op, dtype, arg, pre, ins, own)
     return outs
+
+
+def expected_reduce(op, dtype, inputs, root, nch, slot_bytes=512 << 10, rings=None, nthreads=512,
+                    proto=S.PROTO_SIMPLE, work=None):
+    """Expected output of the ring reduce on `root` (reduce.h:12-55): each
+    element's channel (VCCL's cbd partition of the call, REDUCE_CHUNKSTEPS 1)
+    picks its ring; the fold starts at root's successor and ends at root with
+    postOp — the reduce-scatter fold of the block root owns."""
+    n = len(inputs)
+    rings = rings or ring_orders(n)
+    dev_op, arg = O.host_to_dev_redop(op, dtype, n)
+    pre = dev_op == O.DEV_PREMULSUM
+    count = inputs[0].size
+    if work is None:
+        work = _sched("red", count, inputs[0].dtype.itemsize, n, nch, slot_bytes, nthreads, proto)
+    chan = S.channel_of(work, count)
+    out = np.empty(count, inputs[0].dtype)
+    for c in range(work.channel_lo, work.channel_hi + 1):
+        idx = np.nonzero(chan == c)[0]
+        if idx.size == 0:
+            continue
+        ring = rings[c % len(rings)]
+        ins = [inputs[q][idx] for q in ring]
+        out[idx] = O.ring_fold(dev_op, dtype, arg, pre, ins, np.full(idx.size, ring.index(root), np.int32))
+    return out
 
 
 def direct_shard_elts(count, n, elt_size):

@@ -8,7 +8,7 @@ ncclAllReduce, ncclReduceScatter, ncclAllGather, ncclGroupStart/End, ... to
 this library instead of RCCL.  Both ranks share cuda:0, which RCCL itself
 refuses; VCCL_ALLOW_SHARED_DEVICE=1 lets this library run it.  Checks
 all_reduce (sum, avg, max), reduce_scatter_tensor and all_gather_into_tensor
-exactly, broadcast, a DistributedDataParallel step (state broadcast at
+exactly, broadcast, reduce, a DistributedDataParallel step (state broadcast at
 construction, gradient-bucket all-reduce in backward) and an all_reduce on a
 sub-group (new_group); exit 0 on success.  Rendezvous: RANK, WORLD_SIZE, MASTER_ADDR /
 MASTER_PORT (TCPStore carries ncclUniqueId)."""
@@ -64,6 +64,12 @@ def main():
     dist.broadcast(b, src=world - 1)
     if not torch.equal(b, torch.full_like(b, float((world - 1) * 10 + 1))):
         bad.append(("broadcast", 1234))
+    # reduce (ncclReduce) to the last rank: only the destination changes
+    rd = torch.arange(4099, device="cuda", dtype=torch.float32) % 31 + rank
+    dist.reduce(rd, dst=world - 1)
+    base = torch.arange(4099, device="cuda", dtype=torch.float32) % 31
+    if not torch.equal(rd, base * world + world * (world - 1) / 2 if rank == world - 1 else base + rank):
+        bad.append(("reduce", 4099))
     torch.manual_seed(rank)
     model = torch.nn.Linear(64, 32).cuda()
     torch.manual_seed(0)

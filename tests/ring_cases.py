@@ -107,7 +107,33 @@ def _fp8_codes(dt, x):
 def gen_input(case_idx, rank, n_ranks):
     name, coll, op, dt, count = CASES[case_idx]
     total = count * n_ranks if coll == "rs" else count
-    rng = np.random.default_rng(1000 * case_idx + rank)
+    return _gen_values(np.random.default_rng(1000 * case_idx + rank), op, dt, total)
+
+
+# ncclReduce cases (name, op, dtype, count, inplace): every root of each is
+# run; ragged counts, every op family, PreMulSum (avg), and one bucket of
+# several chunks per channel
+REDUCE_CASES = [
+    ("red_f32_sum_ragged", 0, 7, 300_001, False),
+    ("red_f32_sum_one", 0, 7, 1, False),
+    ("red_f16_sum", 0, 6, 70_001, False),
+    ("red_bf16_sum", 0, 9, (1 << 20) + 3, False),
+    ("red_f32_avg", 4, 7, 123_457, False),
+    ("red_i32_max", 2, 2, 5_000, False),
+    ("red_u8_prod", 1, 1, 4_099, False),
+    ("red_f64_min", 3, 8, 1_000, False),
+    ("red_bf16_prod", 1, 9, 33_333, False),
+    ("red_i64_sum_multichunk", 0, 4, 1 << 21, False),
+    ("red_f32_sum_inplace", 0, 7, 200_003, True),
+]
+
+
+def gen_reduce_input(ri, rank):
+    name, op, dt, count, _ = REDUCE_CASES[ri]
+    return _gen_values(np.random.default_rng(7000 + 100 * ri + rank), op, dt, count)
+
+
+def _gen_values(rng, op, dt, total):
     if dt in (0, 1, 2, 3, 4, 5):
         npdt = O.NP_DTYPE[dt]
         if op == 1:  # keep products interesting

@@ -72,12 +72,12 @@ def test_null_comm_queries():
 
 
 def test_out_of_scope_calls_are_invalid_usage():
-    """ncclReduce / Send / Recv / AllToAll(v) are exported
-    (include/nccl.h) so a libnccl-linked binary loads, and refuse loudly."""
+    """Send / Recv / AllToAll(v) are exported (include/nccl.h) so a
+    libnccl-linked binary loads, and refuse loudly."""
     L = nccl.lib()
     vp = ctypes.c_void_p
-    assert L.ncclReduce(vp(0x10), vp(0x10), ctypes.c_size_t(4), 7, 0, 0, None, None) == nccl.ncclInvalidUsage
-    # broadcast is implemented: a NULL comm is an invalid argument
+    # reduce and broadcast are implemented: a NULL comm is an invalid argument
+    assert L.ncclReduce(vp(0x10), vp(0x10), ctypes.c_size_t(4), 7, 0, 0, None, None) == nccl.ncclInvalidArgument
     assert L.ncclBcast(vp(0x10), ctypes.c_size_t(4), 7, 0, None, None) == nccl.ncclInvalidArgument
     assert L.ncclBroadcast(vp(0x10), vp(0x10), ctypes.c_size_t(4), 7, 0, None, None) == nccl.ncclInvalidArgument
     assert L.ncclSend(vp(0x10), ctypes.c_size_t(4), 7, 1, None, None) == nccl.ncclInvalidUsage

@@ -427,6 +427,63 @@ def test_broadcast(n, geom):
     assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
 
 
+@pytest.mark.parametrize("n,geom", [(2, "test"), (3, "test"), (4, "test"), (4, "ll128"), (2, "default")])
+def test_reduce(n, geom):
+    """ncclReduce (reduce.h ring): RC.REDUCE_CASES at every root, bit-exact
+    against the oracle's fold on the call's ring partition (start at the
+    root's successor, end at the root with postOp), fp sum / prod also within
+    the §8c tolerance of the exact value; a group of reduces to different
+    roots with an all-reduce against VCCL's grouped plan
+    (tests/mp_reduce_worker.py; n ranks sharing the GPU; "ll128": the LL128
+    ring)."""
+    from tests.mp_reduce_worker import GROUP
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    proto = 2
+    if geom == "default":
+        for k in TEST_GEOM:
+            env.pop(k, None)
+        env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
+        nch, slot = _ring.n_channels(n), 512 << 10
+    else:
+        env.update(TEST_GEOM)
+        nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
+        if geom == "ll128":
+            env["NCCL_PROTO"] = "LL128"
+            proto = 1
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_reduce_worker.py"),
+                                   str(r), str(n), hexid, d], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
+    for ri, (name, op, dt, count, _) in enumerate(RC.REDUCE_CASES):
+        ins = [RC.gen_reduce_input(ri, r) for r in range(n)]
+        for root in range(n):
+            exp = _ring.expected_reduce(op, dt, ins, root, nch, slot, proto=proto)
+            got = res[root][f"{name}_r{root}"]
+            assert_bitexact(dt, got, exp, minmax=op in (2, 3), what=f"reduce {name} n={n} root {root}")
+            if op in RC.TOLERANCE_OPS and dt in (6, 7, 8, 9):
+                assert_fold_tolerance(dt, op, got, exact_f64(dt, op, ins), ins, exp_is_exact=True,
+                                      what=f"reduce {name} n={n} root {root} vs exact")
+    # the group: every call on its aggregate's path and its place in VCCL's plan
+    algos = [str(a) for a in res[0]["group_algos"]]
+    assert all(str(a) == algos[k] for r in range(n) for k, a in enumerate(res[r]["group_algos"]))
+    calls = [("red", RC.REDUCE_CASES[ri][1], RC.REDUCE_CASES[ri][2], RC.REDUCE_CASES[ri][3]) for ri, _ in GROUP]
+    calls.append(("ar", 0, 7, 1 << 20))
+    works = _ring.group_works(calls, n, nch, slot, algos=algos)
+    for k, (ri, root) in enumerate(GROUP):
+        name, op, dt, count, _ = RC.REDUCE_CASES[ri]
+        ins = [RC.gen_reduce_input(ri, r) for r in range(n)]
+        exp = _ring.expected_reduce(op, dt, ins, root % n, nch, slot, proto=1 if algos[k] == "ll128" else 2,
+                                    work=works[k])
+        assert_bitexact(dt, res[root % n][f"group{k}"], exp, minmax=op in (2, 3),
+                        what=f"group reduce {k} ({name}) n={n} root {root % n}")
+
+
 @pytest.mark.parametrize("n", [2, 4])
 def test_comm_split(n):
     """ncclCommSplit (nccl.h.in:173-174): by color with reversed keys, and

@@ -24,7 +24,7 @@ from oracle import vccl_sched as S
 from tests import _ring
 from vccl_amd import nccl
 
-COLL = {0: "ar", 1: "rs", 2: "ag", 3: "bc"}
+COLL = {0: "ar", 1: "rs", 2: "ag", 3: "bc", 4: "red"}
 ESZ = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2, 10: 1, 11: 1}
 
 
@@ -229,7 +229,7 @@ def test_library_group_plan_ex_equals_oracle(n):
         k = int(rng.integers(1, 21))
         calls = []
         for _ in range(k):
-            coll = int(rng.integers(0, 4))  # incl. broadcast
+            coll = int(rng.integers(0, 5))  # incl. broadcast and reduce
             dt = int(rng.choice([7, 9, 6, 2, 0, 8]))
             op = int(rng.choice([0, 1, 2, 3]))
             count = int(rng.choice([1, 100, 4096, 16384, 40_000, 65_536, 300_000, 1 << 20, 3 << 20])) \
@@ -317,3 +317,22 @@ def test_broadcast_partition():
                     w = S.cbd_schedule("bc", count, ESZ[dt], n, nch, buff_size=(512 << 10) * 8, nthreads=nt)
                     ref = _as_tuple(w)
                     assert lib[:5] == ref[:5] and lib[5] == ref[5] == 512 << 10, (n, nch, count, dt, lib, ref)
+
+
+def test_reduce_partition():
+    """The ring reduce's partition (traffic 1 per byte, REDUCE_CHUNKSTEPS 1,
+    collectives.h:25-26; typed elements, not bytes): library
+    (vcclRingPartition coll 4) == oracle, SIMPLE and LL128."""
+    for n in (2, 3, 4, 8):
+        for nch in (1, 14, 56, 64):
+            for count, dt in ((1, 7), (1000, 7), (300_001, 9), (1 << 22, 0), ((1 << 24) + 3, 6), (77_777, 4)):
+                for nt in (256, 512):
+                    lib = nccl.ring_partition(4, count, dt, n, nch, 512 << 10, nt)
+                    w = S.cbd_schedule("red", count, ESZ[dt], n, nch, buff_size=(512 << 10) * 8, nthreads=nt)
+                    ref = _as_tuple(w)
+                    assert lib[:5] == ref[:5] and lib[5] == ref[5] == (512 << 10) // ESZ[dt], \
+                        (n, nch, count, dt, lib, ref)
+                lib = nccl.ring_partition(4, count, dt, n, nch, S.DEFAULT_BUFFSIZE[S.PROTO_LL128] // 8, 640,
+                                          proto=S.PROTO_LL128)
+                ref = _as_tuple(S.cbd_schedule("red", count, ESZ[dt], n, nch, proto=S.PROTO_LL128))
+                assert lib[:5] == ref[:5] and lib[5] == ref[5], (n, nch, count, dt, lib, ref)

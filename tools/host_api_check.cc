@@ -40,7 +40,7 @@ int main() {
     std::vector<int> colls(k), dt(k), ops(k), algos(k, -1), order(k, -1), planOf(k, -1);
     std::vector<size_t> counts(k);
     for (int i = 0; i < k; i++) {
-      colls[i] = (int)(rng() % 4);  // AR, RS, AG, broadcast
+      colls[i] = (int)(rng() % 5);  // AR, RS, AG, broadcast, reduce
       dt[i] = dts[rng() % 10];
       ops[i] = (int)(rng() % 4);
       counts[i] = (size_t)pick({1, 7, 100, 4096, 65537, 1 << 20, (1 << 22) + 3}) + rng() % 17;
@@ -71,7 +71,7 @@ int main() {
       // the parts cover the call: lo + mid * (channels - 2) + hi (AG in bytes)
       const int64_t nCh = c[1] - c[0] + 1;
       const int64_t cover = nCh == 1 ? c[2] : c[2] + c[3] * (nCh - 2) + c[4];
-      const int64_t want = colls[i] >= 2 ? (int64_t)counts[i] * (dt[i] == ncclFloat64 || dt[i] == ncclInt64 ||
+      const int64_t want = colls[i] == 2 || colls[i] == 3 ? (int64_t)counts[i] * (dt[i] == ncclFloat64 || dt[i] == ncclInt64 ||
                                                                   dt[i] == ncclUint64 ? 8
                                                                   : dt[i] == ncclFloat16 || dt[i] == ncclBfloat16 ? 2
                                                                   : dt[i] <= ncclUint8 ? 1 : 4)
@@ -103,7 +103,7 @@ int main() {
     const int d = dts[rng() % 10];
     int64_t out[8];
     const size_t step = proto == 1 ? 614400 : proto == 0 ? 65536 : 512 << 10;
-    EXPECT(vcclRingPartition((int)(rng() % 4), count, (ncclDataType_t)d, n, nch, proto, step,
+    EXPECT(vcclRingPartition((int)(rng() % 5), count, (ncclDataType_t)d, n, nch, proto, step,
                              proto == 1 ? 640 : 512, out) == ncclSuccess);
     int64_t ck[3];
     EXPECT(vcclRingChunkOf(count, (ncclDataType_t)d, n, nch, 512 << 10, 512, rng() % count, ck) == ncclSuccess);

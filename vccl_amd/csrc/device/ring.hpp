@@ -470,6 +470,36 @@ __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, 
   }
 }
 
+// -------------------------------------------------------------------- Reduce
+// reduce.h:12-55 (runRing): each chunk starts at the root's ring successor
+// (send), every rank but the root adds its own input to what it receives and
+// forwards it (recvReduceSend, own input as src0), and the root writes
+// own ⊕ recv to its output with the postOp (recvReduceCopy) — the fold of
+// the reduce-scatter chunk the root owns.  One FIFO step per chunk
+// (REDUCE_CHUNKSTEPS 1).
+template <class Fn, int UNROLL, int PROTO = kProtoSimple>
+__device__ void ring_reduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
+  using T = typename Fn::EltType;
+  const int n = w.nRanks;
+  int64_t partOff, partCount, chunkCount;
+  if (!cbd_part(w, c, &partOff, &partCount, &chunkCount)) return;
+  const T* in = (const T*)w.sendbuff;
+  T* out = (T*)w.recvbuff;
+  const int me = r.ch->ringRanks[0], prev = r.ch->ringRanks[n - 1];
+  for (int64_t eo = 0; eo < partCount; eo += chunkCount) {
+    const int64_t nelem = partCount - eo < chunkCount ? partCount - eo : chunkCount;
+    const int64_t off = partOff + eo;
+    // slot offset from the element offset: the same on every rank
+    const int m = (int)((off * (int64_t)sizeof(T)) & 15);
+    if (prev == w.root)
+      ring_step<Fn, false, true, true, false, UNROLL, PROTO>(r, fn, in + off, nullptr, nelem, false, 0, m);
+    else if (me == w.root)
+      ring_step<Fn, true, false, true, true, UNROLL, PROTO>(r, fn, in + off, out + off, nelem, true, m, 0);
+    else
+      ring_step<Fn, true, true, true, false, UNROLL, PROTO>(r, fn, in + off, nullptr, nelem, false, m, m);
+  }
+}
+
 // ----------------------------------------------------------------- AllGather
 // all_gather.h:12-83: byte copies (enqueue.cc:2400-2404 rewrites AG as int8).
 template <int UNROLL, int PROTO = kProtoSimple>

@@ -1,6 +1,6 @@
 // Collective kernels for ONE kernel element type (VCCL_KT) and ONE family
 // (VCCL_PART: 0 ring, 1 LL, 2 direct — separate objects, built in parallel):
-// per reduction functor the ring all-reduce / reduce-scatter (one workgroup
+// per reduction functor the ring all-reduce / reduce-scatter / reduce (one workgroup
 // per channel, enqueue.cc:1576-1666), the one-shot LL and the direct
 // (two-shot all-reduce, one-hop reduce-scatter) kernels; in the K_U8 unit
 // also the type-agnostic all-gathers (ring, LL, direct).
@@ -52,6 +52,7 @@ __device__ __forceinline__ void ring_run(RingCtx& r, const Fn& fn, const RingWor
   if constexpr (COLL == kCollAllReduce) ring_allreduce<Fn, UNROLL, PROTO>(r, fn, w, blockIdx.x);
   else if constexpr (COLL == kCollReduceScatter)
     ring_reducescatter<Fn, UNROLL, PROTO>(r, fn, w, blockIdx.x);
+  else if constexpr (COLL == kCollReduce) ring_reduce<Fn, UNROLL, PROTO>(r, fn, w, blockIdx.x);
   else if constexpr (COLL == kCollAllGather) ring_allgather<UNROLL, PROTO>(r, w, blockIdx.x);
   else ring_broadcast<UNROLL, PROTO>(r, w, blockIdx.x);
 }
@@ -116,6 +117,8 @@ hipError_t VCCL_RING_LAUNCH<VCCL_KT>(int coll, int devOp, const RingBatch& w, in
     } else if (coll == kCollReduceScatter) {
       err = launch_k(k_ring<kCollReduceScatter, Fn, ring_unroll<Fn>(), kPartProto>, grid, block, stream, stop,
                      w);
+    } else if (coll == kCollReduce) {
+      err = launch_k(k_ring<kCollReduce, Fn, ring_unroll<Fn>(), kPartProto>, grid, block, stream, stop, w);
     }
   });
   return err;

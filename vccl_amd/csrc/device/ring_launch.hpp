@@ -9,7 +9,7 @@
 
 namespace vccl {
 
-enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2, kCollBroadcast = 3 };
+enum : int { kCollAllReduce = 0, kCollReduceScatter = 1, kCollAllGather = 2, kCollBroadcast = 3, kCollReduce = 4 };
 // 16-byte packs per thread per operand in flight in a ring step: 4 (2 for
 // the fp8 types, whose per-element prod / min / max / PreMulSum kernels
 // spill at 4).  Twice round 1's 2 keeps twice the write-through stores in

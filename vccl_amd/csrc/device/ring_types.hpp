@@ -200,7 +200,7 @@ struct RingWork {
   int64_t chunkLo, chunkMid, chunkHi;
   // LL128 ring (proto = kProtoLL128): bytes per LL128 FIFO slot
   int64_t ll128SlotBytes;
-  int root;                          // broadcast: the root's rank
+  int root;                          // broadcast / reduce: the root's rank
 };
 
 // Protocols of the ring kernels (nccl_common.h ids).

@@ -26,7 +26,7 @@
 
 namespace vccl {
 
-enum Coll { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2, kBroadcast = 3 };
+enum Coll { kAllReduce = 0, kReduceScatter = 1, kAllGather = 2, kBroadcast = 3, kReduce = 4 };
 // Byte-copy collectives: the host rewrites them as int8 (enqueue.cc:2400-2404).
 static inline bool is_copy_coll(int coll) { return coll == kAllGather || coll == kBroadcast; }
 
@@ -49,7 +49,7 @@ struct Task {
   int devOp;
   uint64_t arg;
   const void* argPtr;  // ncclScalarDevice PreMulSum scalar
-  int root;            // broadcast
+  int root;            // broadcast / reduce
   ncclComm* comm;
   hipStream_t stream;
   // Set by the group planner (launch_planned): this call's partition inside
@@ -367,7 +367,7 @@ static ncclResult_t launch_one_rank(const Task& t) {
 constexpr uint64_t kMinTraffic = 16 << 10;  // MinTrafficPerChannel, enqueue.cc:528
 static int64_t div_up(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static int64_t traffic_per_byte(int coll, int nRanks) {  // ncclFuncTrafficPerByte (enqueue.cc:67-74)
-  return coll == kAllReduce ? 2 : coll == kBroadcast ? 1 : nRanks;
+  return coll == kAllReduce ? 2 : coll == kBroadcast || coll == kReduce ? 1 : nRanks;
 }
 
 // nMaxChannels of a task (or of an aggregate of tasks, ncclPrepareTasks):
@@ -382,7 +382,8 @@ static int ring_nmax_channels(int coll, int64_t count, int64_t eltSize, int nRan
   const int64_t threshold = proto == kProtoSimple ? 64
                             : proto == kProtoLL128 || coll == kAllReduce ? 8 : 8 * (int64_t)nRanks;
   // ncclFuncMaxSendRecvCount (enqueue.h:36-38): RS / AG move n blocks
-  const int64_t nBytes = eltSize * (coll == kAllReduce || coll == kBroadcast ? count : (int64_t)nRanks * count);
+  const int64_t nBytes =
+      eltSize * (coll == kReduceScatter || coll == kAllGather ? (int64_t)nRanks * count : count);
   int64_t nc = commChannels;
   while (nBytes < nc * nThreads * threshold && nc >= 2) nc--;
   return (int)nc;
@@ -453,10 +454,11 @@ static CbdPlan cbd_place(PlanCursor& pc, int coll, int64_t count, int64_t eltSiz
   // LL128 = one step, 15/16 of it data; LL = half a step; rounded down to
   // the protocol grain (device.h:290-295: SIMPLE 512, LL128 1920, LL 16);
   // independent of size.
-  // (broadcast: BROADCAST_CHUNKSTEPS 1, collectives.h:23-24)
+  // (broadcast / reduce: BROADCAST_CHUNKSTEPS / REDUCE_CHUNKSTEPS 1,
+  // collectives.h:23-26)
   const int64_t grain = ll128 ? 1920 : ll ? 16 : 512;
   const int64_t chunkBytes =
-      ll128 ? stepBytes / 16 * 15 : ll ? stepBytes / 2 : (coll == kBroadcast ? 1 : 4) * stepBytes;
+      ll128 ? stepBytes / 16 * 15 : ll ? stepBytes / 2 : (coll == kBroadcast || coll == kReduce ? 1 : 4) * stepBytes;
   const int64_t chunkElts = chunkBytes / grain * grain / eltSize;
   p.chunkLo = p.chunkMid = p.chunkHi = chunkElts;
   // advance the cursor (enqueue.cc:667-681)
@@ -527,7 +529,7 @@ static int select_algo(const AlgoPolicy& p, int coll, int64_t eltSize, int64_t c
   if (p.nRanks < 2 || p.algoForce == 1) return kAlgoRing;
   // NCCL_PROTO=LL128 (or vcclCommSetAlgo): the LL128 ring for every size
   if (p.algoForce == 4) return p.ll128 ? kAlgoRingLL128 : kAlgoRing;
-  if (coll == kBroadcast) {  // the ring broadcast (broadcast.h), SIMPLE or the LL128 window
+  if (coll == kBroadcast || coll == kReduce) {  // the rings of broadcast.h / reduce.h: SIMPLE or the LL128 window
     const uint64_t bytes = (uint64_t)(count * eltSize);
     return p.ll128 && p.ll128Max && bytes >= p.ll128Min && bytes <= p.ll128Max ? kAlgoRingLL128 : kAlgoRing;
   }
@@ -715,7 +717,8 @@ static void group_plan(const std::vector<GroupTask>& ts, int nRanks, int commCha
 static int dev_coll(int coll) {
   return coll == kAllReduce ? kCollAllReduce
          : coll == kReduceScatter ? kCollReduceScatter
-         : coll == kBroadcast ? kCollBroadcast : kCollAllGather;
+         : coll == kBroadcast ? kCollBroadcast
+         : coll == kReduce ? kCollReduce : kCollAllGather;
 }
 
 // A call's partition: its place in its group's plan (launch_planned, under
@@ -1222,7 +1225,7 @@ static ncclResult_t enqueue_check_impl(int coll, const char* name, const void* s
                                        void* recvbuff, size_t count, ncclDataType_t dt,
                                        ncclRedOp_t op, ncclComm* comm, hipStream_t stream, int root) {
   NCCLCHECK(comm_check(comm, name));
-  if (coll == kBroadcast && (root < 0 || root >= comm->nRanks)) {  // argcheck.cc:66-69
+  if ((coll == kBroadcast || coll == kReduce) && (root < 0 || root >= comm->nRanks)) {  // argcheck.cc:66-69
     VWARN("%s : invalid root %d (root should be in the 0..%d range)", name, root, comm->nRanks);
     return ncclInvalidArgument;
   }
@@ -1231,8 +1234,10 @@ static ncclResult_t enqueue_check_impl(int coll, const char* name, const void* s
         name, (unsigned long)comm->opCount, sendbuff, recvbuff, count, (int)dt, (int)op,
         (void*)comm, comm->nRanks, (void*)stream);
   if (count == 0) return ncclSuccess;  // enqueue.cc:2372
-  // broadcast: a non-root's sendbuff is never read (argcheck.cc:76-78)
-  if (!recvbuff || (!sendbuff && !(coll == kBroadcast && comm->rank != root))) {
+  // broadcast: a non-root's sendbuff is never read, reduce: a non-root's
+  // recvbuff never written (argcheck.cc:76-81)
+  if ((!recvbuff && !(coll == kReduce && comm->rank != root)) ||
+      (!sendbuff && !(coll == kBroadcast && comm->rank != root))) {
     VWARN("%s : NULL buffer", name);
     return ncclInvalidArgument;
   }
@@ -1279,13 +1284,9 @@ using namespace vccl;
 // Out-of-scope calls of the reference API (include/nccl.h):
 // exported so a binary linked against libnccl loads, never silently wrong.
 static ncclResult_t out_of_scope(const char* name) {
-  VWARN("%s is not part of this library's scope (AllReduce / ReduceScatter / AllGather only)",
+  VWARN("%s is not part of this library's scope (AllReduce / ReduceScatter / AllGather / Broadcast / Reduce only)",
         name);
   return ncclInvalidUsage;
-}
-VCCL_EXPORT ncclResult_t ncclReduce(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int,
-                                    ncclComm_t, hipStream_t) {
-  return out_of_scope("ncclReduce");
 }
 
 VCCL_EXPORT ncclResult_t ncclSend(const void*, size_t, ncclDataType_t, int, ncclComm_t,
@@ -1332,6 +1333,13 @@ VCCL_EXPORT ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, siz
                                        ncclDataType_t datatype, int root, ncclComm_t comm, hipStream_t stream) {
   return enqueue_check(kBroadcast, "Broadcast", sendbuff, recvbuff, count, datatype, ncclSum, comm, stream,
                        root);
+}
+// reduce.h / collectives.cc:132-143: the ring reduce, count elements of
+// datatype reduced from every rank's sendbuff into root's recvbuff (a
+// non-root's recvbuff is never written, argcheck.cc:79-81)
+VCCL_EXPORT ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream) {
+  return enqueue_check(kReduce, "Reduce", sendbuff, recvbuff, count, datatype, op, comm, stream, root);
 }
 // collectives.cc:112-123: the in-place broadcast
 VCCL_EXPORT ncclResult_t ncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root, ncclComm_t comm,
@@ -1477,14 +1485,14 @@ ncclResult_t pncclRecv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream
 extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count,
                                          ncclDataType_t datatype, int* algo) {
   NCCLCHECK(comm_check(comm, "vcclCommCollAlgo"));
-  if (!algo || coll < 0 || coll > 3 || type_size(datatype) < 1) return ncclInvalidArgument;
+  if (!algo || coll < kAllReduce || coll > kReduce || type_size(datatype) < 1) return ncclInvalidArgument;
   if (comm->nRanks == 1) {
     *algo = vcclAlgoOneRank;
     return ncclSuccess;
   }
   Task t{};
   t.comm = comm;
-  t.coll = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : coll == 2 ? kAllGather : kBroadcast;
+  t.coll = coll;  // the public codes are the Coll values (vccl_ext.h)
   t.count = count;
   t.datatype = datatype;
   const int a = choose_algo(t);
@@ -1496,11 +1504,11 @@ extern "C" ncclResult_t vcclCommCollAlgo(ncclComm_t comm, int coll, size_t count
 extern "C" __attribute__((visibility("default"))) ncclResult_t vcclRingPartition(
     int coll, size_t count, ncclDataType_t datatype, int nRanks, int nChannels, int proto,
     size_t stepBytes, int nThreads, int64_t* out) {
-  if (!out || coll < 0 || coll > 3 || type_size(datatype) < 1 || nRanks < 1 ||
+  if (!out || coll < kAllReduce || coll > kReduce || type_size(datatype) < 1 || nRanks < 1 ||
       nChannels < 1 || nChannels > kMaxChannels || count == 0 || stepBytes < 4096 || nThreads < 64 ||
       (proto != kProtoSimple && proto != kProtoLL128 && proto != kProtoLL))
     return ncclInvalidArgument;
-  const int c = coll == 0 ? kAllReduce : coll == 1 ? kReduceScatter : coll == 2 ? kAllGather : kBroadcast;
+  const int c = coll;
   const int64_t esz = is_copy_coll(c) ? 1 : type_size(datatype);
   const int64_t cnt = is_copy_coll(c) ? (int64_t)count * type_size(datatype) : (int64_t)count;
   const CbdPlan p = cbd_schedule(c, cnt, esz, nRanks, nChannels, proto, (int64_t)stepBytes, nThreads);
@@ -1540,9 +1548,8 @@ static ncclResult_t group_plan_export(int nCalls, const int* colls, const size_t
   for (int i = 0; i < nCalls; i++) {
     const ncclDataType_t dt = (ncclDataType_t)datatypes[i];
     const int tsz = type_size(dt);
-    if (colls[i] < 0 || colls[i] > 3 || tsz < 1 || counts[i] == 0) return ncclInvalidArgument;
-    const int c = colls[i] == 0 ? kAllReduce : colls[i] == 1 ? kReduceScatter : colls[i] == 2 ? kAllGather
-                                                                                            : kBroadcast;
+    if (colls[i] < kAllReduce || colls[i] > kReduce || tsz < 1 || counts[i] == 0) return ncclInvalidArgument;
+    const int c = colls[i];
     const bool ag = is_copy_coll(c);
     int devOp = OP_SUM;
     uint64_t arg = 0;

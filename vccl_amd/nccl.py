@@ -100,6 +100,7 @@ def lib() -> ctypes.CDLL:
         "ncclReduceScatter": [vp, vp, c_size, c_int, c_int, vp, vp],
         "ncclAllGather": [vp, vp, c_size, c_int, vp, vp],
         "ncclBroadcast": [vp, vp, c_size, c_int, c_int, vp, vp],
+        "ncclReduce": [vp, vp, c_size, c_int, c_int, c_int, vp, vp],
         "ncclGroupStart": [],
         "ncclGroupEnd": [],
         "vcclReduceCopy": [c_int, c_int, u64, c_int, c_int, c_int, ctypes.POINTER(vp), c_int,
@@ -340,6 +341,10 @@ class Comm:
 
     def broadcast(self, send: int, recv: int, count: int, dtype: int, root: int, stream: int = 0):
         check(lib().ncclBroadcast(send, recv, count, dtype, root, self.handle, stream), "ncclBroadcast")
+
+    def reduce(self, send: int, recv: int, count: int, dtype: int, op: int, root: int, stream: int = 0):
+        """ncclReduce (reduce.h ring): `count` elements reduced into root's `recv`."""
+        check(lib().ncclReduce(send, recv, count, dtype, op, root, self.handle, stream), "ncclReduce")
 
     def coll_algo(self, coll: int, count: int, dtype: int) -> str:
         """vcclCommCollAlgo: "ring" | "ll" | "direct" | "one_rank" (coll 0 AR, 1 RS, 2 AG)."""
