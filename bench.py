@@ -1106,6 +1106,10 @@ def bench_extras(dist, comm, rank, world, args):
         ex["broadcast_f32"] = [_bcast_row(dist, comm, rank, world, S) for S in BCAST_SIZES]
     except Exception as e:  # noqa: BLE001
         ex["broadcast_error"] = repr(e)
+    try:  # the ring reduce into the last rank
+        ex["reduce_f32"] = [_reduce_row(dist, comm, rank, world, S) for S in BCAST_SIZES]
+    except Exception as e:  # noqa: BLE001
+        ex["reduce_error"] = repr(e)
     try:  # small / mid buckets: the one-hop LL / direct RS + AG vs the ring
         ex["rs_ag_f32_sizes"] = []
         for S in EXTRA_RSAG_SIZES:
@@ -1156,6 +1160,28 @@ def _bcast_row(dist, comm, rank, world, S, root=0):
     del x, y, ref
     return {"bytes": S, "us": round(t / steps * 1e6, 2), "busbw": round(S / (t / steps) / 1e9, 3),
             "correct": ok, "algo": comm.coll_algo(3, S, nccl.ncclUint8)}
+
+
+def _reduce_row(dist, comm, rank, world, S, root=None):
+    """ncclReduce (f32 sum) of S bytes into `root` (default the last rank):
+    us per call and busbw (nccl-tests: busbw = algbw = S / t for reduce);
+    the root's output checked."""
+    root = world - 1 if root is None else root
+    sp = torch.cuda.current_stream().cuda_stream
+    n = S // 4
+    x = torch.empty(n, device="cuda")
+    pattern_fill(x, rank, world)
+    y = torch.full((n,), float("nan"), device="cuda") if rank == root else None
+    steps = 20 if S <= (8 << 20) else 5
+
+    def call():
+        comm.reduce(x.data_ptr(), y.data_ptr() if y is not None else 0, n, nccl.ncclFloat32, nccl.ncclSum,
+                    root, sp)
+    t = _time_coll(dist, call, steps, 2)
+    ok = bool(_all_ok(dist, pattern_ok(y, world) if y is not None else True))
+    del x, y
+    return {"bytes": S, "us": round(t / steps * 1e6, 2), "busbw": round(S / (t / steps) / 1e9, 3),
+            "correct": ok, "algo": comm.coll_algo(4, n, nccl.ncclFloat32)}
 
 
 def _rs_ag(dist, comm, rank, world, S, steps, warmup, dtype="bf16"):

@@ -347,7 +347,7 @@ class Comm:
         check(lib().ncclReduce(send, recv, count, dtype, op, root, self.handle, stream), "ncclReduce")
 
     def coll_algo(self, coll: int, count: int, dtype: int) -> str:
-        """vcclCommCollAlgo: "ring" | "ll" | "direct" | "one_rank" (coll 0 AR, 1 RS, 2 AG)."""
+        """vcclCommCollAlgo: "ring" | "ll" | "direct" | "ll128" | "one_rank" (coll 0 AR, 1 RS, 2 AG, 3 broadcast, 4 reduce)."""
         a = ctypes.c_int()
         check(lib().vcclCommCollAlgo(self.handle, coll, ctypes.c_size_t(count), dtype,
                                      ctypes.byref(a)), "vcclCommCollAlgo")
