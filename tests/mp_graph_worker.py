@@ -8,7 +8,8 @@ into one graph on a side stream (after an eager call on the current stream,
 and followed by another), replays it 4 times with new integer-valued inputs (exact in any
 fold order) and checks every output; then two captures interleaved on the
 same comm (interleaved_captures); a group of ring and direct calls on two
-streams inside one capture (group_in_capture); then collectives that fail
+streams inside one capture (group_in_capture); a reduce, a broadcast and an
+all-gather in one capture (rooted_in_capture); then collectives that fail
 inside a capture (failing_calls_in_capture); exit code 0 = all replays
 correct."""
 import os
@@ -63,6 +64,44 @@ def interleaved_captures(comm, rank, n):
             ok &= torch.equal(y, sum(val(r, k) for r in range(n)))
     if not ok:
         print(f"rank {rank}: interleaved captures mismatch", flush=True)
+    return ok
+
+
+def rooted_in_capture(comm, rank, n):
+    """A reduce (into rank 0), a broadcast (from the last rank) and an
+    all-gather captured in one graph on one stream replay exactly with fresh
+    inputs each time: the rooted rings keep their roots and partitions in the
+    captured kernel arguments."""
+    cnt = 700_001
+    x, y = torch.empty(cnt, device="cuda"), torch.full((cnt,), float("nan"), device="cuda")
+    b = torch.empty(cnt, device="cuda")
+    ag_in, ag_out = torch.empty(4099, device="cuda"), torch.empty(4099 * n, device="cuda")
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    f32 = nccl.ncclFloat32
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        g.capture_begin(capture_error_mode="relaxed")
+        comm.reduce(x.data_ptr(), y.data_ptr() if rank == 0 else 0, cnt, f32, nccl.ncclSum, 0, s.cuda_stream)
+        comm.broadcast(b.data_ptr(), b.data_ptr(), cnt, f32, n - 1, s.cuda_stream)
+        comm.all_gather(ag_in.data_ptr(), ag_out.data_ptr(), 4099, f32, s.cuda_stream)
+        g.capture_end()
+    ok = True
+    for it in range(3):
+        def val(r, m, k):
+            return ((torch.arange(m, device="cuda") * (r + 7 + k) + 3 * it) % 79).float()
+        x.copy_(val(rank, cnt, 0))
+        b.copy_(val(rank, cnt, 1))
+        ag_in.copy_(val(rank, 4099, 2))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        if rank == 0:
+            ok &= torch.equal(y, sum(val(r, cnt, 0) for r in range(n)))
+        ok &= torch.equal(b, val(n - 1, cnt, 1))
+        ok &= torch.equal(ag_out, torch.cat([val(r, 4099, 2) for r in range(n)]))
+    if not ok:
+        print(f"rank {rank}: rooted collectives in capture mismatch", flush=True)
     return ok
 
 
@@ -271,6 +310,7 @@ def main():
     ok &= torch.equal(eager_y, exp_eager)
     ok &= interleaved_captures(comm, rank, n)
     ok &= group_in_capture(comm, rank, n)
+    ok &= rooted_in_capture(comm, rank, n)
     ok &= failing_calls_in_capture(comm, rank, n)
     ok &= captures_on_destroyed_streams(comm, rank, n)
     ok &= comm.async_error() == 0
