@@ -148,6 +148,9 @@ const char*  ncclGetErrorString(ncclResult_t result);
 const char* pncclGetErrorString(ncclResult_t result);
 const char*  ncclGetLastError(ncclComm_t comm);
 const char* pncclGetLastError(ncclComm_t comm);
+/* nccl.h.in:191-193: reload the environment variables that set logging */
+void  ncclResetDebugInit(void);
+void pncclResetDebugInit(void);
 ncclResult_t  ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
 ncclResult_t pncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError);
 ncclResult_t  ncclCommCount(const ncclComm_t comm, int* count);

@@ -17,7 +17,7 @@ def _declared():
         if not h.endswith(".h"):
             continue
         text = open(os.path.join(ROOT, "include", h)).read()
-        names |= set(re.findall(r"^\s*(?:ncclResult_t|const char\*|int)\s+(p?(?:nccl|vccl)[A-Z]\w*)\s*\(",
+        names |= set(re.findall(r"^\s*(?:ncclResult_t|const char\*|int|void)\s+(p?(?:nccl|vccl)[A-Z]\w*)\s*\(",
                                 text, flags=re.M))
     return names
 
@@ -134,3 +134,28 @@ def test_group_with_failing_call_launches_nothing():
     assert L.ncclReduceScatter(None, None, 1, 99, 0, None, None) == nccl.ncclInvalidArgument
     assert L.ncclGroupEnd() == nccl.ncclSuccess
     assert L.ncclGroupEnd() == nccl.ncclInvalidArgument
+
+
+def test_reset_debug_init_reloads_level():
+    """ncclResetDebugInit (nccl.h.in:191-193): NCCL_DEBUG is re-read, so a
+    WARN is silenced under NONE and printed again under WARN (a child process
+    owns the C-level stderr)."""
+    code = r"""
+import ctypes, os, sys
+sys.path.insert(0, sys.argv[1])
+from vccl_amd import nccl
+L = nccl.lib()
+def warn():  # a NULL-comm call: WARN + invalid argument, no GPU needed
+    L.ncclReduce(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_size_t(4), 7, 0, 0, None, None)
+os.environ["NCCL_DEBUG"] = "NONE"; L.ncclResetDebugInit(); warn()
+sys.stderr.flush(); print("--mark--", file=sys.stderr, flush=True)
+os.environ["NCCL_DEBUG"] = "WARN"; L.pncclResetDebugInit(); warn()
+"""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("NCCL_DEBUG", "VCCL_DEBUG")}
+    r = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    before, after = r.stderr.split("--mark--")
+    assert "WARN" not in before, before
+    assert "WARN" in after, after

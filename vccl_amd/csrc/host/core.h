@@ -25,6 +25,7 @@ namespace vccl {
 // NCCL_DEBUG=WARN|INFO|TRACE (debug.h:22-34); VCCL_DEBUG is an alias.
 enum LogLevel { kLogNone = 0, kLogWarn = 1, kLogInfo = 2, kLogTrace = 3 };
 int log_level();
+void reset_log_level();
 void log_msg(int level, const char* file, int line, const char* fmt, ...)
     __attribute__((format(printf, 4, 5)));
 #define VWARN(...) ::vccl::log_msg(::vccl::kLogWarn, __FILE__, __LINE__, __VA_ARGS__)

@@ -1,6 +1,7 @@
 // Logging and environment parameters.
 // Reference idioms: NCCL_DEBUG / ncclDebugLog (src/debug.cc, include/debug.h:22-34)
 // and NCCL_PARAM (include/param.h:17-25, misc/param.cc:52-98).
+#include <atomic>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -20,14 +21,22 @@ static int parse_level(const char* s) {
   return kLogWarn;
 }
 
+// -1: not read yet (first use, or after ncclResetDebugInit)
+static std::atomic<int> g_level{-1};
+
 int log_level() {
-  static int level = [] {
+  int level = g_level.load(std::memory_order_relaxed);
+  if (level < 0) {
     const char* s = getenv("VCCL_DEBUG");
     if (!s) s = getenv("NCCL_DEBUG");
-    return parse_level(s);
-  }();
+    level = parse_level(s);
+    g_level.store(level, std::memory_order_relaxed);
+  }
   return level;
 }
+
+// ncclResetDebugInit (debug.cc:367-378): the next log call re-reads the level
+void reset_log_level() { g_level.store(-1, std::memory_order_relaxed); }
 
 void log_msg(int level, const char* file, int line, const char* fmt, ...) {
   if (log_level() < level) return;

@@ -1080,8 +1080,12 @@ VCCL_EXPORT ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoc
   return ncclSuccess;
 }
 
+// nccl.h.in:191-193: reload the logging level from NCCL_DEBUG / VCCL_DEBUG
+VCCL_EXPORT void ncclResetDebugInit() { reset_log_level(); }
+
 // pnccl* profiling aliases (src/include/core.h:18-31)
 extern "C" {
+void pncclResetDebugInit() VCCL_ALIAS(ncclResetDebugInit);
 ncclResult_t pncclGetVersion(int*) VCCL_ALIAS(ncclGetVersion);
 ncclResult_t pncclGetUniqueId(ncclUniqueId*) VCCL_ALIAS(ncclGetUniqueId);
 ncclResult_t pncclCommInitRank(ncclComm_t*, int, ncclUniqueId, int) VCCL_ALIAS(ncclCommInitRank);

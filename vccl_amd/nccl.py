@@ -42,9 +42,10 @@ EXPORTED = [
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
     "vcclCommRingTrace", "vcclCommGroupAlgos",
     "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders", "vcclGroupPlan", "vcclGroupPlanEx", "vcclAlgoSelection",
+    # rooted rings, split and debug reload
+    "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclCommSplit", "ncclResetDebugInit",
     # out of scope, exported so libnccl-linked binaries load: WARN + ncclInvalidUsage
-    "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclSend", "ncclRecv", "ncclCommSplit",
-    "ncclGroupSimulateEnd", "ncclAllToAll", "ncclAllToAllv",
+    "ncclSend", "ncclRecv", "ncclGroupSimulateEnd", "ncclAllToAll", "ncclAllToAllv",
     # memory / registration / scalable init (what a libnccl caller such as
     # PyTorch's nccl backend imports)
     "ncclMemAlloc", "ncclMemFree", "ncclCommInitRankScalable", "ncclCommRegister", "ncclCommDeregister",
