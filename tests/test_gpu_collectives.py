@@ -427,6 +427,31 @@ def test_broadcast(n, geom):
     assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
 
 
+@pytest.mark.parametrize("env,want", [({}, 16), ({"NCCL_NCHANNELS": "12"}, 12),
+                                      ({"NCCL_MAX_NCHANNELS": "5"}, 5), ({"NCCL_MAX_NRINGS": "7"}, 7),
+                                      ({"NCCL_NCHANNELS": "4", "NCCL_MIN_NCHANNELS": "9"}, 9),
+                                      ({"NCCL_MAX_CTAS": "6"}, 6), ({"NCCL_MIN_CTAS": "20"}, 20)])
+def test_channel_count_knobs(monkeypatch, env, want):
+    """The ring channel count at 2 ranks: the link-bound default (16), then
+    NCCL_NCHANNELS, NCCL_MIN/MAX_NCHANNELS (legacy MIN/MAX_NRINGS,
+    graph/connect.cc:326-360) and NCCL_MIN/MAX_CTAS bounding it.  Init only:
+    the data path at other channel counts runs in the ring tests; two ranks of
+    one process here would only be co-resident when their streams land on
+    distinct hardware queues (see test_single_process_ranks)."""
+    for k in list(TEST_GEOM) + ["NCCL_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS",
+                                "NCCL_MAX_NRINGS", "NCCL_MIN_CTAS", "NCCL_MAX_CTAS", "VCCL_CHANNELS_PER_RING"]:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("VCCL_ALLOW_SHARED_DEVICE", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    comms = nccl.Comm.init_all([0, 0])
+    try:
+        assert [c.n_channels() for c in comms] == [want, want]
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 @pytest.mark.parametrize("n,geom", [(2, "test"), (3, "test"), (4, "test"), (4, "ll128"), (2, "default")])
 def test_reduce(n, geom):
     """ncclReduce (reduce.h ring): RC.REDUCE_CASES at every root, bit-exact

@@ -271,8 +271,15 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   int perRing = (int)param_int("CHANNELS_PER_RING",
                                std::max(1, std::min(perRingModel, kVcclMaxChannels / nRings)));
   int nch = (int)param_int("NCHANNELS", (int64_t)perRing * nRings);
-  // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490)
+  // minCTAs / maxCTAs bound the channel count (graph/connect.cc:486-490), and
+  // so do NCCL_MIN_NCHANNELS / NCCL_MAX_NCHANNELS (legacy MIN_NRINGS /
+  // MAX_NRINGS, connect.cc:326-360)
   nch = std::max(c->minCTAs, std::min(nch, c->maxCTAs));
+  int64_t minNch = param_int("MIN_NRINGS", -2), maxNch = param_int("MAX_NRINGS", -2);
+  if (param_int("MIN_NCHANNELS", -2) != -2) minNch = param_int("MIN_NCHANNELS", -2);
+  if (param_int("MAX_NCHANNELS", -2) != -2) maxNch = param_int("MAX_NCHANNELS", -2);
+  if (maxNch != -2) nch = std::min<int64_t>(nch, std::max<int64_t>(1, maxNch));
+  if (minNch > 0) nch = std::max<int64_t>(nch, minNch);
   nch = std::max(1, std::min(nch, kMaxChannels));
   c->nChannels = n > 1 ? nch : 0;
   // Step = VCCL's FIFO step: NCCL_BUFFSIZE / NCCL_STEPS (init.cc:619-633,

@@ -384,6 +384,13 @@ class Comm:
               "vcclCommLaunchStats")
         return a.value, b.value
 
+    def n_channels(self) -> int:
+        """The ring channel count of this communicator (vcclCommRingTrace's
+        size query, which needs no trace buffer)."""
+        nch = ctypes.c_int()
+        lib().vcclCommRingTrace(self.handle, None, 0, ctypes.byref(nch), None)
+        return nch.value
+
     def ring_trace(self):
         """vcclCommRingTrace: the SIMPLE ring's slot timeline of the last launch
         as a numpy structured array [nChannels, cap] (VCCL_RING_TRACE at init)."""
