@@ -145,6 +145,26 @@ def test_oracle_chain_fold_order():
             assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (dt, n)
 
 
+def test_reduce_expectation_fold_order():
+    """The ring reduce's expected output (tests/_ring.py expected_reduce,
+    reduce.h:12-55) restated element by element with numpy's IEEE f32 adds:
+    on one channel of ring R the chunk starts at root's successor, every
+    next rank computes own + received, and the root ends with own + received
+    — x_root + (x_{R[i-1]} + (... + x_{R[i+1]})) for root = R[i]."""
+    from tests import _ring
+    rng = np.random.default_rng(13)
+    for n in (2, 3, 4, 5):
+        xs = [rng.uniform(-1, 1, 1001).astype(np.float32) for _ in range(n)]
+        ring = _ring.ring_orders(n)[0]
+        for root in range(n):
+            i = ring.index(root)
+            acc = xs[ring[(i + 1) % n]].copy()
+            for k in range(2, n + 1):
+                acc = (xs[ring[(i + k) % n]] + acc).astype(np.float32)
+            got = _ring.expected_reduce(0, 7, xs, root, 1)
+            assert np.array_equal(got.view(np.uint8), acc.view(np.uint8)), (n, root)
+
+
 # ---------------------------------------------------------------- fp8
 # The reference reduces fp8 through __half (reduce_kernel.h:309-321) with
 # CUDA's cuda_fp8.h conversions (absent here).  The oracle's conversions and
