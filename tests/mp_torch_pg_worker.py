@@ -70,6 +70,18 @@ def main():
     base = torch.arange(4099, device="cuda", dtype=torch.float32) % 31
     if not torch.equal(rd, base * world + world * (world - 1) / 2 if rank == world - 1 else base + rank):
         bad.append(("reduce", 4099))
+    # uneven lists: torch runs these as grouped ncclBroadcast / ncclReduce
+    sizes = [1000 + 37 * r for r in range(world)]
+    mine = torch.full((sizes[rank],), float(rank + 1), device="cuda")
+    outs = [torch.empty(sz, device="cuda") for sz in sizes]
+    dist.all_gather(outs, mine)
+    if not all(torch.equal(o, torch.full_like(o, float(r + 1))) for r, o in enumerate(outs)):
+        bad.append(("all_gather uneven", sizes))
+    ins = [torch.full((sz,), float(rank + r), device="cuda") for r, sz in enumerate(sizes)]
+    got = torch.empty(sizes[rank], device="cuda")
+    dist.reduce_scatter(got, ins)
+    if not torch.equal(got, torch.full_like(got, float(world * rank + world * (world - 1) / 2))):
+        bad.append(("reduce_scatter uneven", sizes))
     torch.manual_seed(rank)
     model = torch.nn.Linear(64, 32).cuda()
     torch.manual_seed(0)

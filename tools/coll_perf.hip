@@ -1,12 +1,12 @@
 // nccl-tests-style driver (all_reduce_perf / reduce_scatter_perf /
-// all_gather_perf) written against the C API only: include/nccl.h +
+// all_gather_perf / broadcast_perf / reduce_perf) written against the C API only: include/nccl.h +
 // libvccl.so, exactly as a C/C++ caller of the reference links libnccl.
 // SURVEY.md §8b names nccl-tests as the path's caller; this is the same
 // shape of program (size sweep, algbw / busbw columns, #wrong), not a copy.
 //
-//   coll_perf -C allreduce|reducescatter|allgather -r <ranks> -b <min bytes>
-//             -e <max bytes> -f <factor> -n <iters> -w <warmup>
-//             -d float|half|bfloat16|int32|double -o sum|max|min
+//   coll_perf -C allreduce|reducescatter|allgather|broadcast|reduce -r <ranks>
+//             -b <min bytes> -e <max bytes> -f <factor> -n <iters> -w <warmup>
+//             -d float|half|bfloat16|int32|double -o sum|max|min -R <root>
 //
 // One process per rank: the parent creates the unique id (sockets only, no
 // GPU call), forks the ranks and waits; each rank uses GPU (rank % ndev).
@@ -66,7 +66,7 @@ __global__ void fill(T* p, size_t n, size_t base, int r) {
 
 struct Args {
   std::string coll = "allreduce", dtype = "float", op = "sum";
-  int ranks = 2, iters = 20, warmup = 5;
+  int ranks = 2, iters = 20, warmup = 5, root = 0;
   size_t minBytes = 8, maxBytes = 64 << 20;
   double factor = 2;
 };
@@ -75,10 +75,11 @@ static ncclRedOp_t op_of(const std::string& s) {
   return s == "max" ? ncclMax : s == "min" ? ncclMin : ncclSum;
 }
 
-// Expected output element j (AR: element j; RS: element rank*count + j of the
-// sum; AG: element j of the concatenation).
+// Expected output element j (AR / reduce: element j; RS: element rank*count + j
+// of the sum; AG: element j of the concatenation; broadcast: the root's).
 static double expect(const Args& a, int nranks, int rank, size_t count, size_t j) {
   if (a.coll == "allgather") return val(j % count, (int)(j / count));
+  if (a.coll == "broadcast") return val(j, a.root);
   const size_t i = a.coll == "reducescatter" ? rank * count + j : j;
   double acc = a.op == "sum" ? 0 : val(i, 0);
   for (int r = 0; r < nranks; r++) {
@@ -99,7 +100,10 @@ static int run_rank(const Args& a, int rank, ncclUniqueId id, ncclDataType_t dt)
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int n = a.ranks;
-  const double busFactor = a.coll == "allreduce" ? 2.0 * (n - 1) / n : (double)(n - 1) / n;
+  // nccl-tests' bus factors: AR 2(n-1)/n, RS / AG (n-1)/n, broadcast / reduce 1
+  const double busFactor = a.coll == "allreduce"                           ? 2.0 * (n - 1) / n
+                           : a.coll == "broadcast" || a.coll == "reduce" ? 1.0
+                                                                         : (double)(n - 1) / n;
   if (rank == 0) {
     printf("# coll_perf %s  ranks %d  dtype %s  op %s  iters %d  warmup %d (libvccl via include/nccl.h)\n",
            a.coll.c_str(), n, a.dtype.c_str(), a.op.c_str(), a.iters, a.warmup);
@@ -139,6 +143,10 @@ static int run_rank(const Args& a, int rank, ncclUniqueId id, ncclDataType_t dt)
         CK(ncclAllReduce(in, out, collCount, dt, op_of(a.op), comm, s));
       else if (a.coll == "reducescatter")
         CK(ncclReduceScatter(in, out, collCount, dt, op_of(a.op), comm, s));
+      else if (a.coll == "broadcast")
+        CK(ncclBroadcast(in, out, collCount, dt, a.root, comm, s));
+      else if (a.coll == "reduce")
+        CK(ncclReduce(in, out, collCount, dt, op_of(a.op), a.root, comm, s));
       else
         CK(ncclAllGather(in, out, collCount, dt, comm, s));
     };
@@ -162,7 +170,8 @@ static int run_rank(const Args& a, int rank, ncclUniqueId id, ncclDataType_t dt)
     std::vector<T> h(outElts);
     CK(hipMemcpy(h.data(), out, outElts * sizeof(T), hipMemcpyDeviceToHost));
     long long wrong = 0;
-    for (size_t j = 0; j < outElts; j++)
+    const bool checked = a.coll != "reduce" || rank == a.root;  // a non-root's reduce output is untouched
+    for (size_t j = 0; checked && j < outElts; j++)
       wrong += to_double(h[j]) != expect(a, n, rank, collCount, j);
     ncclResult_t ae;
     CK(ncclCommGetAsyncError(comm, &ae));
@@ -172,7 +181,7 @@ static int run_rank(const Args& a, int rank, ncclUniqueId id, ncclDataType_t dt)
     const double algbw = sz / (us * 1e-6) / 1e9;
     if (rank == 0)
       printf(" %12zu %12zu %8s %6s %10.2f %9.2f %9.2f %7lld\n", (size_t)sz, collCount,
-             a.dtype.c_str(), a.coll == "allgather" ? "none" : a.op.c_str(), us, algbw,
+             a.dtype.c_str(), a.coll == "allgather" || a.coll == "broadcast" ? "none" : a.op.c_str(), us, algbw,
              algbw * busFactor, wrong);
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
@@ -198,6 +207,7 @@ int main(int argc, char** argv) {
     else if (k == "-w") a.warmup = atoi(v.c_str());
     else if (k == "-d") a.dtype = v;
     else if (k == "-o") a.op = v;
+    else if (k == "-R") a.root = atoi(v.c_str());
     else {
       fprintf(stderr, "unknown option %s\n", k.c_str());
       return 2;
