@@ -33,7 +33,7 @@ def main():
     tr = comm.ring_trace()
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), ok=ok, nch=tr.shape[0], cus=cus,
-             t=np.stack([tr[k].astype(np.int64) for k in ("t0", "t1", "t2", "t3", "t4")], axis=-1),
+             t=np.stack([tr[k].astype(np.int64) for k in ("t0", "t1", "t2", "tc", "t3", "t4")], axis=-1),
              shape=tr["shape"].astype(np.int64), bytes=tr["bytes"].astype(np.int64))
     comm.destroy()
 

@@ -885,9 +885,9 @@ def test_ring_trace_and_shared_cap(n):
         assert bool(res[r]["ok"]), f"rank {r}: all-reduce output"
         assert int(res[r]["nch"]) == want, (int(res[r]["nch"]), want)
         t, shape, nbytes = res[r]["t"], res[r]["shape"], res[r]["bytes"]
-        used = t[..., 4] > 0
+        used = t[..., 5] > 0  # t4 stored
         assert used.any()
-        ts = t[used]
+        ts = t[used]  # t0 <= t1 <= t2 <= tc (thread 0's accesses issued) <= t3 <= t4
         assert (np.diff(ts, axis=-1) >= 0).all(), "stamps out of order"
         assert set(int(s) for s in shape[used]) <= ar_shapes
         assert nbytes[used].sum() > 0 and (nbytes[used] % 16 == 0).all()

@@ -4,7 +4,8 @@ run under torch.distributed.run (ranks may share the GPU).  For each
 collective in TRACE_COLLS on a TRACE_BYTES fp32 bucket (ring forced): two
 warm-up calls, one traced call, then per primitive shape the mean time
 waiting for credits (t1-t0), for the workgroup release (t2-t1), moving and
-draining the payload (t3-t2), posting (t4-t3), the gap to the channel's next
+draining the payload (t3-t2: thread 0's accesses issued, tc-t2, then the
+drain and the wait for the slowest wave, t3-tc), posting (t4-t3), the gap to the channel's next
 slot, and the payload rate of the copy phase.  Rank 0 prints one JSON line
 per collective.  Measurement tool, not product code."""
 import json
@@ -31,19 +32,23 @@ def summarize(tr):
         for i, r in enumerate(rec):
             d = rows.setdefault(SHAPES.get(int(r["shape"]), str(int(r["shape"]))),
                                 {"n": 0, "wait": 0.0, "release": 0.0, "copy": 0.0, "post": 0.0, "gap": 0.0,
-                                 "bytes": 0})
+                                 "issue": 0.0, "drain": 0.0, "bytes": 0})
             d["n"] += 1
             d["wait"] += (int(r["t1"]) - int(r["t0"])) / 100.0  # us (100 MHz)
             d["release"] += (int(r["t2"]) - int(r["t1"])) / 100.0
             d["copy"] += (int(r["t3"]) - int(r["t2"])) / 100.0
             d["post"] += (int(r["t4"]) - int(r["t3"])) / 100.0
+            if int(r["tc"]):  # copy = issue (thread 0's accesses issued) + drain (pipeline empty, all waves)
+                d["issue"] += (int(r["tc"]) - int(r["t2"])) / 100.0
+                d["drain"] += (int(r["t3"]) - int(r["tc"])) / 100.0
             if i + 1 < len(rec):
                 d["gap"] += (int(rec[i + 1]["t0"]) - int(r["t4"])) / 100.0
             d["bytes"] += int(r["bytes"])
     out = {}
     for k, d in rows.items():
         n = d["n"]
-        out[k] = {"n": n, **{f: round(d[f] / n, 2) for f in ("wait", "release", "copy", "post", "gap")},
+        out[k] = {"n": n, **{f: round(d[f] / n, 2) for f in ("wait", "release", "copy", "issue", "drain", "post",
+                                                              "gap")},
                   "payload_GBs_in_copy": round(d["bytes"] / (d["copy"] * 1e3), 1) if d["copy"] else None}
     return out
 

@@ -88,7 +88,7 @@ struct RingCtx {
                        int recvOff = 0, int sendOff = 0) {
     if (aborted()) return;
     const bool tr = trace != nullptr && traceN < comm->traceCap;
-    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, tc = 0;
     if (tid == 0) {
       if (tr) t0 = __builtin_amdgcn_s_memrealtime();
       bool ok = true;
@@ -129,6 +129,7 @@ struct RingCtx {
       a.postOp = postOp ? 1 : 0;
       reduce_copy<Fn, NS, ND, UNROLL, POLS, 0, true>(fn, a, nelem, 0, 1, tid, nthreads);
     }
+    if (tid == 0 && tr) tc = __builtin_amdgcn_s_memrealtime();
     drain_vmem();  // every storing wave: its write-through payload stores are complete
     __syncthreads();
     if (tid == 0) {
@@ -153,6 +154,7 @@ struct RingCtx {
         rec.shape = (RECV ? 1u : 0u) | (SEND ? 2u : 0u) | (SRC ? 4u : 0u) | (DST ? 8u : 0u);
         rec.bytes = (uint32_t)(nelem > 0 ? nelem * (int64_t)sizeof(typename Fn::EltType) : 0);
         rec.step = SEND ? sendStep : recvStep;
+        rec.tc = tc;
       }
     }
     if (tr) traceN++;

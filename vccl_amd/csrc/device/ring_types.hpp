@@ -114,13 +114,16 @@ struct DevComm {
 // One SIMPLE-ring slot hand-off, s_memrealtime ticks (100 MHz), taken by
 // thread 0: entry, credits seen, workgroup released, payload drained
 // (every wave's stores complete, second barrier), flags stored; shape =
-// RECV | SEND << 1 | SRC << 2 | DST << 3; bytes of payload.
+// RECV | SEND << 1 | SRC << 2 | DST << 3; bytes of payload; tc = thread 0's
+// own loads and stores issued (before its drain), so t3 - tc is the drain of
+// the memory pipeline plus the wait for the slowest wave.
 struct RingTraceRec {
   uint64_t t0, t1, t2, t3, t4;
   uint32_t shape, bytes;
   uint64_t step;
+  uint64_t tc;
 };
-static_assert(sizeof(RingTraceRec) == 56, "trace record layout");
+static_assert(sizeof(RingTraceRec) == 64, "trace record layout");
 
 // The part of VCCL's cbd partition a reduce-scatter needs to know which
 // channel (hence ring, hence fold order) an element of the block is on.

@@ -398,7 +398,7 @@ class Comm:
         nch, cap = ctypes.c_int(), ctypes.c_int()
         lib().vcclCommRingTrace(self.handle, None, 0, ctypes.byref(nch), ctypes.byref(cap))
         dt = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("t2", "<u8"), ("t3", "<u8"), ("t4", "<u8"),
-                       ("shape", "<u4"), ("bytes", "<u4"), ("step", "<u8")])
+                       ("shape", "<u4"), ("bytes", "<u4"), ("step", "<u8"), ("tc", "<u8")])
         out = np.zeros((nch.value, cap.value), dtype=dt)
         check(lib().vcclCommRingTrace(self.handle, out.ctypes.data_as(ctypes.c_void_p),
                                       ctypes.c_size_t(out.nbytes), None, None), "vcclCommRingTrace")
