@@ -25,6 +25,11 @@
 // 512 MiB bucket (2 ranks, 3 interleaved reps, profiles/r03j).
 #define VCCL_RING_OUT_POL kNT
 #endif
+#ifndef VCCL_RING_OUT2_POL
+// Store policy of the own output beside a FIFO slot (the two-destination
+// steps S+F->F+O, S->F+O, F->F+O): nontemporal (profiles/r03a twodst sweep).
+#define VCCL_RING_OUT2_POL kNT
+#endif
 
 namespace vccl {
 
@@ -115,7 +120,7 @@ struct RingCtx {
       constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
       constexpr int ND = (SEND ? 1 : 0) + (DST ? 1 : 0);
       constexpr int S0 = SRC ? VCCL_RING_SRC_POL : kSys, S1 = kSys;
-      constexpr int D0 = SEND ? kSys : VCCL_RING_OUT_POL, D1 = kNT;
+      constexpr int D0 = SEND ? kSys : VCCL_RING_OUT_POL, D1 = VCCL_RING_OUT2_POL;
       constexpr int POLS = mkpol(S0, S1, S1, S1, D0, D1, D1, D1);
       RCArgs a;
       int s = 0, d = 0;
