@@ -32,6 +32,100 @@ import time
 
 _T_START = time.perf_counter()  # before torch import: the line's wall time includes it
 
+
+# ------------------------------------------------------------ rank launcher
+# `bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment (a
+# driver that does not go through torch.distributed.run): this process spawns
+# the N rank processes itself — children, never an exec, and before anything
+# here touches the GPU (torch is not even imported yet) — each with RANK /
+# LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 / MASTER_PORT, so every rank
+# binds device LOCAL_RANK % device_count (one rank per GPU), and prints rank
+# 0's JSON line with n_gpus = N.  --gpus and a WORLD_SIZE that disagree are an
+# error, not a silent 1-GPU line.
+def _gpus_arg(argv):
+    """The --gpus value in argv, or None when absent."""
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return None
+
+
+def world_check(argv, env):
+    """(n, spawn): the world size this run has, and whether this process must
+    spawn the ranks.  Raises SystemExit when --gpus and WORLD_SIZE disagree."""
+    g = _gpus_arg(argv)
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if g is not None and g != int(ws):
+            raise SystemExit(f"bench.py: --gpus {g} but WORLD_SIZE={ws}; launch one process per GPU "
+                             f"(torch.distributed.run --nproc-per-node {g}) or drop WORLD_SIZE")
+        return int(ws), False
+    g = g or 1
+    if g < 1:
+        raise SystemExit(f"bench.py: --gpus {g}")
+    return g, g > 1
+
+
+def rank_launch_plan(argv, env, script=None, port=None):
+    """[(cmd, env)] of the N rank processes `bench.py --gpus N` starts."""
+    import socket
+    n, spawn = world_check(argv, env)
+    if not spawn:
+        return []
+    if port is None:
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+    script = script or os.path.abspath(__file__)
+    plan = []
+    for r in range(n):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                 VCCL_BENCH_LAUNCHER="bench.py")
+        plan.append(([sys.executable, "-u", script] + list(argv), e))
+    return plan
+
+
+def _spawn_ranks(plan, poll_s=0.5):
+    import subprocess
+    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if k == 0 else subprocess.DEVNULL)
+             for k, (cmd, e) in enumerate(plan)]
+    out0 = []
+    import threading
+    t = threading.Thread(target=lambda: out0.extend(procs[0].stdout.read().decode().splitlines()), daemon=True)
+    t.start()
+    rc, failed_at = 0, None
+    while any(p.poll() is None for p in procs):
+        bad = [p for p in procs if p.poll() not in (None, 0)]
+        if bad and failed_at is None:
+            failed_at = time.monotonic()
+            rc = bad[0].returncode
+        if failed_at is not None and time.monotonic() - failed_at > 60:
+            for p in procs:  # the exact children this process started
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(poll_s)
+    t.join(timeout=10)
+    codes = [p.returncode for p in procs]
+    rc = rc or next((c for c in codes if c), 0)
+    for line in out0:
+        if line.startswith("{"):
+            print(line, flush=True)
+        else:
+            print(line, file=sys.stderr, flush=True)
+    if rc:
+        print(f"bench.py: rank exit codes {codes}", file=sys.stderr, flush=True)
+    return rc
+
+
+if __name__ == "__main__":
+    _plan = rank_launch_plan(sys.argv[1:], os.environ)
+    if _plan:
+        sys.exit(_spawn_ranks(_plan))
+
 import numpy as np
 import torch
 
@@ -901,7 +995,10 @@ def bench_allreduce(args):
                       "bytes_per_rank": last["bytes"], "busbw_per_rank": round(last["busbw"], 2),
                       "aggregate_busbw_all_ranks": round(last["busbw"] * world, 2),
                       "algbw": round(last["algbw"], 2), "parallelism": f"{last['algo']} x{world}",
-                      "async_error": err, "correct": correct_all},
+                      "async_error": err, "correct": correct_all,
+                      "launcher": os.environ.get("VCCL_BENCH_LAUNCHER", "torch.distributed.run"),
+                      "devices": {"visible": torch.cuda.device_count(),
+                                  "ranks_per_device": -(-world // max(1, torch.cuda.device_count()))}},
            "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": round(peak, 2),
                         "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
                         "note": (f"per-rank busbw vs {links} link(s) x {XGMI_LINK_GBS} GB/s per link and "
@@ -1254,7 +1351,7 @@ def main():
     ap.add_argument("--nt-stores", type=int, default=0)
     ap.add_argument("--preroll-s", type=float, default=0.5)
     args = ap.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world, _ = world_check(sys.argv[1:], os.environ)
     workload = args.workload or ("reduce_copy" if world == 1 else "allreduce")
     if workload == "reduce_copy":
         out = bench_reduce_copy(args)

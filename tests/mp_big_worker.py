@@ -16,6 +16,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 BIG = (1 << 29) + 1037  # f32 elements: 2 GiB + 4148 B
@@ -28,9 +29,9 @@ def gen(rank, n_elts):
 
 
 def main():
-    rank, nranks, device = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    rank, nranks = int(sys.argv[1]), int(sys.argv[2])  # argv[3]: device (unused: rank % devices)
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[4]))
-    torch.cuda.set_device(device)
+    _mp.bind(rank, nranks)
     comm = nccl.Comm.init_rank(nranks, uid, rank)
     s = torch.cuda.current_stream().cuda_stream
     bad = []

@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 
@@ -260,7 +261,7 @@ def failing_calls_in_capture(comm, rank, n):
 def main():
     rank, n = int(sys.argv[1]), int(sys.argv[2])
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     small, mid, large, rc = 10_001, 600_001, 3 << 20, 100_003
     xs = torch.empty(small, device="cuda")

@@ -23,6 +23,7 @@ import torch  # noqa: E402
 
 from oracle import oracle as O  # noqa: E402
 from tests import _ring  # noqa: E402
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 COLLS = ("ar", "rs", "ag")
@@ -72,7 +73,7 @@ def main():
     rank, n = int(sys.argv[1]), int(sys.argv[2])
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
     outdir = sys.argv[4]
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     calls = stress_calls(n)

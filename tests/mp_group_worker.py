@@ -20,6 +20,7 @@ import torch  # noqa: E402
 
 from oracle import oracle as O  # noqa: E402
 from tests import _ring  # noqa: E402
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 GROUP_RS = [(f"rs{i}", 9, (8 << 20) // 2) for i in range(16)]        # (name, dtype, bucket elements)
@@ -57,7 +58,7 @@ def main():
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
     outdir = sys.argv[4]
     group_rs, group_ar, reps = SETS[sys.argv[5] if len(sys.argv) > 5 else "zero"]
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     s = torch.cuda.current_stream().cuda_stream
     bufs = {}

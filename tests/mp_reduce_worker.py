@@ -19,6 +19,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from tests import ring_cases as RC  # noqa: E402
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 # the group: (case index, root) — one aggregate of f32 sums, a bf16 sum
@@ -33,7 +34,7 @@ def main():
     rank, n = int(sys.argv[1]), int(sys.argv[2])
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
     outdir = sys.argv[4]
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     sp = torch.cuda.current_stream().cuda_stream
     res, bad = {}, []

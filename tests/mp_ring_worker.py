@@ -15,14 +15,15 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from tests import ring_cases as RC  # noqa: E402
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 
 def main():
-    rank, nranks, device = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    rank, nranks = int(sys.argv[1]), int(sys.argv[2])  # argv[3]: device (unused: rank % devices)
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[4]))
     outdir = sys.argv[5]
-    torch.cuda.set_device(device)
+    _mp.bind(rank, nranks)
     comm = nccl.Comm.init_rank(nranks, uid, rank)
     if os.environ.get("VCCL_TEST_SET_ALGO"):  # vcclCommSetAlgo for every call
         comm.set_algo(os.environ["VCCL_TEST_SET_ALGO"])

@@ -15,6 +15,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 
@@ -31,7 +32,7 @@ def allreduce_ok(comm, world, n=300_001, base=0):
 def main():
     rank, n = int(sys.argv[1]), int(sys.argv[2])
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     bad = []
     sub = comm.split(rank % 2, -rank)

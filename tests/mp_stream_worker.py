@@ -19,6 +19,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 # (collective, bytes per rank of the input)
@@ -29,7 +30,7 @@ PLAN = [("ar", 4096), ("ar", 1 << 20), ("rs", 256 << 10), ("ar", 64), ("ag", 64 
 def main():
     rank, n = int(sys.argv[1]), int(sys.argv[2])
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     streams = [torch.cuda.Stream() for _ in range(3)]
     calls = []

@@ -21,11 +21,19 @@ import torch.distributed as dist
 
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    torch.cuda.set_device(0)
+    # one rank per GPU where the box has them (rank % devices); ranks
+    # beyond the device count share (VCCL_ALLOW_SHARED_DEVICE, tests/_mp.py)
+    ndev = max(1, torch.cuda.device_count())
+    dev = rank % ndev
+    if world > ndev:
+        os.environ["VCCL_ALLOW_SHARED_DEVICE"] = "1"
+    else:
+        os.environ.pop("VCCL_ALLOW_SHARED_DEVICE", None)
+    torch.cuda.set_device(dev)
     # lazy communicator init: sub-groups get their own ncclCommInitRankConfig;
     # eager (device_id=): torch splits the default communicator (ncclCommSplit)
     if os.environ.get("VCCL_TEST_TORCH_INIT", "lazy") == "eager":
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
     else:
         dist.init_process_group("nccl", rank=rank, world_size=world)
     bad = []

@@ -14,13 +14,14 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 
 def main():
     rank, n, outdir = int(sys.argv[1]), int(sys.argv[2]), sys.argv[4]
     uid = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[3]))
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     comm.set_algo("ring")
     count = 2 << 20

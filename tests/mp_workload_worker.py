@@ -25,6 +25,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402  (pattern_fill / pattern_ok: the N>1 line's own checker)
 from tests import _workload as W  # noqa: E402
+from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
 C4_BYTES = 4 << 30
@@ -111,7 +112,7 @@ def main():
     outdir = sys.argv[4]
     geo = (int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7]))  # nch, slot, nthreads
     cases = sys.argv[8].split(",")
-    torch.cuda.set_device(0)
+    _mp.bind(rank, n)
     comm = nccl.Comm.init_rank(n, uid, rank)
     res = {}
     ok = True

@@ -222,7 +222,7 @@ def expected_ar(op, dt, ins, n_ranks, nch, slot_bytes, ll_max, direct_max, direc
 
 
 def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_chunk=16 << 20,
-             nthreads=512, proto=2, chain=None):
+             nthreads=512, proto=2, chain=None, ll_rs_max=None):
     """proto: the ring's protocol (2 SIMPLE, 1 LL128 — VCCL's LL128 partition)."""
     """Per-rank expected outputs.  All-reduce buckets of at most `ll_max`
     bytes take the one-shot LL path, whose fold is the chain-tree order
@@ -238,7 +238,9 @@ def expected(case_idx, n_ranks, nch, slot_bytes, ll_max=0, direct_max=0, direct_
         # the one-hop LL reduce-scatter (one rank's block within the LL
         # threshold, n <= 8; n x the threshold is the RS / AG default) folds
         # per channel of VCCL's LL ring partition
-        ll = n_ranks <= 8 and count * ins[0].dtype.itemsize <= ll_max
+        # (ll_rs_max: that threshold when it differs from the all-reduce's —
+        # NCCL_ALGO=Ring keeps ring LL for RS / AG but no LL all-reduce)
+        ll = n_ranks <= 8 and count * ins[0].dtype.itemsize <= (ll_max if ll_rs_max is None else ll_rs_max)
         return _ring.expected_reducescatter(op, dt, ins, nch, nthreads=nthreads,
                                             proto=_ring.S.PROTO_LL if ll else proto)
     full = np.concatenate(ins)

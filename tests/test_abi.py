@@ -159,3 +159,31 @@ os.environ["NCCL_DEBUG"] = "WARN"; L.pncclResetDebugInit(); warn()
     before, after = r.stderr.split("--mark--")
     assert "WARN" not in before, before
     assert "WARN" in after, after
+
+
+def test_get_last_error_returns_the_warn_text():
+    """ncclGetLastError (init.cc:2223-2225, debug.cc:29 / :265-272): the text
+    of the last WARN, kept whatever NCCL_DEBUG says; comm unused (NULL here).
+    A NULL-comm ncclCommCount is ncclInvalidArgument and WARNs (no GPU needed)."""
+    code = r"""
+import ctypes, os, sys
+sys.path.insert(0, sys.argv[1])
+from vccl_amd import nccl
+L = nccl.lib()
+os.environ["NCCL_DEBUG"] = "NONE"; L.ncclResetDebugInit()
+assert nccl.last_error() == "", nccl.last_error()
+v = ctypes.c_int()
+assert L.ncclCommCount(None, ctypes.byref(v)) == nccl.ncclInvalidArgument
+print(nccl.last_error())
+assert L.ncclAllReduce(None, None, 1, 99, 0, None, None) == nccl.ncclInvalidArgument
+print(L.pncclGetLastError(ctypes.c_void_p(0x10)).decode())
+"""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("NCCL_DEBUG", "VCCL_DEBUG")}
+    r = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    first, second = r.stdout.splitlines()[-2:]
+    assert first == "ncclCommCount : comm argument is NULL", first
+    assert "NULL" in second or "invalid" in second.lower(), second
+    assert "WARN" not in r.stderr  # NCCL_DEBUG=NONE: nothing printed, the text still kept

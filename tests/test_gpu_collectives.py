@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 import torch
 
+from tests import _mp
 from tests import _ring
 from tests import ring_cases as RC
 from tests._util import assert_bitexact, assert_fold_tolerance, exact_f64
@@ -50,13 +51,13 @@ DIRECT_CHUNK_TEST = 1 << 20  # buckets of 1-4 MiB stream through the inbox in ch
 
 
 def _check(ci, n, outs, nch, slot, ll_max, direct_max, chunk=DIRECT_CHUNK_TEST, nthreads=512, proto=2,
-           chain=None):
+           chain=None, ll_rs_max=None):
     """Bit-exact against the path's own fold order (the ring's IS VCCL's
     schedule on our rings and channels); for fp sum / prod additionally
     within the §8c tolerance of the exact value and of VCCL's result on its
     reference geometry (RC.vccl_reference)."""
     name, coll, op, dt, count = RC.CASES[ci]
-    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto, chain)
+    exp = RC.expected(ci, n, nch, slot, ll_max, direct_max, chunk, nthreads, proto, chain, ll_rs_max)
     for r in range(n):
         assert_bitexact(dt, outs[r], exp[r], minmax=op in (2, 3), what=f"{name} n={n} rank {r}")
     vref = RC.vccl_reference(ci, n)
@@ -94,7 +95,9 @@ def test_algorithm_choice(monkeypatch):
                     (0, (1 << 24) + 4): "ring", (0, 1 << 28): "ring",
                     (1, 1 << 10): "ll", (2, 1 << 10): "ll", (1, 16 << 10): "ll",
                     (1, 17 << 10): "ring", (2, 1 << 20): "ring", (2, 1 << 26): "ring"},
-             "Ring": {(0, 1 << 10): "ring", (0, 1 << 20): "ring", (1, 1 << 10): "ring",
+             # NCCL_ALGO=Ring: no LL all-reduce (VCCL's LL all-reduce is the
+             # tree's here), ring LL for small RS / AG
+             "Ring": {(0, 1 << 10): "ring", (0, 1 << 20): "ring", (1, 1 << 10): "ll",
                       (2, 1 << 20): "ring"},
              "Tree": {(0, 1 << 10): "ll", (0, 1 << 20): "ring", (1, 1 << 10): "ll",
                       (2, 1 << 26): "ring"},
@@ -174,12 +177,36 @@ def test_single_process_ranks(n, monkeypatch):
                                     (3, "net"), (2, "ll128"), (4, "ll128"), (8, "ll128"),
                                     (4, "chain"), (8, "chain"), (2, "net_ll128")])
 def test_multi_process_ranks(n, geom):
+    _ring_ranks(n, geom)
+
+
+# the same parity run with ONE RANK PER GPU (peer FIFOs over
+# xGMI, IPC-mapped across processes) at library defaults — fences off (the
+# default) and on, and every call on the LL128 ring — collected the first time
+# the suite runs on a box with more than one GPU.  Each rank process binds
+# device rank % device_count (tests/_mp.py).
+def _multi_gpu_ns():
+    ndev = torch.cuda.device_count()
+    return sorted({2, min(ndev, 8)}) if ndev >= 2 else [2]
+
+
+@pytest.mark.parametrize("geom", ["xgmi", "xgmi_fences", "xgmi_ll128"])
+@pytest.mark.parametrize("n", _multi_gpu_ns())
+def test_one_rank_per_gpu(n, geom):
+    ndev = torch.cuda.device_count()
+    if ndev < n:
+        pytest.skip(f"one rank per GPU needs {n} GPUs; this box has {ndev} "
+                    "(the shared-GPU rehearsals above cover the protocol)")
+    _ring_ranks(n, geom)
+
+
+def _ring_ranks(n, geom):
     uid = nccl.get_unique_id()  # root thread lives in this process
     hexid = nccl.unique_id_to_bytes(uid).hex()
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
     ll_max, direct_max, chunk = LL_DEFAULT, DIRECT_TEST, DIRECT_CHUNK_TEST
-    nthreads, proto, chain = 512, 2, None
+    nthreads, proto, chain, ll_rs_max = 512, 2, None, None
     if geom == "chain":
         # VERDICT r3 missing #2: the LL all-reduce folds along a chain other
         # than the identity (VCCL's tree chain follows its topology order,
@@ -199,9 +226,10 @@ def test_multi_process_ranks(n, geom):
     elif geom in ("test", "ring_only", "direct_only"):
         env.update(TEST_GEOM)
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
-        if geom == "ring_only":  # NCCL_ALGO forces the ring for every size
-            env["NCCL_ALGO"] = "Ring"
+        if geom == "ring_only":  # NCCL_ALGO=Ring: the ring for every all-reduce,
+            env["NCCL_ALGO"] = "Ring"  # ring LL (one-hop) for small RS / AG
             ll_max = direct_max = 0
+            ll_rs_max = LL_DEFAULT
         if geom == "direct_only":  # every collective takes the direct path, any size
             env["NCCL_ALGO"] = "Direct"
             ll_max, direct_max = 0, 1 << 62
@@ -219,6 +247,19 @@ def test_multi_process_ranks(n, geom):
             # no LL128 slot is mapped there, so every call must take the
             # SIMPLE ring, not a ring of null LL128 slots
             env.update(VCCL_LL128_ALLOC="1", VCCL_TEST_SET_ALGO="ll128")
+    elif geom.startswith("xgmi"):
+        # library defaults, one rank per device (nothing shared, no cap)
+        for k in TEST_GEOM:
+            env.pop(k, None)
+        nch, slot = _ring.n_channels(n), 512 << 10
+        ll_max = (64 << 10) if n <= 2 else (128 << 10)
+        direct_max, chunk = (8 << 20) if n >= 4 else 0, 16 << 20
+        if geom == "xgmi_fences":  # system-scope acquire / release around every slot
+            env["VCCL_FENCES"] = "1"
+        if geom == "xgmi_ll128":  # every collective on the LL128 ring
+            env["NCCL_PROTO"] = "LL128"
+            ll_max = direct_max = 0
+            proto = 1
     elif geom == "default8":
         # library defaults except the LL grid (8 ranks share the one GPU)
         for k in TEST_GEOM:
@@ -237,7 +278,7 @@ def test_multi_process_ranks(n, geom):
         direct_max, chunk = (8 << 20) if n >= 4 else 0, 16 << 20
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_ring_worker.py"),
-                                   str(r), str(n), "0", hexid, d], env=env,
+                                   str(r), str(n), "0", hexid, d], env=_mp.worker_env(env),
                                   stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(n)]
         logs = []
@@ -254,7 +295,7 @@ def test_multi_process_ranks(n, geom):
         res = [np.load(os.path.join(d, f"rank{r}.npz")) for r in range(n)]
         for ci, case in enumerate(RC.CASES):
             _check(ci, n, [res[r][case[0]] for r in range(n)], nch, slot, ll_max, direct_max, chunk,
-                   nthreads, proto, chain)
+                   nthreads, proto, chain, ll_rs_max)
         assert [str(a) for a in res[0]["group_algos"]] == [str(a) for a in res[0]["lib_group_algos"]]
         _check_group(n, [{k: res[r][k] for k in res[r].files} for r in range(n)], nch, slot,
                      [str(a) for a in res[0]["group_algos"]], nthreads, chain)
@@ -810,8 +851,9 @@ def test_group_plan_stress(geom):
     algos = [str(a) for a in res[0]["algos"]]
     assert algos == [str(a) for a in res[0]["lib_algos"]]  # oracle aggregation == library's
     assert set(algos) <= {"ll", "ring", "direct", "ll128"}, algos
-    if geom == "ring_only":
-        assert set(algos) == {"ring"}
+    if geom == "ring_only":  # NCCL_ALGO=Ring: the ring, ring LL for small RS / AG only
+        assert set(algos) <= {"ring", "ll"} and "ring" in algos, algos
+        assert all(c in ("rs", "ag") for (_, c, _, _, _), a in zip(calls, algos) if a == "ll"), algos
     elif geom == "ll128_window":
         assert set(algos) == {"ll", "ll128", "direct", "ring"}, algos  # all four paths in one plan
     else:
@@ -879,7 +921,7 @@ def test_ring_trace_and_shared_cap(n):
         assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)
         res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(n)]
     cus = int(res[0]["cus"])
-    want = min(_ring.n_channels(n), max(1, cus * 7 // 8 // n))
+    want = _mp.shared_channel_cap(n, _ring.n_channels(n), cus)
     ar_shapes = {0b0110, 0b0111, 0b1111, 0b1011, 0b1001}  # S->F, S+F->F, S+F->F+O, F->F+O, F->O
     for r in range(n):
         assert bool(res[r]["ok"]), f"rank {r}: all-reduce output"

@@ -1,0 +1,78 @@
+"""The hot path's failure handling on MI355X.
+
+VCCL polls an abort word in every spin (src/device/primitives.h:142-152) and
+ncclCommAbort raises it and reclaims the comm waiting only on its own work
+(src/init.cc:2079-2111).  Here every spin of the ring, LL and direct kernels
+checks the abort word and a no-progress timeout (VCCL_SPIN_TIMEOUT_S), and
+comm_destroy waits on the comm's own launches (host/init.cc
+wait_own_launches), never the whole device.  With one rank that never
+enqueues (tests/mp_fail_worker.py):
+  * the other ranks' ring, LL and direct all-reduce kernels end within the
+    spin timeout, ncclCommGetAsyncError reports ncclRemoteError, and
+    ncclCommAbort / ncclCommDestroy return;
+  * ncclCommAbort from a second host thread ends a kernel spinning on the
+    lost peer long before its timeout;
+and the process stays usable (a torch kernel and vcclReduceCopy, exact).
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from tests import _mp  # noqa: E402
+from vccl_amd import nccl  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(n, mode, ncomms, spin_timeout):
+    uids = ",".join(nccl.unique_id_to_bytes(nccl.get_unique_id()).hex() for _ in range(ncomms))
+    env = _mp.worker_env(os.environ)
+    env["VCCL_SPIN_TIMEOUT_S"] = str(spin_timeout)
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mp_fail_worker.py"),
+                                   str(r), str(n), d, mode, uids], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        logs = []
+        for p in procs:
+            try:
+                logs.append(p.communicate(timeout=300)[0].decode(errors="replace")[-3000:])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(logs)
+        res = []
+        for r in range(n):
+            with open(os.path.join(d, f"rank{r}.json")) as f:
+                res.append(json.load(f))
+    return res, "\n".join(logs)
+
+
+def test_lost_peer_ends_ring_ll_direct_kernels():
+    n, timeout_s = 3, 3
+    res, logs = _run(n, "peer_loss", 3, timeout_s)
+    for r in res[:-1]:
+        for path in ("ring", "ll", "direct"):
+            v = r[path]
+            assert v["ok"], (r["rank"], path, v, logs)
+            assert v["async_error"] == nccl.ncclRemoteError
+        assert r["usable_after"], (r, logs)
+    assert res[-1]["ok"] and res[-1]["lost_peer"]
+
+
+def test_abort_from_second_thread_ends_spinning_kernel():
+    res, logs = _run(2, "abort", 1, 60)  # the spin timeout alone would take 60 s
+    v = res[0]["abort_thread"]
+    assert v["ok"], (v, logs)
+    assert v["kernel_end_s"] < 20 and v["abort_s"] < 15
+    assert res[0]["usable_after"], (res[0], logs)

@@ -23,6 +23,7 @@ import numpy as np
 import pytest
 import torch
 
+from tests import _mp
 from tests import _ring
 from tests import _workload as W
 from tests._util import assert_bitexact
@@ -46,6 +47,10 @@ def _run(n, geom):
         env.update(TEST_GEOM)
         nch, slot, nt = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"]), 512
     else:
+        # geom "xgmi" / "xgmi_fences": one rank per GPU, the
+        # latter with system-scope fences around every FIFO slot
+        if geom == "xgmi_fences":
+            env["VCCL_FENCES"] = "1"
         # library defaults: nothing overridden — no channel, LL-grid or
         # direct-grid knob — so the co-residency caps that ranks sharing one
         # GPU get (host/init.cc: 7/8 of the CUs / sharing ranks, for ring
@@ -53,15 +58,14 @@ def _run(n, geom):
         # capture abort, 10b3277) are what runs
         for k in TEST_GEOM:
             env.pop(k, None)
-        env["VCCL_ALLOW_SHARED_DEVICE"] = "1"
         cus = torch.cuda.get_device_properties(0).multi_processor_count
-        nch, slot, nt = min(_ring.n_channels(n), max(1, cus * 7 // 8 // n)), 512 << 10, 512
+        nch, slot, nt = _mp.shared_channel_cap(n, _ring.n_channels(n), cus), 512 << 10, 512
     uid = nccl.get_unique_id()
     hexid = nccl.unique_id_to_bytes(uid).hex()
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mp_workload_worker.py"),
                                    str(r), str(n), hexid, d, str(nch), str(slot), str(nt), ",".join(CASES)],
-                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                                  env=_mp.worker_env(env), stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
                  for r in range(n)]
         logs = []
         for p in procs:
@@ -78,9 +82,15 @@ def _run(n, geom):
     return res, (nch, slot, nt)
 
 
+_NDEV = torch.cuda.device_count()
+_MULTI = [(min(_NDEV, 8), g) for g in ("xgmi", "xgmi_fences")] if _NDEV >= 2 else [(2, "xgmi")]
+
+
 @pytest.mark.timeout(1200)
-@pytest.mark.parametrize("n,geom", [(2, "default"), (4, "test"), (8, "default")])
+@pytest.mark.parametrize("n,geom", [(2, "default"), (4, "test"), (8, "default")] + _MULTI)
 def test_baseline_workloads_full_size(n, geom):
+    if geom.startswith("xgmi") and _NDEV < n:
+        pytest.skip(f"one rank per GPU needs {n} GPUs; this box has {_NDEV}")
     res, geo = _run(n, geom)
     # config 4: pattern over the whole outputs
     for case in ("c4", "c4_direct"):

@@ -166,24 +166,29 @@ def test_budget_splits_plans():
 
 
 def test_algo_selection():
-    LL, LL128, SIMPLE, DIRECT = 1, 2, 4, 8
+    LL, LL128, SIMPLE, DIRECT, LLRS = 1, 2, 4, 8, 16  # LL: the LL all-reduce; LLRS: LL RS / AG
     cases = {
-        (None, None): (0, LL | LL128 | SIMPLE | DIRECT),
+        (None, None): (0, LL | LLRS | LL128 | SIMPLE | DIRECT),
         (None, "LL128"): (4, LL128),
-        (None, "^LL128"): (0, LL | SIMPLE | DIRECT),      # excludes LL128
-        (None, "LL,LL128"): (0, LL | LL128),              # no longer "LL128 everywhere"
-        (None, "ll"): (2, LL),
+        (None, "^LL128"): (0, LL | LLRS | SIMPLE | DIRECT),  # excludes LL128
+        (None, "LL,LL128"): (0, LL | LLRS | LL128),         # no longer "LL128 everywhere"
+        (None, "ll"): (2, LL | LLRS),
         (None, "Simple"): (0, SIMPLE | DIRECT),
-        ("Ring", None): (0, LL128 | SIMPLE),
+        ("Ring", None): (0, LLRS | LL128 | SIMPLE),         # ring LL for RS / AG
         ("Ring", "Simple"): (1, SIMPLE),
-        ("Tree", None): (2, LL),
+        ("Ring", "LL"): (2, LLRS),                          # ring + LL is a valid pair
+        ("Tree", None): (2, LL | LLRS),
+        ("Tree", "Simple"): (1, SIMPLE),                    # no SIMPLE tree here: the SIMPLE ring, WARNed
+        ("Tree", "LL128"): (1, SIMPLE),
         ("Direct", None): (3, DIRECT),
-        ("^Direct", None): (0, LL | LL128 | SIMPLE),
-        ("ring;allreduce:tree", None): (0, LL128 | SIMPLE),  # per-collective entries ignored
+        ("^Direct", None): (0, LL | LLRS | LL128 | SIMPLE),
+        ("ring;allreduce:tree", None): (0, LLRS | LL128 | SIMPLE),  # per-collective entries ignored
     }
     for (algo, proto), want in cases.items():
         assert nccl.algo_selection(algo, proto) == want, (algo, proto)
-    for algo, proto in ((None, "bogus"), ("Ring,Foo", None), (None, "^LL,LL128,Simple")):
+    # unknown names, or lists that leave no protocol / no algorithm at all
+    for algo, proto in ((None, "bogus"), ("Ring,Foo", None), (None, "^LL,LL128,Simple"),
+                        ("^Tree,Ring,CollnetDirect,CollnetChain,NVLS,NVLSTree,PAT,Direct", None)):
         with pytest.raises(nccl.VcclError) as e:
             nccl.algo_selection(algo, proto)
         assert e.value.code == nccl.ncclInvalidUsage

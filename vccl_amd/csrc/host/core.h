@@ -26,6 +26,8 @@ namespace vccl {
 enum LogLevel { kLogNone = 0, kLogWarn = 1, kLogInfo = 2, kLogTrace = 3 };
 int log_level();
 void reset_log_level();
+// The last WARN's text (ncclGetLastError), kept whatever the log level.
+const char* last_error();
 void log_msg(int level, const char* file, int line, const char* fmt, ...)
     __attribute__((format(printf, 4, 5)));
 #define VWARN(...) ::vccl::log_msg(::vccl::kLogWarn, __FILE__, __LINE__, __VA_ARGS__)
@@ -185,6 +187,8 @@ struct ncclComm {
 namespace vccl {
 constexpr uint64_t kCommMagic = 0x76636363'6c6d6933ull;  // "vccclmi3"
 ncclResult_t comm_check(const ncclComm* comm, const char* api);
+// Waits until every eager launch of `comm` has completed (init.cc).
+ncclResult_t comm_wait_own_launches(ncclComm* comm);
 
 // Net proxy (proxy.cc).  net_listen opens this rank's listener before the
 // peer exchange (address published in `me`); net_connect builds the

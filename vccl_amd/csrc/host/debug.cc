@@ -38,16 +38,24 @@ int log_level() {
 // ncclResetDebugInit (debug.cc:367-378): the next log call re-reads the level
 void reset_log_level() { g_level.store(-1, std::memory_order_relaxed); }
 
+// ncclLastError (debug.cc:29): the last WARN as human-readable text, saved
+// before the level filter (debug.cc:265-272), returned by ncclGetLastError.
+static std::mutex g_mu;
+static char g_lastError[1024] = "";
+const char* last_error() { return g_lastError; }
+
 void log_msg(int level, const char* file, int line, const char* fmt, ...) {
-  if (log_level() < level) return;
-  static std::mutex mu;
+  const bool warn = level == kLogWarn;
+  if (!warn && log_level() < level) return;
   char buf[1024];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
   va_end(ap);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (warn) memcpy(g_lastError, buf, sizeof(buf));
+  if (log_level() < level) return;
   const char* base = strrchr(file, '/');
-  std::lock_guard<std::mutex> lk(mu);
   fprintf(stderr, "[vccl %d] %s %s:%d %s\n", (int)getpid(), level == kLogWarn ? "WARN" : "INFO",
           base ? base + 1 : file, line, buf);
 }

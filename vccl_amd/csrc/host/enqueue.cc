@@ -1101,6 +1101,7 @@ static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, cons
         hipStreamWaitEvent(s0, comm->joinEvent, 0) != hipSuccess)
       r = ncclUnhandledCudaError;
   }
+  bool bound = false;  // a launch of this sequence carries the ordering event
   for (size_t k = 0; k < runs.size() && r == ncclSuccess; k++) {
     // every launch goes onto s0 (the launchers use their first task's
     // stream): runs of one comm must never overlap on its channels
@@ -1111,9 +1112,18 @@ static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, cons
     r = algo == kAlgoLL ? launch_ll(run.data(), n, stop)
         : algo == kAlgoDirect ? launch_direct(run.data(), n, stop)
                               : launch_ring(run.data(), n, algo == kAlgoRingLL128, stop);
+    bound |= r == ncclSuccess && stop != nullptr;
     if (n > 1) comm->fusedLaunches++;
   }
-  if (r == ncclSuccess) r = stream_mark(comm, s0, cs);
+  if (r == ncclSuccess) {
+    r = stream_mark(comm, s0, cs);
+  } else if (bound) {
+    // an earlier run already bound the ordering event to its
+    // kernel on s0, so the next call from another stream must still wait on
+    // it even though a later run of this sequence failed
+    comm->lastStream = s0;
+    comm->hasLastLaunch = true;
+  }
   const hipEvent_t done = stream_last_event(comm, cs);
   for (hipStream_t s : others)
     if (r == ncclSuccess && hipStreamWaitEvent(s, done, 0) != hipSuccess)

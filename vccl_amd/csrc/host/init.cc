@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstddef>
 #include <cstring>
 #include <string>
@@ -87,13 +88,18 @@ std::vector<std::vector<int>> ring_orders(int n) {
 // (graph/tuning.cc:53-116) — a comma list of names, case-insensitive, a
 // leading '^' enables everything but the listed ones; per-collective
 // "func:list" entries after a ';' are not supported here (WARNed and
-// ignored).  Unknown names fail init with ncclInvalidUsage, as the
-// reference's tuner does.  Paths: LL (protocol LL / algorithm Tree), LL128
-// ring, SIMPLE ring, and the direct path (algorithm "Direct", an extension;
-// allowed only while NCCL_ALGO is unset or lists it).  A path is forced when
-// it is the only one the lists leave; otherwise the excluded ones are
-// dropped from the automatic choice.
-enum { kAllowLL = 1, kAllowLL128 = 2, kAllowSimple = 4, kAllowDirect = 8 };
+// ignored).  Unknown names, or lists that leave no protocol or no algorithm
+// at all, fail init with ncclInvalidUsage.  Paths: the one-hop LL
+// all-reduce (protocol LL, algorithm Tree: it restates VCCL's chain-tree LL
+// fold), the one-hop LL reduce-scatter / all-gather (protocol LL, algorithm
+// Tree or Ring: they restate VCCL's ring-LL fold), the LL128 ring, the SIMPLE
+// ring, and the direct path (algorithm "Direct", an extension; allowed only
+// while NCCL_ALGO is unset or lists it).  A path is forced when it is the
+// only one the lists leave; otherwise the excluded ones are dropped from the
+// automatic choice.  A pair the reference accepts but no path here serves
+// (e.g. Tree with Simple: VCCL's SIMPLE tree is out of scope) falls back to
+// the SIMPLE ring with a WARN.
+enum { kAllowLL = 1, kAllowLL128 = 2, kAllowSimple = 4, kAllowDirect = 8, kAllowLLRsAg = 16 };
 static ncclResult_t parse_name_list(const char* env, const char* str, const char* const* names, int nNames,
                                     unsigned* mask) {
   *mask = (1u << nNames) - 1;
@@ -139,20 +145,29 @@ ncclResult_t algo_proto_select(const char* algo, const char* proto, int* force, 
   unsigned p = 0, a = 0;
   NCCLCHECK(parse_name_list("NCCL_PROTO", proto, kProtos, 3, &p));
   NCCLCHECK(parse_name_list("NCCL_ALGO", algo, kAlgos, 8, &a));
+  if (p == 0 || a == 0) {
+    VWARN("NCCL_ALGO=%s / NCCL_PROTO=%s leave no %s", algo ? algo : "", proto ? proto : "",
+          p == 0 ? "protocol" : "algorithm");
+    return ncclInvalidUsage;
+  }
   const bool tree = a & 1, ring = a & 2, direct = a & 0x80;
-  // the one-hop LL path restates VCCL's chain-tree LL fold: algorithm Tree;
-  // the direct path moves SIMPLE-style bulk copies
+  // the one-hop LL all-reduce restates VCCL's chain-tree LL fold (Tree), the
+  // one-hop LL reduce-scatter / all-gather its ring-LL one (Tree or Ring, as
+  // before: VCCL's tree carries no RS / AG); the direct path moves
+  // SIMPLE-style bulk copies
   int m = 0;
-  if ((p & 1) && tree) m |= kAllowLL;
+  if ((p & 1) && tree) m |= kAllowLL | kAllowLLRsAg;
+  if ((p & 1) && ring) m |= kAllowLLRsAg;
   if ((p & 2) && ring) m |= kAllowLL128;
   if ((p & 4) && ring) m |= kAllowSimple;
   if ((p & 4) && direct) m |= kAllowDirect;
   if (m == 0) {
-    VWARN("NCCL_ALGO=%s / NCCL_PROTO=%s leave no algorithm and protocol", algo ? algo : "",
-          proto ? proto : "");
-    return ncclInvalidUsage;
+    VWARN("NCCL_ALGO=%s / NCCL_PROTO=%s: no path of this library serves that pair; using the SIMPLE ring",
+          algo ? algo : "", proto ? proto : "");
+    m = kAllowSimple;
   }
-  const int f = m == kAllowDirect ? 3 : m == kAllowLL128 ? 4 : m == kAllowSimple ? 1 : m == kAllowLL ? 2 : 0;
+  const int f = m == kAllowDirect ? 3 : m == kAllowLL128 ? 4 : m == kAllowSimple ? 1
+                : (m & ~(kAllowLL | kAllowLLRsAg)) == 0 ? 2 : 0;
   *force = f;
   *allowed = m;
   return ncclSuccess;
@@ -464,7 +479,8 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
     }
   }
   // paths NCCL_ALGO / NCCL_PROTO exclude drop out of the automatic choice
-  if (!(c->algoAllowed & kAllowLL)) c->llMaxBytes = c->llRsAgMaxBytes = 0;
+  if (!(c->algoAllowed & kAllowLL)) c->llMaxBytes = 0;
+  if (!(c->algoAllowed & kAllowLLRsAg)) c->llRsAgMaxBytes = 0;
   if (!(c->algoAllowed & kAllowDirect)) c->directMaxBytes = c->directRsAgMaxBytes = 0;
   if (n > 1) NCCLCHECK(net_listen(c, &me));
   VINFO("rank %d: exchange peer info", c->rank);
@@ -788,21 +804,62 @@ ncclResult_t comm_init_rank(ncclComm_t* out, int nranks, const ncclUniqueId* id,
   return ncclSuccess;
 }
 
+// Wait for THIS comm's launches only — its ordering event, which every eager
+// launch of the comm records (bound to the kernel's completion, or a marker
+// behind it; enqueue.cc stream_mark), and the launches of one comm are
+// serialised through it, so the last one done means all done.  The
+// reference's commReclaim likewise waits on the comm's own strong stream
+// (src/init.cc:2079-2111), never the whole device: a hipDeviceSynchronize
+// here would also wait for other comms' kernels (possibly stuck on a lost
+// peer of their own) and for unrelated user work.  timeoutS < 0: no bound.
+// Captured launches belong to their graphs (the caller's to wait for).
+static bool wait_own_launches(ncclComm* c, double timeoutS) {
+  if (!c->hasLastLaunch || !c->lastLaunch) return true;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipEventQuery(c->lastLaunch);
+    if (e != hipErrorNotReady) return true;  // done (or the event is unusable: nothing to wait for)
+    if (timeoutS >= 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeoutS)
+      return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+ncclResult_t comm_wait_own_launches(ncclComm* c) { return wait_own_launches(c, -1) ? ncclSuccess : ncclInternalError; }
+
 ncclResult_t comm_destroy(ncclComm* c, bool abort) {
   int old = -1;
   (void)hipGetDevice(&old);
   (void)hipSetDevice(c->device);
-  if (abort && c->abortFlag) *c->abortFlag = 1;
-  (void)hipDeviceSynchronize();
+  // ncclCommAbort (init.cc:2079-2111): raise the abort word every spin of the
+  // comm's kernels polls (ring.hpp / ll.hpp / direct.hpp, as checkAbort,
+  // primitives.h:142-152), then wait for the comm's own work only.
+  if (abort && c->abortFlag) __atomic_store_n((int*)c->abortFlag, 1, __ATOMIC_RELEASE);
+  // An aborting kernel leaves within a few hundred spins; one still queued
+  // behind other work on its stream will read the abort word when it starts,
+  // so after the bound the comm's memory is left allocated (a kernel may
+  // still touch it) rather than freed under it.
+  const double bound = abort ? (double)param_int("ABORT_WAIT_S", 10) : -1.0;
+  const bool drained = wait_own_launches(c, bound);
   // Peers in OTHER processes may still post a last credit into our flags:
-  // rendezvous before freeing.  Comms of one process (ncclCommInitAll) are
+  // rendezvous before freeing.  Not after an abort or an error: the peer that
+  // failed may never come (the kernels have ended, so no credit is in
+  // flight from this side either).  Comms of one process (ncclCommInitAll) are
   // legitimately destroyed one after another by a single thread (as with the
   // reference), so a barrier there would deadlock; their kernels are already
-  // complete once the owning devices have synchronised.
+  // complete once their own launches are.
   bool remotePeers = false;
   for (const auto& p : c->peers) remotePeers |= p.pid != (int)getpid();
-  if (!abort && remotePeers && c->bootstrap && c->nRanks > 1) (void)bootstrap_barrier(c->bootstrap);
-  free_resources(c);
+  const bool failed = c->asyncError.load() != 0 || (c->errorFlag && *(volatile int*)c->errorFlag);
+  if (!abort && !failed && remotePeers && c->bootstrap && c->nRanks > 1) (void)bootstrap_barrier(c->bootstrap);
+  if (!drained) {
+    VWARN("comm %p rank %d: its last launch has not ended %.0f s after the abort; its device memory is left "
+          "allocated", (void*)c, c->rank, bound);
+    net_stop(c);
+  } else {
+    free_resources(c);
+  }
   bootstrap_close(c->bootstrap);
   c->bootstrap = nullptr;
   c->destroyed = true;
@@ -985,14 +1042,16 @@ VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
   return ncclSuccess;
 }
 
+// ncclCommFinalize (init.cc commFinalize): every operation of the comm has
+// completed when it returns — its own launches, not the whole device.
 VCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
   NCCLCHECK(comm_check(comm, "ncclCommFinalize"));
   int old = -1;
   (void)hipGetDevice(&old);
   (void)hipSetDevice(comm->device);
-  hipError_t e = hipDeviceSynchronize();
+  const ncclResult_t r = comm_wait_own_launches(comm);
   if (old >= 0) (void)hipSetDevice(old);
-  return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+  return r;
 }
 
 VCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
@@ -1021,7 +1080,9 @@ VCCL_EXPORT const char* ncclGetErrorString(ncclResult_t r) {
   }
 }
 
-VCCL_EXPORT const char* ncclGetLastError(ncclComm_t) { return ""; }
+// The text of the last WARN, whatever NCCL_DEBUG filters (debug.cc:29,
+// :265-272 ncclLastError; init.cc:2223-2225: comm unused, may be NULL).
+VCCL_EXPORT const char* ncclGetLastError(ncclComm_t) { return last_error(); }
 
 VCCL_EXPORT ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
   NCCLCHECK(comm_check(comm, "ncclCommGetAsyncError"));
@@ -1064,7 +1125,7 @@ VCCL_EXPORT ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences) {
   int old = -1;
   (void)hipGetDevice(&old);
   HIPCHECK(hipSetDevice(comm->device));
-  HIPCHECK(hipDeviceSynchronize());
+  NCCLCHECK(comm_wait_own_launches(comm));
   HIPCHECK(hipMemcpy((char*)comm->devComm + offsetof(DevComm, useFences), &useFences, sizeof(int),
                      hipMemcpyHostToDevice));
   if (old >= 0) (void)hipSetDevice(old);
@@ -1078,7 +1139,7 @@ VCCL_EXPORT ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoc
   int old = -1;
   (void)hipGetDevice(&old);
   HIPCHECK(hipSetDevice(comm->device));
-  HIPCHECK(hipDeviceSynchronize());
+  NCCLCHECK(comm_wait_own_launches(comm));
   HIPCHECK(hipMemcpy((char*)comm->devComm + offsetof(DevComm, llEpoch), &llEpoch, sizeof(uint32_t),
                      hipMemcpyHostToDevice));
   HIPCHECK(hipMemcpy((char*)comm->devComm + offsetof(DevComm, dEpoch), &directEpoch,

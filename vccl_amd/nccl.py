@@ -73,6 +73,11 @@ class vcclLaunchConfig(ctypes.Structure):
 _lib = None
 
 
+def last_error(comm=None) -> str:
+    """ncclGetLastError: the last WARN's text (comm unused, may be None)."""
+    return (lib().ncclGetLastError(comm) or b"").decode(errors="replace")
+
+
 def lib() -> ctypes.CDLL:
     """Load libvccl.so (fails loudly if it was not built)."""
     global _lib
@@ -136,6 +141,9 @@ def lib() -> ctypes.CDLL:
         fn.restype = c_int
     L.ncclGetErrorString.argtypes = [c_int]
     L.ncclGetErrorString.restype = ctypes.c_char_p
+    for name in ("ncclGetLastError", "pncclGetLastError"):
+        getattr(L, name).argtypes = [vp]
+        getattr(L, name).restype = ctypes.c_char_p
     L.vcclBuildInfo.argtypes = []
     L.vcclBuildInfo.restype = ctypes.c_char_p
     _lib = L
