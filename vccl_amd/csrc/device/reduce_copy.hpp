@@ -287,10 +287,17 @@ __device__ __forceinline__ void rc_hunks(const Fn& fn, const RCArgs& a, int64_t 
 // matters when stores are slow to acknowledge (write-through sc0 sc1 stores
 // to a peer GPU's FIFO over xGMI): without it every iteration pays a full
 // store round trip.
-template <class Fn, int NS, int ND, int UNROLL, int POLS>
+//
+// `hook` runs once, right after the first hunk's NS * UNROLL loads are issued
+// (the ring's per-wave slot hand-off completes the previous slot there with a
+// partial vmcnt, so its store drain overlaps these loads: ring.hpp).
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <class Fn, int NS, int ND, int UNROLL, int POLS, class Hook = NoHook>
 __device__ __forceinline__ void rc_hunks_pipelined(const Fn& fn, const RCArgs& a, int64_t nPacks,
                                                    int64_t worker, int64_t nWorkers, int tid,
-                                                   int nthreads) {
+                                                   int nthreads, Hook&& hook = Hook{}) {
   static_assert(NS >= 1 && ND >= 1, "compile-time operand counts only");
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t nHunks = nPacks / hunkPacks;
@@ -306,6 +313,7 @@ __device__ __forceinline__ void rc_hunks_pipelined(const Fn& fn, const RCArgs& a
       for (int u = 0; u < UNROLL; u++) v[s][u] = ld16_src<POLS>(a, s, off + u * ustride);
   };
   load_hunk(cur, h);
+  hook();
   for (;;) {
     const int64_t hn = h + nWorkers;
     const bool more = hn < nHunks;
@@ -717,17 +725,17 @@ __device__ __forceinline__ bool rc_all_aligned16(const RCArgs& a) {
 }
 
 // Aligned operands: full hunks, then < one hunk of packs, then < 16 bytes.
-template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER, bool PIPE>
+template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER, bool PIPE, class Hook = NoHook>
 __device__ __forceinline__ void reduce_copy_aligned(const Fn& fn, const RCArgs& a, int64_t nElts,
                                                     int64_t worker, int64_t nWorkers, int tid,
-                                                    int nthreads) {
+                                                    int nthreads, Hook&& hook = Hook{}) {
   using T = typename Fn::EltType;
   const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
   const int64_t nPacks = nElts * (int64_t)sizeof(T) / 16;
   const int64_t hunkPacks = (int64_t)nthreads * UNROLL;
   const int64_t fullPacks = (nPacks / hunkPacks) * hunkPacks;
   if constexpr (PIPE && NS >= 1 && ND >= 1)
-    rc_hunks_pipelined<Fn, NS, ND, UNROLL, POLS>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
+    rc_hunks_pipelined<Fn, NS, ND, UNROLL, POLS>(fn, a, fullPacks, worker, nWorkers, tid, nthreads, hook);
   else
     rc_hunks<Fn, NS, ND, UNROLL, POLS, ORDER>(fn, a, fullPacks, worker, nWorkers, tid, nthreads);
   // Remaining packs (< one hunk): one pack per thread, grid-strided.
@@ -764,17 +772,17 @@ __device__ __forceinline__ void reduce_copy_aligned(const Fn& fn, const RCArgs& 
 // 4 measured slower, see above).
 constexpr int kShiftRows = VCCL_SHIFT_ROWS;
 template <class Fn, int NS, int ND, int UNROLL, int POLS, int ORDER = 0, bool PIPE = false,
-          bool DSTR = true>
+          bool DSTR = true, class Hook = NoHook>
 __device__ __forceinline__ void reduce_copy(const Fn& fn, const RCArgs& a, int64_t nElts,
                                             int64_t worker, int64_t nWorkers, int tid,
-                                            int nthreads) {
+                                            int nthreads, Hook&& hook = Hook{}) {
   using T = typename Fn::EltType;
   constexpr int esz = (int)sizeof(T);
   const int64_t gtid = worker * nthreads + tid, gthreads = nWorkers * nthreads;
   if (nElts <= 0) return;
   if (rc_all_aligned16(a)) {
     reduce_copy_aligned<Fn, NS, ND, UNROLL, POLS, ORDER, PIPE>(fn, a, nElts, worker, nWorkers, tid,
-                                                               nthreads);
+                                                               nthreads, hook);
     return;
   }
   // Misaligned (see above): the body is aligned on destination 0; sources

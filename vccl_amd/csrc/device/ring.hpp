@@ -31,15 +31,62 @@
 #define VCCL_RING_OUT2_POL kNT
 #endif
 
+#ifndef VCCL_RING_SPOLL
+// 1: prim_ws reads a missing credit once through the scalar unit before it
+// drains its stores and polls (see sread_u64); 0: drain first, always.
+#define VCCL_RING_SPOLL 1
+#endif
+#ifndef VCCL_RING_WAVE_SYNC
+// 1: per-wave slot hand-off (RingCtx::prim_ws); 0: the workgroup-barrier
+// hand-off of rounds 1-4 (RingCtx::prim_wg), kept for A/B.
+#define VCCL_RING_WAVE_SYNC 1
+#endif
+
+// LDS / global pointers are typed as such: through a generic pointer the
+// compiler emits flat_* accesses, which vmcnt counts out of order (a wait on
+// one drains every outstanding load and store, MI355X_MICROARCH.md) —
+// exactly what the partial vmcnt of the per-wave hand-off must avoid.
+#define VCCL_LDS __attribute__((address_space(3)))
+#define VCCL_GLOBAL __attribute__((address_space(1)))
+
 namespace vccl {
 
+// Per-wave slot hand-off state of one channel workgroup, in LDS (prim_ws).
+// done[i]: waves that completed prim p, cumulative over p = i, i + D, ...;
+// tail / head: the highest credit values any wave has seen; abort: a wave's
+// spin failed (abort word, peer error or timeout).
+constexpr int kSyncDepth = 4;  // prims a wave may run ahead of the slowest (<= kSteps / 2)
+struct WaveSync {
+  uint32_t done[kSyncDepth];
+  uint64_t tail, head;
+  int abort;
+};
+
+// Flags through global-typed pointers: a generic pointer would make these
+// flat_* accesses, which vmcnt retires out of order.
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load((const VCCL_GLOBAL uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void st_sys(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store((VCCL_GLOBAL uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// A flag read through the scalar unit, globally coherent (glc: a scalar-cache
+// miss, so the uncached flag is read from memory): it waits on lgkmcnt only,
+// never behind the wave's outstanding vector stores — the credit check of
+// the per-wave hand-off (prim_ws) reads a fresh flag without draining them.
+__device__ __forceinline__ uint64_t sread_u64(const uint64_t* p) {
+  uint64_t v;
+  asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
+template <class P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {  // in SGPRs (channel pointers are wave-uniform)
+  const uint64_t x = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return (P*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
 
 struct RingCtx {
   DevChannel* ch;
@@ -48,16 +95,45 @@ struct RingCtx {
   int tid, nthreads;
   int slotBytes;
   int64_t ll128Slot;  // bytes per LL128 FIFO slot (LL128 ring only)
-  int* shAbort;  // LDS
-  RingTraceRec* trace;  // this channel's timeline (DevComm::trace) or nullptr
+  VCCL_LDS int* shAbort;  // = &ws->abort
+  VCCL_GLOBAL RingTraceRec* trace;  // this channel's timeline (DevComm::trace) or nullptr
   int traceN;           // records written by this launch
+  // per-wave hand-off (prim_ws): this wave's position and its one pending
+  // prim — stores issued, not yet known complete, flags not yet posted
+  VCCL_LDS WaveSync* ws;
+  // The channel's and comm's fields, read once at kernel start (load()):
+  // read through their pointers later, each would be a memory load whose
+  // value waits for every older store of the wave (vmcnt retires in order)
+  // — the store drain the per-wave hand-off overlaps.  The ring order sits
+  // in LDS (ds_read: lgkmcnt only).
+  char* recvFifo;
+  char* sendFifo;
+  const uint64_t* recvTail;
+  const uint64_t* sendHead;
+  uint64_t* nextRecvTail;
+  uint64_t* prevSendHead;
+  uint32_t* sendSizes;
+  char* ll128Recv;
+  char* ll128Send;
+  int ringPos;
+  VCCL_LDS int* ringRanks;
+  volatile int* abortFlag;
+  int* errorFlag;
+  uint64_t spinTimeout;
+  int useFences, pollMode, traceCap;
+  int lane, nWaves;
+  uint32_t seq;  // prims this workgroup has started in this launch (same in every wave)
+  bool pend;
+  bool pSend, pRecv, pTrace;
+  uint32_t pSeq, pBytes, pTraceIx;
+  uint64_t pSendStep, pRecvStep;
 
   // Bounded spin on `flag` until pred(value); returns false on abort/timeout.
   // The timeout is per wait (no progress for spinTimeoutTicks), not per call.
   __device__ uint64_t poll(const uint64_t* flag) const {
     // pollMode 1: atomic RMW (resolved at the point of coherence, never a
     // cached copy); 0: relaxed system-scope load.
-    if (comm->pollMode == 1)
+    if (pollMode == 1)
       return __hip_atomic_fetch_add((uint64_t*)flag, (uint64_t)0, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_SYSTEM);
     return ld_sys(flag);
@@ -70,37 +146,240 @@ struct RingCtx {
       if ((++spins & 255) == 0) {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (start == 0) start = now;
-        if (*comm->abortFlag) return false;
-        if (now - start > comm->spinTimeoutTicks) {
-          __hip_atomic_store(comm->errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (*abortFlag) return false;
+        if (now - start > spinTimeout) {
+          __hip_atomic_store(errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           return false;
         }
-        if (__hip_atomic_load(comm->errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+        if (__hip_atomic_load(errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
           return false;
       }
     }
     return true;
   }
 
-  __device__ bool aborted() const { return *shAbort != 0; }
+  // Every thread: the fields above from `c` / `m`; ringRanks (nRanks
+  // entries) copied into `shRing` — the caller's barrier publishes them.
+  __device__ __forceinline__ void load(DevChannel* c, const DevComm* m, int nRanks, VCCL_LDS int* shRing) {
+    ch = c;
+    comm = m;
+    recvFifo = c->recvFifo;
+    sendFifo = c->sendFifo;
+    recvTail = uniform_ptr(c->recvTail);
+    sendHead = uniform_ptr(c->sendHead);
+    nextRecvTail = c->nextRecvTail;
+    prevSendHead = c->prevSendHead;
+    sendSizes = c->sendSizes;
+    ll128Recv = c->ll128Recv;
+    ll128Send = c->ll128Send;
+    ringPos = c->ringPos;
+    recvStep = c->recvStep;
+    sendStep = c->sendStep;
+    for (int k = tid; k < nRanks; k += nthreads) shRing[k] = c->ringRanks[k];
+    ringRanks = shRing;
+    abortFlag = m->abortFlag;
+    errorFlag = m->errorFlag;
+    spinTimeout = m->spinTimeoutTicks;
+    useFences = m->useFences;
+    pollMode = m->pollMode;
+    traceCap = m->traceCap;
+  }
+
+  __device__ bool aborted() const { return __hip_atomic_load(shAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; }
+  __device__ void set_aborted() { __hip_atomic_store(shAbort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+  // ---------------------------------------------------- per-wave hand-off
+  // VCCL hands a slot over after the whole workgroup's stores have drained
+  // (prims_simple.h:183-319: postPeer after the barrier).  Round 4's trace put
+  // that drain at 13.2 of 65.7 us per two-destination slot (profiles/r04ap):
+  // every wave idles until the slowest wave's stores are acknowledged.  Here
+  // each wave hands over on its own: a wave issues slot k, moves on to slot
+  // k + 1, issues k + 1's first loads, and only then waits for slot k's
+  // stores with a PARTIAL `s_waitcnt vmcnt(NS * UNROLL)` (vmcnt retires loads
+  // and stores in issue order, MI355X_MICROARCH.md: all but the N youngest
+  // — k + 1's loads — are done), so its drain overlaps its next loads.  It
+  // then counts itself done for slot k in LDS; the wave that completes the
+  // count posts slot k's flags (tail to next, head to prev).  No workgroup
+  // barrier per slot.  Posts stay in slot order: the poster of k + 1 counted
+  // after every wave completed k + 1, which each wave does only after its
+  // own earlier flag stores retired (same vmcnt, in order).  Credits: a wave
+  // checks the highest values any wave has seen (LDS) and polls the flag
+  // itself only when they are not enough, completing its pending slot first
+  // (so no post ever waits on a peer).  A wave runs at most kSyncDepth prims
+  // ahead of the slowest (the done[] ring).
+  __device__ __forceinline__ void post_pending() {
+    if (useFences) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system-scope release (L2 writeback)
+      drain_vmem();
+    }
+    if (pSend && sendSizes) {
+      // the net proxy reads the size once it sees the tail (proxy.cc
+      // send_loop): the size must be visible first — two relaxed stores to
+      // different words carry no order of their own (found when the per-wave
+      // hand-off let these stores overlap the poster's next loads: a stale
+      // size, hence a short slot, in test_multi_process_ranks[3-net])
+      __hip_atomic_store((VCCL_GLOBAL uint32_t*)(sendSizes + pSendStep % kSteps), pBytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      drain_vmem();
+    }
+    if (pSend) st_sys(nextRecvTail, pSendStep + 1);
+    if (pRecv) st_sys(prevSendHead, pRecvStep + 1);
+    if (pTrace) trace[pTraceIx].t4 = __builtin_amdgcn_s_memrealtime();
+  }
+  // Completes this wave's pending prim: its stores (all but the N youngest
+  // memory operations) are done; count it, post when this wave is the last.
+  template <int N>
+  __device__ __forceinline__ void complete_pending() {
+    if (!pend) return;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    if (lane == 0) {
+      if (pTrace && tid == 0) trace[pTraceIx].t3 = __builtin_amdgcn_s_memrealtime();
+      const uint32_t old = __hip_atomic_fetch_add(&ws->done[pSeq % kSyncDepth], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (old + 1 == (uint32_t)nWaves * (pSeq / kSyncDepth + 1) && !aborted()) post_pending();
+    }
+    pend = false;
+  }
+  // Every wave, before the workgroup's final barrier (k_ring).
+  __device__ __forceinline__ void finish() { complete_pending<0>(); }
+  // Wait (LDS) until every wave completed prim q; false on abort.
+  __device__ __forceinline__ bool wait_done(uint32_t q) {
+    const uint32_t want = (uint32_t)nWaves * (q / kSyncDepth + 1);
+    while (__hip_atomic_load(&ws->done[q % kSyncDepth], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+      if (aborted()) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+  }
+  // Bounded spin on a flag until it reaches `target`; the value seen goes to
+  // the LDS cache `*cache` (max).  Lane 0 only.
+  __device__ bool spin_cache(const uint64_t* flag, uint64_t target, VCCL_LDS uint64_t* cache) {
+    uint64_t v = poll(flag);
+    if (v < target) {
+      if (!spin_ge(flag, target)) return false;
+      v = poll(flag);
+    }
+    __hip_atomic_fetch_max(cache, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return true;
+  }
+
+  template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
+  __device__ __forceinline__ void prim_ws(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp, int recvOff,
+                          int sendOff) {
+    using T = typename Fn::EltType;
+    if (aborted()) return;
+    const bool tr = trace != nullptr && traceN < traceCap && tid == 0;
+    uint64_t t0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (seq >= (uint32_t)kSyncDepth && !wait_done(seq - kSyncDepth)) return;
+    const uint64_t needTail = RECV ? recvStep + 1 : 0;
+    const uint64_t needHead = SEND && sendStep + 1 > (uint64_t)kSteps ? sendStep + 1 - kSteps : 0;
+    bool have = __hip_atomic_load(&ws->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needTail &&
+                __hip_atomic_load(&ws->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needHead;
+#if VCCL_RING_SPOLL
+    if (!have && !useFences) {  // one fresh scalar read of each flag, stores still in flight
+      const uint64_t t = RECV ? sread_u64(recvTail) : 0, h = needHead ? sread_u64(sendHead) : 0;
+      if (lane == 0) {
+        if (RECV) __hip_atomic_fetch_max(&ws->tail, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (needHead) __hip_atomic_fetch_max(&ws->head, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      have = t >= needTail && h >= needHead;
+    }
+#endif
+    if (!have || useFences) {
+      complete_pending<0>();  // never hold a post while waiting on a peer
+      int ok = 1;
+      if (lane == 0) {
+        if (RECV && !spin_cache(recvTail, needTail, &ws->tail)) ok = 0;
+        if (ok && needHead && !spin_cache(sendHead, needHead, &ws->head)) ok = 0;
+        if (!ok) set_aborted();
+        if (ok && useFences) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
+          drain_vmem();
+        }
+      }
+      if (!__builtin_amdgcn_readfirstlane(ok)) return;
+    }
+    const uint64_t t1 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
+    constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
+    constexpr int ND = (SEND ? 1 : 0) + (DST ? 1 : 0);
+    constexpr int S0 = SRC ? VCCL_RING_SRC_POL : kSys, S1 = kSys;
+    constexpr int D0 = SEND ? kSys : VCCL_RING_OUT_POL, D1 = VCCL_RING_OUT2_POL;
+    constexpr int POLS = mkpol(S0, S1, S1, S1, D0, D1, D1, D1);
+    if (nelem > 0) {
+      RCArgs a;
+      int s = 0, d = 0;
+      if (SRC) a.srcs[s++] = (const char*)src;
+      if (RECV) a.srcs[s++] = recvFifo + (int64_t)(recvStep % kSteps) * slot_stride(slotBytes) + recvOff;
+      if (SEND) a.dsts[d++] = sendFifo + (int64_t)(sendStep % kSteps) * slot_stride(slotBytes) + sendOff;
+      if (DST) a.dsts[d++] = (char*)dst;
+      a.nSrcs = NS;
+      a.nDsts = ND;
+      a.preOpSrcs = SRC ? 1 : 0;
+      a.postOp = postOp ? 1 : 0;
+      // the hook fires only on the aligned engine's first full hunk; every
+      // other shape completes the pending prim before issuing anything
+      const bool hooked = rc_all_aligned16(a) && nelem * (int64_t)sizeof(T) >= (int64_t)nthreads * UNROLL * 16;
+      if (!hooked) complete_pending<0>();
+      reduce_copy<Fn, NS, ND, UNROLL, POLS, 0, true>(fn, a, nelem, 0, 1, tid, nthreads,
+                                                     [&]() __attribute__((always_inline)) {
+                                                       complete_pending<NS * UNROLL>();
+                                                     });
+    } else {
+      complete_pending<0>();
+    }
+    if (tr) {
+      VCCL_GLOBAL RingTraceRec& rec = trace[traceN];
+      rec.t0 = t0;
+      rec.t1 = t1;
+      rec.t2 = t1;
+      rec.tc = __builtin_amdgcn_s_memrealtime();
+      rec.shape = (RECV ? 1u : 0u) | (SEND ? 2u : 0u) | (SRC ? 4u : 0u) | (DST ? 8u : 0u);
+      rec.bytes = (uint32_t)(nelem > 0 ? nelem * (int64_t)sizeof(T) : 0);
+      rec.step = SEND ? sendStep : recvStep;
+    }
+    pend = true;
+    pSend = SEND;
+    pRecv = RECV;
+    pSeq = seq;
+    pSendStep = sendStep;
+    pRecvStep = recvStep;
+    pBytes = (uint32_t)(nelem > 0 ? sendOff + nelem * (int64_t)sizeof(T) : 0);
+    pTrace = trace != nullptr && traceN < traceCap;
+    pTraceIx = (uint32_t)traceN;
+    if (trace != nullptr && traceN < traceCap) traceN++;
+    seq++;
+    if (SEND) sendStep++;
+    if (RECV) recvStep++;
+  }
+
+  template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
+  __device__ __forceinline__ void prim(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
+                                       int recvOff = 0, int sendOff = 0) {
+#if VCCL_RING_WAVE_SYNC
+    prim_ws<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, src, dst, nelem, postOp, recvOff, sendOff);
+#else
+    prim_wg<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, src, dst, nelem, postOp, recvOff, sendOff);
+#endif
+  }
 
   // One primitive call: at most one slot of payload.
   //   srcs = [SRC ? own input] ++ [RECV ? recv slot]
   //   dsts = [SEND ? peer slot] ++ [DST ? own output]
   //   recvOff / sendOff: byte offset of the chunk inside its slot (< 16)
+  // (Rounds 1-4: the workgroup hand-off — VCCL_RING_WAVE_SYNC=0.)
   template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
-  __device__ void prim(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
-                       int recvOff = 0, int sendOff = 0) {
+  __device__ void prim_wg(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
+                          int recvOff = 0, int sendOff = 0) {
     if (aborted()) return;
-    const bool tr = trace != nullptr && traceN < comm->traceCap;
+    const bool tr = trace != nullptr && traceN < traceCap;
     uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, tc = 0;
     if (tid == 0) {
       if (tr) t0 = __builtin_amdgcn_s_memrealtime();
       bool ok = true;
-      if (RECV) ok = spin_ge(ch->recvTail, recvStep + 1);
-      if (SEND && ok && sendStep + 1 > (uint64_t)kSteps) ok = spin_ge(ch->sendHead, sendStep + 1 - kSteps);
-      if (!ok) *shAbort = 1;
-      if (comm->useFences) {
+      if (RECV) ok = spin_ge(recvTail, recvStep + 1);
+      if (SEND && ok && sendStep + 1 > (uint64_t)kSteps) ok = spin_ge(sendHead, sendStep + 1 - kSteps);
+      if (!ok) set_aborted();
+      if (useFences) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
         drain_vmem();
       }
@@ -125,8 +404,8 @@ struct RingCtx {
       RCArgs a;
       int s = 0, d = 0;
       if (SRC) a.srcs[s++] = (const char*)src;
-      if (RECV) a.srcs[s++] = ch->recvFifo + (int64_t)(recvStep % kSteps) * slot_stride(slotBytes) + recvOff;
-      if (SEND) a.dsts[d++] = ch->sendFifo + (int64_t)(sendStep % kSteps) * slot_stride(slotBytes) + sendOff;
+      if (RECV) a.srcs[s++] = recvFifo + (int64_t)(recvStep % kSteps) * slot_stride(slotBytes) + recvOff;
+      if (SEND) a.dsts[d++] = sendFifo + (int64_t)(sendStep % kSteps) * slot_stride(slotBytes) + sendOff;
       if (DST) a.dsts[d++] = (char*)dst;
       a.nSrcs = NS;
       a.nDsts = ND;
@@ -139,18 +418,21 @@ struct RingCtx {
     __syncthreads();
     if (tid == 0) {
       if (tr) t3 = __builtin_amdgcn_s_memrealtime();
-      if (comm->useFences) {
+      if (useFences) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system-scope release (L2 writeback)
         drain_vmem();
       }
-      if (SEND && ch->sendSizes)
-        __hip_atomic_store(ch->sendSizes + sendStep % kSteps,
+      if (SEND && sendSizes) {  // visible before the tail (post_pending)
+        __hip_atomic_store((VCCL_GLOBAL uint32_t*)(sendSizes + sendStep % kSteps),
                            (uint32_t)(nelem > 0 ? sendOff + nelem * (int64_t)sizeof(typename Fn::EltType) : 0),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (SEND) st_sys(ch->nextRecvTail, sendStep + 1);
-      if (RECV) st_sys(ch->prevSendHead, recvStep + 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        drain_vmem();
+      }
+      if (SEND) st_sys(nextRecvTail, sendStep + 1);
+      if (RECV) st_sys(prevSendHead, recvStep + 1);
       if (tr) {
-        RingTraceRec& rec = trace[traceN];
+        VCCL_GLOBAL RingTraceRec& rec = trace[traceN];
         rec.t0 = t0;
         rec.t1 = t1;
         rec.t2 = t2;
@@ -260,8 +542,8 @@ __device__ void ll128_prim(RingCtx& R, const Fn& fn, const void* srcv, void* dst
   if (R.aborted()) return;
   if (R.tid == 0) {
     bool ok = true;
-    if (SEND && R.sendStep + 1 > (uint64_t)kSteps) ok = R.spin_ge(R.ch->sendHead, R.sendStep + 1 - kSteps);
-    if (!ok) *R.shAbort = 1;
+    if (SEND && R.sendStep + 1 > (uint64_t)kSteps) ok = R.spin_ge(R.sendHead, R.sendStep + 1 - kSteps);
+    if (!ok) R.set_aborted();
   }
   __syncthreads();
   if (R.aborted()) return;
@@ -270,8 +552,8 @@ __device__ void ll128_prim(RingCtx& R, const Fn& fn, const void* srcv, void* dst
   const int64_t nbytes = nelem > 0 ? nelem * (int64_t)sizeof(T) : 0;
   const int64_t nRounds = (nbytes + kLL128RoundData - 1) / kLL128RoundData;
   const uint64_t rflag = R.recvStep + 1, sflag = R.sendStep + 1;
-  const char* rslot = RECV ? R.ch->ll128Recv + (int64_t)(R.recvStep % kSteps) * R.ll128Slot : nullptr;
-  char* sslot = SEND ? R.ch->ll128Send + (int64_t)(R.sendStep % kSteps) * R.ll128Slot : nullptr;
+  const char* rslot = RECV ? R.ll128Recv + (int64_t)(R.recvStep % kSteps) * R.ll128Slot : nullptr;
+  char* sslot = SEND ? R.ll128Send + (int64_t)(R.sendStep % kSteps) * R.ll128Slot : nullptr;
   const int lane = R.tid & 63, wave = R.tid >> 6, nw = R.nthreads >> 6;
   constexpr int S = kLL128LaneSpan;
   const int line = lane / S, sub = lane % S;
@@ -301,10 +583,10 @@ __device__ void ll128_prim(RingCtx& R, const Fn& fn, const void* srcv, void* dst
           if ((++spins & 255) == 0) {
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
             if (start == 0) start = now;
-            if (*R.comm->abortFlag ||
-                __hip_atomic_load(R.comm->errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                now - start > R.comm->spinTimeoutTicks) {
-              __hip_atomic_store(R.comm->errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (*R.abortFlag ||
+                __hip_atomic_load(R.errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                now - start > R.spinTimeout) {
+              __hip_atomic_store(R.errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               fail = true;
               break;
             }
@@ -340,9 +622,9 @@ __device__ void ll128_prim(RingCtx& R, const Fn& fn, const void* srcv, void* dst
       if constexpr (DST) ll128_st_piece<T, kNT>(dst, r * kLL128RoundData + dOff, dLen, nbytes, dstAl, acc);
     }
   }
-  if (fail) *R.shAbort = 1;
+  if (fail) R.set_aborted();
   __syncthreads();  // every lane's reads of the receive slot are done
-  if (R.tid == 0 && RECV && !R.aborted()) st_sys(R.ch->prevSendHead, R.recvStep + 1);
+  if (R.tid == 0 && RECV && !R.aborted()) st_sys(R.prevSendHead, R.recvStep + 1);
   if (SEND) R.sendStep++;
   if (RECV) R.recvStep++;
 }
@@ -403,7 +685,7 @@ __device__ __forceinline__ void ring_step(RingCtx& r, const Fn& fn, const void* 
 // all_reduce.h:12-83 (runRing): RS then AG within one kernel, chunk c of each
 // round finishing at ring position c.
 template <class Fn, int UNROLL, int PROTO = kProtoSimple>
-__device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
+__device__ __forceinline__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
   using T = typename Fn::EltType;
   const int n = w.nRanks;
   const int64_t eltAlign = 16 / sizeof(T) ? 16 / sizeof(T) : 1;
@@ -411,7 +693,7 @@ __device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int 
   if (!cbd_part(w, c, &gridOff, &chCount, &chunkCount)) return;
   const T* in = (const T*)w.sendbuff;
   T* out = (T*)w.recvbuff;
-  const int ringIx = r.ch->ringPos;
+  const int ringIx = r.ringPos;
   const int64_t loopCount = (int64_t)n * chunkCount;
   auto modRanks = [n](int x) { return x >= n ? x - n : x; };
   for (int64_t eo = 0; eo < chCount; eo += loopCount) {
@@ -447,7 +729,7 @@ __device__ void ring_allreduce(RingCtx& r, const Fn& fn, const RingWork& w, int 
 // reduce_scatter.h:12-55: the chunk owned by rank ringRanks[k] starts at its
 // ring successor; the owner writes output[off] with postOp.
 template <class Fn, int UNROLL, int PROTO = kProtoSimple>
-__device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
+__device__ __forceinline__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
   using T = typename Fn::EltType;
   const int n = w.nRanks;
   const int64_t count = (int64_t)w.count;
@@ -455,7 +737,7 @@ __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, 
   if (!cbd_part(w, c, &gridOff, &chCount, &chunkCount)) return;
   const T* in = (const T*)w.sendbuff;
   T* out = (T*)w.recvbuff;
-  const int* ringRanks = r.ch->ringRanks;
+  const VCCL_LDS int* ringRanks = r.ringRanks;
   // A chunk for rank k sits in its slots at k's block misalignment (the same
   // on every rank: dataOff is a 16-byte multiple), so the FIFO operand shares
   // the input block's alignment (reduce_copy_misaligned).
@@ -485,14 +767,14 @@ __device__ void ring_reducescatter(RingCtx& r, const Fn& fn, const RingWork& w, 
 // the reduce-scatter chunk the root owns.  One FIFO step per chunk
 // (REDUCE_CHUNKSTEPS 1).
 template <class Fn, int UNROLL, int PROTO = kProtoSimple>
-__device__ void ring_reduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
+__device__ __forceinline__ void ring_reduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) {
   using T = typename Fn::EltType;
   const int n = w.nRanks;
   int64_t partOff, partCount, chunkCount;
   if (!cbd_part(w, c, &partOff, &partCount, &chunkCount)) return;
   const T* in = (const T*)w.sendbuff;
   T* out = (T*)w.recvbuff;
-  const int me = r.ch->ringRanks[0], prev = r.ch->ringRanks[n - 1];
+  const int me = r.ringRanks[0], prev = r.ringRanks[n - 1];
   for (int64_t eo = 0; eo < partCount; eo += chunkCount) {
     const int64_t nelem = partCount - eo < chunkCount ? partCount - eo : chunkCount;
     const int64_t off = partOff + eo;
@@ -510,7 +792,7 @@ __device__ void ring_reduce(RingCtx& r, const Fn& fn, const RingWork& w, int c) 
 // ----------------------------------------------------------------- AllGather
 // all_gather.h:12-83: byte copies (enqueue.cc:2400-2404 rewrites AG as int8).
 template <int UNROLL, int PROTO = kProtoSimple>
-__device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
+__device__ __forceinline__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
   using Fn = FnCopy<uint8_t>;
   const Fn fn(0);
   const int n = w.nRanks;
@@ -519,7 +801,7 @@ __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
   if (!cbd_part(w, c, &partOff, &partCount, &chunkCount)) return;
   const uint8_t* in = (const uint8_t*)w.sendbuff;
   uint8_t* out = (uint8_t*)w.recvbuff;
-  const int* ringRanks = r.ch->ringRanks;
+  const VCCL_LDS int* ringRanks = r.ringRanks;
   // A block for rank k travels at k's output misalignment inside the slots
   // (same on every rank), so the slot and the output block share alignment.
   auto mis = [&](int k) { return (int)(((int64_t)k * count) & 15); };
@@ -553,14 +835,14 @@ __device__ void ring_allgather(RingCtx& r, const RingWork& w, int c) {
 // rank receives into its output and forwards, the root's predecessor only
 // receives.  One FIFO step per chunk (BROADCAST_CHUNKSTEPS 1).
 template <int UNROLL, int PROTO = kProtoSimple>
-__device__ void ring_broadcast(RingCtx& r, const RingWork& w, int c) {
+__device__ __forceinline__ void ring_broadcast(RingCtx& r, const RingWork& w, int c) {
   using Fn = FnCopy<uint8_t>;
   const Fn fn(0);
   int64_t partOff, partCount, chunkCount;
   if (!cbd_part(w, c, &partOff, &partCount, &chunkCount)) return;
   const uint8_t* in = (const uint8_t*)w.sendbuff;
   uint8_t* out = (uint8_t*)w.recvbuff;
-  const int me = r.ch->ringRanks[0], next = r.ch->ringRanks[1];
+  const int me = r.ringRanks[0], next = r.ringRanks[1];
   for (int64_t eo = 0; eo < partCount; eo += chunkCount) {
     const int64_t nelem = partCount - eo < chunkCount ? partCount - eo : chunkCount;
     const int64_t off = partOff + eo;

@@ -63,27 +63,36 @@ __device__ __forceinline__ void ring_run(RingCtx& r, const Fn& fn, const RingWor
 template <int COLL, class Fn, int UNROLL, int PROTO>
 __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
   const RingWork& w = b.w;
-  __shared__ int shAbort;
-  if (threadIdx.x == 0) shAbort = 0;
-  __syncthreads();
+  __shared__ WaveSync ws;
+  __shared__ int shRing[kMaxRanks];
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < kSyncDepth; i++) ws.done[i] = 0;
+    ws.tail = ws.head = 0;
+    ws.abort = 0;
+  }
   DevChannel* ch = &w.channels[blockIdx.x];
   RingCtx r;
-  r.ch = ch;
-  r.comm = w.comm;
-  r.recvStep = ch->recvStep;
-  r.sendStep = ch->sendStep;
   r.tid = threadIdx.x;
   r.nthreads = blockDim.x;
+  r.load(ch, w.comm, w.nRanks, (VCCL_LDS int*)shRing);
+  __syncthreads();
   r.slotBytes = w.slotBytes;
   r.ll128Slot = w.ll128SlotBytes;
-  r.shAbort = &shAbort;
-  r.trace = w.comm->trace ? (RingTraceRec*)w.comm->trace + (int64_t)blockIdx.x * w.comm->traceCap : nullptr;
+  r.ws = (VCCL_LDS WaveSync*)&ws;
+  r.shAbort = &r.ws->abort;
+  r.lane = threadIdx.x & 63;
+  r.nWaves = (int)(blockDim.x >> 6);
+  r.seq = 0;
+  r.pend = false;
+  r.trace = w.comm->trace ? (VCCL_GLOBAL RingTraceRec*)((RingTraceRec*)w.comm->trace + (int64_t)blockIdx.x * w.comm->traceCap)
+                          : nullptr;
   r.traceN = 0;
   const Fn fn(load_op_arg(w.redArgPtr, w.redArgBytes, w.redArg));
   const uint64_t recv0 = r.recvStep, send0 = r.sendStep;
   ring_run<COLL, Fn, UNROLL, PROTO>(r, fn, w);
   for (int i = 1; i < b.nParts; i++)
     ring_run<COLL, Fn, UNROLL, PROTO>(r, fn, ring_work_with(w, b.more[i - 1]));
+  r.finish();  // this wave's last prim: drained, counted, posted by the last wave
   __syncthreads();
   // a channel none of the parts touched (below every part's channelLo) keeps
   // its counters untouched
