@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One rank of the ncclCommSplit test (tests/test_gpu_collectives.py).
 
-argv: rank nranks uid_hex
+argv: rank nranks uid_hex [uid_hex of the CTA-bounded parent]
 Splits the n-rank comm by color = rank % 2 with key = -rank (each half in
 reversed parent order), and a second split where rank 0 passes
 NCCL_SPLIT_NOCOLOR; checks the sub-comms' sizes and ranks and an exact
@@ -52,6 +52,20 @@ def main():
     for c in (sub, sub2):
         if c is not None:
             c.destroy()
+    # a split with config NULL takes the parent's config
+    # (copyCommConfig, src/init.cc:2160-2161) — a parent bounded to 3 CTAs
+    # gives a child of 3 channels, not the default count
+    uid2 = nccl.unique_id_from_bytes(bytes.fromhex(sys.argv[4])) if len(sys.argv) > 4 else None
+    if uid2 is not None:
+        bounded = nccl.Comm.init_rank(n, uid2, rank, config=nccl.ncclConfig_t.initializer(maxCTAs=3))
+        child = bounded.split(0, rank)
+        if bounded.n_channels() != 3 or child is None or child.n_channels() != 3:
+            bad.append(("split of a bounded parent", bounded.n_channels(), child and child.n_channels()))
+        elif not allreduce_ok(child, n, base=4 << 20):
+            bad.append(("bounded child all-reduce", n))
+        if child is not None:
+            child.destroy()
+        bounded.destroy()
     err = comm.async_error()
     comm.destroy()
     if bad or err:

@@ -561,8 +561,9 @@ def test_comm_split(n):
     env = dict(os.environ)
     env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
     env.update(TEST_GEOM)
+    hexid2 = nccl.unique_id_to_bytes(nccl.get_unique_id()).hex()  # the CTA-bounded parent
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_split_worker.py"),
-                               str(r), str(n), hexid], env=env,
+                               str(r), str(n), hexid, hexid2], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
     outs = [p.communicate(timeout=240)[0].decode(errors="replace")[-2000:] for p in procs]
     assert [p.returncode for p in procs] == [0] * n, "\n".join(outs)

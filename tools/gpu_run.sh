@@ -7,6 +7,8 @@
 #        prof      rocprofv3 --kernel-trace --stats of bench.py (no CPU leg)
 #        n2        bench.py N>1 rehearsal: 2 ranks sharing the one GPU
 #        nr:<n>    the same with n ranks
+#        spawn:<n> bench.py --gpus <n> without torch.distributed.run (the
+#                  script starts its own rank processes)
 #        smoke     __graft_entry__.smoke()
 #        py:<file> python <file> (a tool script)
 #        sweep:<mode>  tools/sweep_rc.py with SWEEP_MODE=<mode> (6 rounds)
@@ -32,6 +34,7 @@ for s in "$@"; do
     prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --no-extras > $O/bench_prof.json 2> $O/bench_prof.err) ;;
     n2) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 > $O/bench_n2.json 2> $O/bench_n2.err ;;
     nr:*) timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#nr:} --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus ${s#nr:} --steps 5 --warmup 2 > $O/bench_n${s#nr:}.json 2> $O/bench_n${s#nr:}.err ;;
+    spawn:*) timeout -k 10 900 python bench.py --gpus ${s#spawn:} --steps 5 --warmup 2 > $O/bench_spawn_n${s#spawn:}.json 2> $O/bench_spawn_n${s#spawn:}.err ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
     py:*) timeout -k 10 600 python -u ${s#py:} > $O/$(basename ${s#py:} .py).log 2>&1 ;;
     sweep:*) SWEEP_MODE=${s#sweep:} SWEEP_ROUNDS=${SWEEP_ROUNDS:-6} timeout -k 10 300 python -u tools/sweep_rc.py > $O/sweep_${s#sweep:}.log 2>&1 ;;

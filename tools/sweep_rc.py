@@ -35,6 +35,8 @@ def main():
         return dtype_geometry(int(mode[5:]), n * 4, rounds, reps)
     if mode == "twodst":
         return two_dst(n, rounds, reps)
+    if mode == "twodst_geom":
+        return two_dst(n, rounds, reps, geom=True)
     if mode == "policies":
         # load/store policy: 0 plain, 1 nt, 2 sc0 sc1, 3 sc1 nt; order 1 = XCD-contiguous hunks
         for block, unroll, ld, st, order in itertools.product(
@@ -130,7 +132,7 @@ def misaligned(n, rounds, reps):
 POL = {"plain": 0, "nt": 1, "sys": 2, "sc1nt": 3}
 
 
-def two_dst(n, rounds, reps):
+def two_dst(n, rounds, reps, geom=False):
     """The two-destination shape (2 x n f32 -> 2 x n: the ring's final reduce
     step and every recv-copy-send step) against its read/write-mix reference,
     the 1 -> 1 copy (ours and torch's), interleaved in one process.  2 -> 2
@@ -144,9 +146,20 @@ def two_dst(n, rounds, reps):
     s = torch.cuda.current_stream()
     hunk = lambda u: 256 * u * 16  # noqa: E731
     variants = []  # (name, nsrc, ndst, cfg)
+    if geom:
+        # round 5: workgroup size x hunks per workgroup (grid-stride) x
+        # unroll x order for the two policy mixes that lead the round-3 sweep
+        for blk, per, u, (p0, p1), order in itertools.product(
+                (256, 512, 1024), (1, 2, 4), (2, 4), (("sys", "nt"), ("nt", "sys")), (0, 1, 4)):
+            hk = blk * u * 16
+            cfg = {"blockSize": blk, "unroll": u, "gridBlocks": max(1, (n * 4 + hk - 1) // hk // per),
+                   "ntLoads": 1, "ntStores": 16 | POL[p0] | POL[p1] << 2, "order": order}
+            variants.append((f"2to2_b{blk}_p{per}_u{u}_{p0}_{p1}_o{order}", 2, 2, cfg))
     for u, (p0, p1), order in itertools.product(
             (2, 4), (("sys", "sys"), ("nt", "nt"), ("plain", "plain"), ("sys", "nt"), ("nt", "sys"),
                      ("sys", "plain"), ("plain", "sys"), ("sc1nt", "sc1nt")), (0, 3, 4)):
+        if geom:
+            break
         cfg = {"blockSize": 256, "unroll": u, "gridBlocks": (n * 4 + hunk(u) - 1) // hunk(u),
                "ntLoads": 1, "ntStores": 16 | POL[p0] | POL[p1] << 2, "order": order}
         variants.append((f"2to2_u{u}_{p0}_{p1}_o{order}", 2, 2, cfg))

@@ -94,8 +94,8 @@ static hipError_t launch_one(const RCArgs& a, int64_t nElts, uint64_t redArg, co
 // Two-destination sweep (the ring's final-reduce / recv-copy-send shape,
 // 2 sources -> 2 destinations, measurement only): nt loads, unroll {2, 4},
 // a store policy PER destination (ntStores = 16 | d0 | d1 << 2; below 16 the
-// uniform encoding), store order {0 destination-major, 3 interleaved,
-// 4 pipelined}.
+// uniform encoding), store order {0 destination-major, 1 XCD-contiguous
+// hunks, 3 interleaved, 4 pipelined}.
 template <class Fn, int U, int D0, int D1>
 static hipError_t launch_2dst_pol(const RCArgs& a, int64_t n, uint64_t r, const LaunchGeom& lg,
                                   hipStream_t s) {
@@ -105,6 +105,7 @@ static hipError_t launch_2dst_pol(const RCArgs& a, int64_t n, uint64_t r, const 
                        n, r);
     return hipGetLastError();
   };
+  if (lg.order == 1) return go.template operator()<1>();
   if (lg.order == 3) return go.template operator()<3>();
   if (lg.order == 4) return go.template operator()<4>();
   return go.template operator()<0>();

@@ -36,6 +36,11 @@
 // drains its stores and polls (see sread_u64); 0: drain first, always.
 #define VCCL_RING_SPOLL 1
 #endif
+#ifndef VCCL_RING_LAST_DRAINS
+// 1: the wave that finishes issuing a slot last drains and posts at once
+// (prim_ws); 0: every wave defers its drain past its next slot's first loads.
+#define VCCL_RING_LAST_DRAINS 1
+#endif
 #ifndef VCCL_RING_WAVE_SYNC
 // 1: per-wave slot hand-off (RingCtx::prim_ws); 0: the workgroup-barrier
 // hand-off of rounds 1-4 (RingCtx::prim_wg), kept for A/B.
@@ -346,6 +351,16 @@ struct RingCtx {
     pBytes = (uint32_t)(nelem > 0 ? sendOff + nelem * (int64_t)sizeof(T) : 0);
     pTrace = trace != nullptr && traceN < traceCap;
     pTraceIx = (uint32_t)traceN;
+    // The last wave to finish issuing this slot is the one whose drain gates
+    // the post (every other wave has moved on and counted itself): it drains
+    // now instead of after its next credit check and loads, so the post comes
+    // as early as the workgroup hand-off's (the others still overlap).
+#if VCCL_RING_LAST_DRAINS
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ws->done[seq % kSyncDepth], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) + 1 ==
+        (uint32_t)nWaves * (seq / kSyncDepth + 1))
+      complete_pending<0>();
+#endif
     if (trace != nullptr && traceN < traceCap) traceN++;
     seq++;
     if (SEND) sendStep++;

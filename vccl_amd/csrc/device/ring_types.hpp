@@ -216,7 +216,7 @@ enum : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2 };
 //       64-byte write request — the unit a wave store reaches memory in
 //       (every TCC_EA0 write request is 64 B, profiles/r04f), so a line lands
 //       whole;
-//   L = 128 (-DVCCL_LL128_LINE=128, VCCL's 15/16 NVLink line, device.h:
+//   L = 128 (-DVCCL_LL128_LINE=128 -DVCCL_LL128_PROBE_BUILD, VCCL's 15/16 NVLink line, device.h:
 //       82-83): 8 lines, 960 data bytes per round, 2-4 % faster at 1-8 MiB
 //       (profiles/r04e) — but a line is TWO write requests with no order
 //       between them, and r04l caught the tear: 16 fp32 (the first 64 bytes
@@ -226,6 +226,11 @@ enum : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2 };
 #define VCCL_LL128_LINE 64
 #endif
 static_assert(VCCL_LL128_LINE == 64 || VCCL_LL128_LINE == 128, "LL128 line: 64 or 128 bytes");
+// the 128-byte line tears (above), so a build with it is for the
+// tearing probe only and must say so
+#if VCCL_LL128_LINE == 128 && !defined(VCCL_LL128_PROBE_BUILD)
+#error "VCCL_LL128_LINE=128 tears (profiles/r04l): probe builds only, add -DVCCL_LL128_PROBE_BUILD"
+#endif
 constexpr int kLL128LineBytes = VCCL_LL128_LINE;
 constexpr int kLL128LaneSpan = kLL128LineBytes / 16;    // lanes per line
 constexpr int kLL128LinesPerRound = 64 / kLL128LaneSpan;

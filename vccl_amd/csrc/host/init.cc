@@ -964,7 +964,7 @@ VCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void*) {
 // parent: its bootstrap carries every rank's (color, key), then the new
 // roots' ids — the first member of each color hosts its group's root — and
 // the members initialise as with ncclCommInitRankConfig on the parent's
-// device (config NULL: the defaults).
+// device (config NULL: the parent's CTA bounds).
 VCCL_EXPORT ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm,
                                        ncclConfig_t* config) {
   if (newcomm) *newcomm = nullptr;
@@ -998,8 +998,13 @@ VCCL_EXPORT ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, nccl
   int old = -1;
   HIPCHECK(hipGetDevice(&old));
   if (old != comm->device) HIPCHECK(hipSetDevice(comm->device));
-  const ncclResult_t r =
-      comm_init_rank(newcomm, (int)members.size(), &ids[members[0]], newRank, comm->device, config);
+  // config NULL: the parent's (copyCommConfig, src/init.cc:2160-2161) — its
+  // CTA bounds, so the child gets the parent's channel count
+  ncclConfig_t inherit = NCCL_CONFIG_INITIALIZER;
+  inherit.minCTAs = comm->minCTAs;
+  inherit.maxCTAs = comm->maxCTAs;
+  const ncclResult_t r = comm_init_rank(newcomm, (int)members.size(), &ids[members[0]], newRank, comm->device,
+                                        config ? config : &inherit);
   if (old != comm->device) (void)hipSetDevice(old);
   return r;
 }

@@ -70,6 +70,22 @@ class vcclLaunchConfig(ctypes.Structure):
                 ("ntStores", ctypes.c_int), ("order", ctypes.c_int)]
 
 
+class ncclConfig_t(ctypes.Structure):
+    """nccl.h.in:57-85 (include/nccl.h), filled as NCCL_CONFIG_INITIALIZER."""
+    _fields_ = [("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
+                ("blocking", ctypes.c_int), ("cgaClusterSize", ctypes.c_int), ("minCTAs", ctypes.c_int),
+                ("maxCTAs", ctypes.c_int), ("netName", ctypes.c_void_p), ("splitShare", ctypes.c_int),
+                ("trafficClass", ctypes.c_int)]
+
+    @classmethod
+    def initializer(cls, **kw) -> "ncclConfig_t":
+        undef = -2147483648  # NCCL_CONFIG_UNDEF_INT
+        c = cls(ctypes.sizeof(cls), 0xcafebeef, get_version(), undef, undef, undef, undef, None, undef, undef)
+        for k, v in kw.items():
+            setattr(c, k, v)
+        return c
+
+
 _lib = None
 
 
@@ -93,6 +109,7 @@ def lib() -> ctypes.CDLL:
         "ncclGetUniqueId": [ctypes.POINTER(ncclUniqueId)],
         "ncclCommInitRank": [pcomm, c_int, ncclUniqueId, c_int],
         "ncclCommInitAll": [pcomm, c_int, ctypes.POINTER(c_int)],
+        "ncclCommInitRankConfig": [pcomm, c_int, ncclUniqueId, c_int, ctypes.POINTER(ncclConfig_t)],
         "ncclCommFinalize": [vp],
         "ncclCommDestroy": [vp],
         "ncclCommAbort": [vp],
@@ -304,9 +321,13 @@ class Comm:
         self.handle = ctypes.c_void_p(handle)
 
     @classmethod
-    def init_rank(cls, nranks: int, uid: ncclUniqueId, rank: int) -> "Comm":
+    def init_rank(cls, nranks: int, uid: ncclUniqueId, rank: int, config: "ncclConfig_t | None" = None) -> "Comm":
         h = ctypes.c_void_p()
-        check(lib().ncclCommInitRank(ctypes.byref(h), nranks, uid, rank), "ncclCommInitRank")
+        if config is None:
+            check(lib().ncclCommInitRank(ctypes.byref(h), nranks, uid, rank), "ncclCommInitRank")
+        else:
+            check(lib().ncclCommInitRankConfig(ctypes.byref(h), nranks, uid, rank, ctypes.byref(config)),
+                  "ncclCommInitRankConfig")
         return cls(h.value)
 
     @classmethod
