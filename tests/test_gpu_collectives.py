@@ -121,29 +121,44 @@ def test_algorithm_choice(monkeypatch):
 # co-resident if their streams land on distinct hardware queues (HIP: 4 per
 # process, assigned round-robin over every stream the process has created),
 # so the single-process case is kept at n = 2; n >= 3 run as processes below.
-@pytest.mark.parametrize("n", [2])
-def test_single_process_ranks(n, monkeypatch):
+# "all": ncclCommInitAll over every GPU of a multi-GPU box (the reference's
+# single-process harness shape, peers mapped by peer access instead of IPC),
+# bit-exact against the oracle like the shared-GPU case.
+@pytest.mark.parametrize("n,placement", [(2, "shared"), (0, "all")])
+def test_single_process_ranks(n, placement, monkeypatch):
+    ndev = torch.cuda.device_count()
+    if placement == "all":
+        if ndev < 2:
+            pytest.skip(f"ncclCommInitAll over every GPU needs >= 2 GPUs; this box has {ndev}")
+        n = min(ndev, 8)
+    devs = [0] * n if placement == "shared" else list(range(n))
     for k, v in TEST_GEOM.items():
         monkeypatch.setenv(k, v)
+    if placement == "all":
+        monkeypatch.delenv("VCCL_ALLOW_SHARED_DEVICE", raising=False)
     nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
-    comms = nccl.Comm.init_all([0] * n)
+    comms = nccl.Comm.init_all(devs)
+
+    def on(r):  # tensors of rank r live on its device
+        return torch.device("cuda", devs[r])
     try:
         assert [c.rank for c in comms] == list(range(n)) and comms[0].count == n
-        streams = [torch.cuda.Stream() for _ in range(n)]
+        streams = [torch.cuda.Stream(device=on(r)) for r in range(n)]
         for ci, (name, coll, op, dt, count) in enumerate(RC.CASES):
             xs = [RC.gen_input(ci, r, n) for r in range(n)]
-            xb = [torch.from_numpy(x.view(np.uint8).copy()).cuda() for x in xs]
+            xb = [torch.from_numpy(x.view(np.uint8).copy()).to(on(r)) for r, x in enumerate(xs)]
             nout = RC.out_count(ci, n)
-            yb = [torch.empty(nout * xs[0].dtype.itemsize, dtype=torch.uint8, device="cuda")
-                  for _ in range(n)]
+            yb = [torch.empty(nout * xs[0].dtype.itemsize, dtype=torch.uint8, device=on(r))
+                  for r in range(n)]
             keep = []
             if coll == "ar_mis":  # the same bytes at (send, recv) offsets off 16-byte alignment
                 so, ro = RC.mis_offsets(dt)
                 for r in range(n):
-                    xm = torch.zeros(xb[r].numel() + 16, dtype=torch.uint8, device="cuda")
+                    xm = torch.zeros(xb[r].numel() + 16, dtype=torch.uint8, device=on(r))
                     xm[so:so + xb[r].numel()] = xb[r]
-                    keep.append((xm, torch.zeros(yb[r].numel() + 16, dtype=torch.uint8, device="cuda")))
-            torch.cuda.synchronize()
+                    keep.append((xm, torch.zeros(yb[r].numel() + 16, dtype=torch.uint8, device=on(r))))
+            for r in range(n):
+                torch.cuda.synchronize(on(r))
             nccl.group_start()
             for r, c in enumerate(comms):
                 sp = streams[r].cuda_stream
@@ -160,7 +175,8 @@ def test_single_process_ranks(n, monkeypatch):
                 else:
                     c.all_gather(xb[r].data_ptr(), yb[r].data_ptr(), count, dt, sp)
             nccl.group_end()
-            torch.cuda.synchronize()
+            for r in range(n):
+                torch.cuda.synchronize(on(r))
             for c in comms:
                 assert c.async_error() == 0, f"{name}: spin timeout (protocol hang)"
             outs = [(xb[r] if coll == "ar_inplace" else yb[r]).cpu().numpy().view(xs[0].dtype)
