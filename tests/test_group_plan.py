@@ -277,6 +277,29 @@ def test_hand_derived_ll_call_moves_the_cursor():
     assert ring_parts[1][:5] != parts[1][:5]
 
 
+def test_hand_derived_ll_split_then_ring_at_four_ranks():
+    """another plan worked through enqueue.cc:352-437, :518-681 by
+    hand and asserted on the library directly (not only through the Python
+    restatement).  4 ranks, 48 channels: fp32 all-reduces of 32 KiB (LL) and
+    4 MiB (ring) in one group.  Sorter + LIFO bin: [32 KiB, 4 MiB]; 4 MiB is
+    not within 4x of 32 KiB, so two aggregates.  trafficBytes: LL 32 KiB x 2
+    x 4 = 256 KiB, ring 4 MiB x 2 = 8 MiB; nMaxChannels: LL (threshold 8, 512
+    threads) 8, ring 48 -> min(56, 48) = 48; trafficPerChannel = 8,650,752 /
+    48 = 180,224 B.
+      LL call at (0, 0): cell 2 KiB (traffic x 8), 16 cells, cellsPerChannel
+        = cellsLo = divUp(180,224, 16,384) = 11, hi 5 -> ch 0..1, counts
+        (5,632, 0, 2,560); cursor -> (1, 2,560 x 32 = 81,920)
+      ring call at (1, 81,920): cell 8 KiB, 512 cells, lo = divUp(98,304,
+        16,384) = 6, 46 mid x 11 with no remainder -> 45 mid + hi 11
+        -> ch 1..47, counts (12,288, 22,528, 22,528)."""
+    pol = dict(DEFAULTS_8, ll_rsag_max=4 * (128 << 10))
+    calls = [(0, 8192, 7, 0), (0, 1 << 20, 7, 0)]
+    algos, order, plan_of, parts = _check_equal_ex(calls, 4, 48, pol)
+    assert algos == ["ll", "ring"] and order == [0, 1] and plan_of == [0, 0]
+    assert parts[0][:5] == (0, 1, 5632, 0, 2560)
+    assert parts[1][:5] == (1, 47, 12288, 22528, 22528)
+
+
 def test_aggregate_takes_one_path():
     """Two fp32 all-reduces of 48 KiB and 100 KiB at 8 ranks: each alone is
     on the LL path (<= 128 KiB), but the second is within 4x of the first, so
