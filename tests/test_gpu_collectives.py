@@ -40,7 +40,11 @@ TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": 
              "VCCL_ALLOW_SHARED_DEVICE": "1", "VCCL_LL_THRESHOLD": str(1 << 20),
              "VCCL_LL_MAX_BLOCKS": "32", "VCCL_DIRECT_THRESHOLD": str(4 << 20),
              "VCCL_DIRECT_MAX_BLOCKS": "16", "VCCL_DIRECT_CHUNK_BYTES": str(1 << 20),
-             "VCCL_DIRECT_RSAG_THRESHOLD": str(64 << 20)}
+             "VCCL_DIRECT_RSAG_THRESHOLD": str(64 << 20),
+             # every SIMPLE-ring slot through the per-wave hand-off (the
+             # default takes it from 512 KiB slots up; "ring_only" below runs
+             # the workgroup hand-off for every slot instead)
+             "VCCL_RING_WAVE_MIN": "0"}
 # the group tests' direct thresholds: a group's aggregate takes the path of
 # its summed size, so the ZeRO loop's 128 MiB of reduce-scatters and 16 MiB
 # of all-reduces need raised thresholds to stay on the direct path
@@ -244,6 +248,7 @@ def _ring_ranks(n, geom):
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
         if geom == "ring_only":  # NCCL_ALGO=Ring: the ring for every all-reduce,
             env["NCCL_ALGO"] = "Ring"  # ring LL (one-hop) for small RS / AG
+            env["VCCL_RING_WAVE_MIN"] = str(1 << 40)  # the workgroup hand-off for every slot
             ll_max = direct_max = 0
             ll_rs_max = LL_DEFAULT
         if geom == "direct_only":  # every collective takes the direct path, any size

@@ -34,7 +34,7 @@
 #ifndef VCCL_RING_SPOLL
 // 1: prim_ws reads a missing credit once through the scalar unit before it
 // drains its stores and polls (see sread_u64); 0: drain first, always.
-#define VCCL_RING_SPOLL 1
+#define VCCL_RING_SPOLL 0
 #endif
 #ifndef VCCL_RING_LAST_DRAINS
 // 1: the wave that finishes issuing a slot last drains and posts at once
@@ -42,9 +42,17 @@
 #define VCCL_RING_LAST_DRAINS 1
 #endif
 #ifndef VCCL_RING_WAVE_SYNC
-// 1: per-wave slot hand-off (RingCtx::prim_ws); 0: the workgroup-barrier
-// hand-off of rounds 1-4 (RingCtx::prim_wg), kept for A/B.
-#define VCCL_RING_WAVE_SYNC 1
+// 0 (default): the workgroup hand-off (RingCtx::prim_wg: every wave drains,
+// a barrier, thread 0 posts).  1: the per-wave hand-off (RingCtx::prim_ws:
+// each wave drains its slot behind its next slot's loads, the last wave
+// posts; workgroup hand-off below VCCL_RING_WAVE_MIN).  Round 5 built and
+// measured it: the drain per slot fell from 9.8 to 3.3 us, but on every
+// shared-GPU rehearsal row the ring was level or slower — 2-3 us per call
+// at 256 KiB - 8 MiB, 2-4 % at 1 GiB (profiles/r05k, r05n, r05o) — so it
+// stays an opt-in build (make VARIANT=_ws DEFS=-DVCCL_RING_WAVE_SYNC=1)
+// until a run over xGMI, where remote stores acknowledge slowly, says
+// otherwise.
+#define VCCL_RING_WAVE_SYNC 0
 #endif
 
 // LDS / global pointers are typed as such: through a generic pointer the
@@ -65,6 +73,7 @@ struct WaveSync {
   uint32_t done[kSyncDepth];
   uint64_t tail, head;
   int abort;
+  int poller;  // 1 while one wave polls the flags for the workgroup
 };
 
 // Flags through global-typed pointers: a generic pointer would make these
@@ -126,6 +135,7 @@ struct RingCtx {
   int* errorFlag;
   uint64_t spinTimeout;
   int useFences, pollMode, traceCap;
+  int64_t waveMin;  // prim_ws: slots of at least this many bytes hand over per wave
   int lane, nWaves;
   uint32_t seq;  // prims this workgroup has started in this launch (same in every wave)
   bool pend;
@@ -188,6 +198,7 @@ struct RingCtx {
     useFences = m->useFences;
     pollMode = m->pollMode;
     traceCap = m->traceCap;
+    waveMin = m->ringWaveMin;
   }
 
   __device__ bool aborted() const { return __hip_atomic_load(shAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; }
@@ -256,16 +267,112 @@ struct RingCtx {
     }
     return true;
   }
-  // Bounded spin on a flag until it reaches `target`; the value seen goes to
-  // the LDS cache `*cache` (max).  Lane 0 only.
+  // Bounded spin on a flag until it reaches `target`; every value seen goes
+  // to the LDS cache `*cache` (max) at once — other waves wait on that cache
+  // for targets of their own, possibly lower ones this spin passes on the way
+  // (a wave behind must not wait for the poller's higher target: its own
+  // slot may be what lets the peer reach it).  Lane 0 only.
   __device__ bool spin_cache(const uint64_t* flag, uint64_t target, VCCL_LDS uint64_t* cache) {
-    uint64_t v = poll(flag);
-    if (v < target) {
-      if (!spin_ge(flag, target)) return false;
-      v = poll(flag);
+    uint64_t spins = 0, start = 0, seen = 0;
+    for (;;) {
+      const uint64_t v = poll(flag);
+      if (v > seen) {
+        seen = v;
+        __hip_atomic_fetch_max(cache, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (v >= target) return true;
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (start == 0) start = now;
+        if (*abortFlag) return false;
+        if (now - start > spinTimeout) {
+          __hip_atomic_store(errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return false;
+        }
+        if (__hip_atomic_load(errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
+      }
     }
-    __hip_atomic_fetch_max(cache, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return true;
+  }
+
+  // The poller's spin (lane 0): BOTH flags every round, every value seen
+  // published to the LDS cache at once, until its own targets are met —
+  // whatever another wave waits for (tail or head, a lower target or a
+  // higher one) shows in the cache as soon as it is in memory, so no wave
+  // waits on the poller's own target.
+  __device__ bool poll_both(uint64_t needTail, uint64_t needHead) {
+    uint64_t spins = 0, start = 0, seenT = 0, seenH = 0;
+    for (;;) {
+      const uint64_t t = poll(recvTail), h = poll(sendHead);
+      if (t > seenT) {
+        seenT = t;
+        __hip_atomic_fetch_max(&ws->tail, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (h > seenH) {
+        seenH = h;
+        __hip_atomic_fetch_max(&ws->head, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (t >= needTail && h >= needHead) return true;
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255) == 0) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (start == 0) start = now;
+        if (*abortFlag) return false;
+        if (now - start > spinTimeout) {
+          __hip_atomic_store(errorFlag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return false;
+        }
+        if (__hip_atomic_load(errorFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return false;
+      }
+    }
+  }
+  // This wave polls the flags itself (lane 0) until they reach the targets
+  // (system-scope acquire after them with VCCL_FENCES); false on abort /
+  // peer error / timeout.
+  template <bool RECV>
+  __device__ __forceinline__ bool poll_credits(uint64_t needTail, uint64_t needHead) {
+    int ok = 1;
+    if (lane == 0) {
+      if (RECV && !spin_cache(recvTail, needTail, &ws->tail)) ok = 0;
+      if (ok && needHead && !spin_cache(sendHead, needHead, &ws->head)) ok = 0;
+      if (!ok) set_aborted();
+      if (ok && useFences) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
+        drain_vmem();
+      }
+    }
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+  }
+  // One poller per workgroup: the first wave that needs a credit the LDS
+  // cache lacks takes the poller token and polls the flags; the others watch
+  // the cache (an LDS read, no memory traffic) and take the token over when
+  // it is free and the cache still falls short.  With every wave polling on
+  // its own, the slot starts when the LAST wave happens to re-read the flag
+  // (+1 µs per step on 256 KiB - 8 MiB rings, profiles/r05k).
+  template <bool RECV>
+  __device__ __forceinline__ bool wait_credits(uint64_t needTail, uint64_t needHead) {
+    for (;;) {
+      if (__hip_atomic_load(&ws->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needTail &&
+          __hip_atomic_load(&ws->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needHead)
+        return true;
+      if (aborted()) return false;
+      int got = 0;
+      if (lane == 0) {
+        int expect = 0;
+        got = __hip_atomic_compare_exchange_strong(&ws->poller, &expect, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+      }
+      if (__builtin_amdgcn_readfirstlane(got)) {
+        int ok = 1;
+        if (lane == 0) {
+          ok = poll_both(needTail, needHead) ? 1 : 0;
+          if (!ok) set_aborted();
+          __hip_atomic_store(&ws->poller, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return __builtin_amdgcn_readfirstlane(ok) != 0;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
   }
 
   template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
@@ -278,6 +385,22 @@ struct RingCtx {
     if (seq >= (uint32_t)kSyncDepth && !wait_done(seq - kSyncDepth)) return;
     const uint64_t needTail = RECV ? recvStep + 1 : 0;
     const uint64_t needHead = SEND && sendStep + 1 > (uint64_t)kSteps ? sendStep + 1 - kSteps : 0;
+    // Slots below VCCL_RING_WAVE_MIN (latency-bound: a few KiB per wave)
+    // hand over as a workgroup: without the barrier the waves drift apart and
+    // every step waits for the last of them (+1 us per step from 256 KiB to
+    // 8 MiB, profiles/r05k / r05m); the overlap pays from full slots up.
+    const bool waveMode = (nelem > 0 ? nelem * (int64_t)sizeof(T) : 0) >= waveMin;  // wave-uniform
+    if (!waveMode) {
+      complete_pending<0>();
+      drain_vmem();  // a per-wave post of the previous slot retires before this slot's post
+      prim_wg<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, src, dst, nelem, postOp, recvOff, sendOff);
+      // prim_wg stepped the counters; count the slot done for every wave
+      if (tid == 0)
+        __hip_atomic_fetch_add(&ws->done[seq % kSyncDepth], (uint32_t)nWaves, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      seq++;
+      return;
+    }
     bool have = __hip_atomic_load(&ws->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needTail &&
                 __hip_atomic_load(&ws->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needHead;
 #if VCCL_RING_SPOLL
@@ -292,17 +415,7 @@ struct RingCtx {
 #endif
     if (!have || useFences) {
       complete_pending<0>();  // never hold a post while waiting on a peer
-      int ok = 1;
-      if (lane == 0) {
-        if (RECV && !spin_cache(recvTail, needTail, &ws->tail)) ok = 0;
-        if (ok && needHead && !spin_cache(sendHead, needHead, &ws->head)) ok = 0;
-        if (!ok) set_aborted();
-        if (ok && useFences) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire
-          drain_vmem();
-        }
-      }
-      if (!__builtin_amdgcn_readfirstlane(ok)) return;
+      if (!(useFences ? poll_credits<RECV>(needTail, needHead) : wait_credits<RECV>(needTail, needHead))) return;
     }
     const uint64_t t1 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
     constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
@@ -342,7 +455,6 @@ struct RingCtx {
       rec.bytes = (uint32_t)(nelem > 0 ? nelem * (int64_t)sizeof(T) : 0);
       rec.step = SEND ? sendStep : recvStep;
     }
-    pend = true;
     pSend = SEND;
     pRecv = RECV;
     pSeq = seq;
@@ -351,6 +463,7 @@ struct RingCtx {
     pBytes = (uint32_t)(nelem > 0 ? sendOff + nelem * (int64_t)sizeof(T) : 0);
     pTrace = trace != nullptr && traceN < traceCap;
     pTraceIx = (uint32_t)traceN;
+    pend = true;
     // The last wave to finish issuing this slot is the one whose drain gates
     // the post (every other wave has moved on and counted itself): it drains
     // now instead of after its next credit check and loads, so the post comes
@@ -383,7 +496,7 @@ struct RingCtx {
   //   recvOff / sendOff: byte offset of the chunk inside its slot (< 16)
   // (Rounds 1-4: the workgroup hand-off — VCCL_RING_WAVE_SYNC=0.)
   template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
-  __device__ void prim_wg(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
+  __device__ __forceinline__ void prim_wg(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
                           int recvOff = 0, int sendOff = 0) {
     if (aborted()) return;
     const bool tr = trace != nullptr && traceN < traceCap;

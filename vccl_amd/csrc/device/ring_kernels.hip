@@ -69,6 +69,7 @@ __global__ __launch_bounds__(kRingMaxThreads) void k_ring(RingBatch b) {
     for (int i = 0; i < kSyncDepth; i++) ws.done[i] = 0;
     ws.tail = ws.head = 0;
     ws.abort = 0;
+    ws.poller = 0;
   }
   DevChannel* ch = &w.channels[blockIdx.x];
   RingCtx r;

@@ -109,6 +109,9 @@ struct DevComm {
   // hand-offs of each launch as RingTraceRec; nullptr = off.
   uint64_t* trace;
   int traceCap;
+  // SIMPLE ring slots of at least this many bytes hand over per wave
+  // (ring.hpp prim_ws), smaller ones as a workgroup (VCCL_RING_WAVE_MIN)
+  int64_t ringWaveMin;
 };
 
 // One SIMPLE-ring slot hand-off, s_memrealtime ticks (100 MHz), taken by

@@ -599,6 +599,10 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   dc.useFences = (int)param_int("FENCES", 0);
   if (anyNet) dc.useFences = 1;  // slots and flags in host memory: full system-scope fences
   dc.pollMode = (int)param_int("POLL_MODE", 0);
+  // SIMPLE ring hand-off per slot size (ring.hpp prim_ws): per wave from a
+  // full default slot up (the bandwidth regime), as a workgroup below
+  // (latency-bound slots, profiles/r05k); 0 = always per wave
+  dc.ringWaveMin = std::max<int64_t>(0, param_int("RING_WAVE_MIN", 512 << 10));
   // Opt-in slot timeline of the SIMPLE ring (vcclCommRingTrace)
   c->ringTraceCap = n > 1 ? (int)std::max<int64_t>(0, std::min<int64_t>(param_int("RING_TRACE", 0), 1 << 16)) : 0;
   if (c->ringTraceCap > 0) {
