@@ -1217,6 +1217,11 @@ def bench_extras(dist, comm, rank, world, args):
         ex["rs_ag_sizes_error"] = repr(e)
     finally:
         comm.set_algo(None)
+    try:  # config 3 on communicators bounded to C ring channels: the link model's headroom
+        ex["allreduce_f32_by_channels"] = _channel_rows(dist, rank, world, args.bytes or (1 << 30),
+                                                        min(args.steps, 5))
+    except Exception as e:  # noqa: BLE001
+        ex["channels_error"] = repr(e)
     # Last: config 5 without per-call launch cost (nccl-tests -G: HIP graph
     # replay).  Its capture stream is one more hardware queue per process;
     # with 8 ranks sharing one GPU (rehearsal) that oversubscribes the
@@ -1236,6 +1241,43 @@ def bench_extras(dist, comm, rank, world, args):
 
 
 BCAST_SIZES = (64 << 10, 8 << 20, 256 << 20)
+CHANNELS_PER_RING = (2, 4, 8, 16, 32, 64)  # x rings, within the device limit of 128
+
+
+def _channel_rows(dist, rank, world, S, steps, warmup=2):
+    """Config 3 (S-byte fp32 ring all-reduce) on fresh communicators bounded
+    to C ring channels (ncclConfig minCTAs = maxCTAs = C, graph/connect.cc:
+    486-490), C = rings x {2 .. 64}: on one rank per GPU the row where busbw
+    stops growing measures the headroom H the default channel model assumes
+    (host/init.cc); ranks sharing a GPU are capped to their
+    co-resident share (n_channels says what ran).  Each row's output is
+    checked on the same comm (pattern inputs, every rank)."""
+    rings = len(nccl.ring_orders(world))
+    counts = sorted({min(128, rings * k) for k in CHANNELS_PER_RING})
+    sp = torch.cuda.current_stream().cuda_stream
+    n = S // 4
+    x = torch.rand(n, device="cuda") * 2 - 1
+    y = torch.empty_like(x)
+    rows = []
+    for C in counts:
+        obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        cfg = nccl.ncclConfig_t.initializer(minCTAs=C, maxCTAs=C)
+        c = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank, config=cfg)
+        try:
+            c.set_algo("ring")
+            dt = _time_coll(dist, lambda: c.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32,
+                                                       nccl.ncclSum, sp), steps, warmup)
+            c.set_algo(None)
+            ok = check_ar(dist, c, rank, world, S, algo="ring")
+            algbw = n * 4 * steps / dt / 1e9
+            rows.append({"channels_asked": C, "n_channels": c.n_channels(), "bytes": n * 4,
+                         "us": round(dt / steps * 1e6, 1),
+                         "busbw": round(algbw * 2 * (world - 1) / world, 2), "correct": ok})
+        finally:
+            c.destroy()
+    del x, y
+    return rows
 
 
 def _bcast_row(dist, comm, rank, world, S, root=0):
