@@ -952,6 +952,7 @@ def bench_allreduce(args):
             plan[f"ar_default_{S}"] = ("ar", {"nbytes": S})
         for S in EXTRA_F16_SIZES:
             plan[f"ar_f16_{S}"] = ("ar", {"nbytes": S, "dtype": "f16"})
+            plan[f"ar_f16_ring_{S}"] = ("ar", {"nbytes": S, "dtype": "f16", "algo": "ring"})
         for algo in ("ring", "direct"):
             for S in (64 << 20, head):
                 plan[f"ar_{algo}_{S}"] = ("ar", {"nbytes": S, "algo": algo})
@@ -1021,7 +1022,8 @@ def bench_allreduce(args):
 
 
 EXTRA_F32_SIZES = (8, 1 << 10, 8 << 10, 64 << 10, 1 << 20, 8 << 20, 64 << 20)
-EXTRA_F16_SIZES = (8, 1 << 10, 16 << 10, 128 << 10)
+EXTRA_F16_SIZES = tuple(8 << k for k in range(15))  # config 5: 8 B - 128 KiB in x2 steps
+GRAPH_F16_SIZES = (8, 1 << 10, 16 << 10, 128 << 10)  # config 5 in graph mode
 EXTRA_GROUP_SIZES = (4 << 10, 32 << 10)
 EXTRA_RSAG_SIZES = (64 << 10, 1 << 20, 8 << 20)  # whole bucket (n blocks), f32
 # the mid range VCCL's tuner gives LL128 (enqueue.cc:2032): every path forced
@@ -1161,8 +1163,13 @@ def bench_extras(dist, comm, rank, world, args):
                                      for S in EXTRA_F32_SIZES]
         ex["allreduce_f16_ll"] = [_ar_size_row(dist, comm, rank, world, S, "f16", 50, 5)
                                   for S in EXTRA_F16_SIZES]
+        comm.set_algo("ring")  # config 5's comparison: the SIMPLE ring at the same sizes
+        ex["allreduce_f16_ring"] = [_ar_size_row(dist, comm, rank, world, S, "f16", 50, 5)
+                                    for S in EXTRA_F16_SIZES]
     except Exception as e:  # noqa: BLE001 - reported, not fatal to the headline
         ex["allreduce_error"] = repr(e)
+    finally:
+        comm.set_algo(None)
     try:
         ex["group_fusion_f32"] = [_group_row(dist, comm, rank, world, S, 16) for S in EXTRA_GROUP_SIZES]
         ex["zero_group_rs_bf16"] = _zero_group_row(dist, comm, rank, world)
@@ -1233,7 +1240,7 @@ def bench_extras(dist, comm, rank, world, args):
         # ~4.2 us (tools/ll_graph_probe.py, profiles/r04g)
         cap = torch.cuda.Stream()
         ex["allreduce_f16_ll_graph"] = [_ar_graph_row(dist, comm, rank, world, S, stream=cap)
-                                        for S in EXTRA_F16_SIZES]
+                                        for S in GRAPH_F16_SIZES]
     except Exception as e:  # noqa: BLE001
         ex["graph_error"] = repr(e)
     ex["async_error"] = comm.async_error()
