@@ -15,10 +15,12 @@ N > 1 (torch.distributed.run, one process per GPU): BASELINE config 3 at a
   over ranks rides along as config.aggregate_busbw_all_ranks.
   torch.distributed (gloo, CPU tensors) only ships the unique id, barriers and
   the max-over-ranks time.  The same run adds `extras` (not `value`): config 3
-  at a few sizes, config 5 (fp16 LL sizes), config 4 (RS + AG bf16, 4 GiB
-  bucket), the ring and the direct algorithm each forced at 64 MiB and the
-  headline bucket, and group aggregation (16 small all-reduces issued one by
-  one vs in one group) — skip with --no-extras.
+  at a few sizes, config 5 (fp16, 8 B - 128 KiB, beside the SIMPLE ring and
+  in graph mode), config 4 (RS + AG bf16, 4 GiB bucket), the ring and the
+  direct algorithm each forced at 64 MiB and the headline bucket, the
+  mid-range paths, group aggregation (16 small all-reduces issued one by one
+  vs in one group), and config 3 on comms bounded to rings x 2..64 channels
+  — skip with --no-extras.  Every timed path is checked afterwards.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--bytes S]
        [--workload reduce_copy|allreduce|rs_ag] [--sweep] [--no-extras]
