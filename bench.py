@@ -834,7 +834,7 @@ def _fences_plan(plan, algo_of):
     algo_of(kind, kw) -> the algorithm the library runs for that check."""
     fam = {}
     for name, (kind, kw) in plan.items():
-        key = (kind, kw.get("dtype"), algo_of(kind, kw), kw.get("k"))
+        key = (kind, kw.get("dtype"), algo_of(kind, kw), kw.get("k"), kw.get("wave"))
         if key not in fam or kw.get("nbytes", 0) < fam[key][1][1].get("nbytes", 0):
             fam[key] = (name, (kind, kw))
     out = {}
@@ -869,6 +869,8 @@ def run_checks(dist, comm, rank, world, plan):
         r = {}
         for name, (kind, kw) in pl.items():
             t0 = time.perf_counter()
+            kw = dict(kw)
+            comm.set_ring_wave(kw.pop("wave", False))  # the ring's slot hand-off for this check
             try:
                 if kind == "ar":
                     r[name] = check_ar(dist, comm, rank, world, **kw)
@@ -881,6 +883,8 @@ def run_checks(dist, comm, rank, world, plan):
                     r[name + "_rs"], r[name + "_ag"] = rs_ok, ag_ok
             except Exception as e:  # noqa: BLE001 - a failed check is a verdict, not a crash
                 r[name] = f"error: {e!r}"
+            finally:
+                comm.set_ring_wave(False)
             res["check_ms"][f"{mode}:{name}"] = round((time.perf_counter() - t0) * 1e3, 1)
         res[mode] = r
     comm.set_fences(False)
@@ -961,6 +965,10 @@ def bench_allreduce(args):
         for algo in MID_ALGOS:
             for S in MID_SIZES:
                 plan[f"ar_mid_{algo}_{S}"] = ("ar", {"nbytes": S, "algo": algo})
+        for S in (64 << 20, head):  # the ring's per-wave slot hand-off (ring_handoff rows)
+            plan[f"ar_ring_wave_{S}"] = ("ar", {"nbytes": S, "algo": "ring", "wave": True})
+        plan[f"rs_ag_bf16_ring_wave_{args.rs_ag_bytes}"] = ("rs_ag", {"nbytes": args.rs_ag_bytes, "algo": "ring",
+                                                                      "wave": True})
         for S in EXTRA_GROUP_SIZES:
             plan[f"group16_{S}"] = ("group", {"nbytes": S, "k": 16})
         plan[f"zero_group16_{ZERO_BUCKET}"] = ("zero_group", {"nbytes": ZERO_BUCKET, "k": 16})
@@ -1188,6 +1196,22 @@ def bench_extras(dist, comm, rank, world, args):
     except Exception as e:  # noqa: BLE001
         ex["by_algo_error"] = repr(e)
     finally:
+        comm.set_algo(None)
+    try:  # the SIMPLE ring's slot hand-off: the workgroup one (default) vs per wave
+        # (vcclCommSetRingWave / VCCL_RING_WAVE), config 3 and config 4 on the ring
+        ex["ring_handoff"] = {}
+        comm.set_algo("ring")
+        for wave in (False, True):
+            comm.set_ring_wave(wave)
+            ex["ring_handoff"]["per_wave" if wave else "workgroup"] = {
+                "allreduce_f32": [_ar_size_row(dist, comm, rank, world, S, "f32", st, 2)
+                                  for S, st in ((64 << 20, 10), (args.bytes or (1 << 30), 5))],
+                "rs_ag_bf16": _rs_ag(dist, comm, rank, world, args.rs_ag_bytes, min(args.steps, 10), 2)}
+        ex["ring_handoff"]["per_wave_launches"] = comm.set_ring_wave(False)
+    except Exception as e:  # noqa: BLE001
+        ex["ring_handoff_error"] = repr(e)
+    finally:
+        comm.set_ring_wave(False)
         comm.set_algo(None)
     try:  # the mid range (64 KiB - 8 MiB: LL128's slot in VCCL's tuner), each path forced
         ex["allreduce_f32_mid_by_algo"] = {}

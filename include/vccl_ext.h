@@ -38,6 +38,22 @@
  *                     one process can check a transport both ways.  Blocks
  *                     until the device is idle; call with no collective of
  *                     this communicator in flight.
+ *   vcclCommSetRingWave  the SIMPLE ring's slot hand-off for this
+ *                     communicator's later launches: 0 (the default, or
+ *                     VCCL_RING_WAVE=0 at init) the workgroup hand-off — every
+ *                     wave drains its stores, a barrier, one thread posts, as
+ *                     the reference's postPeer after its barrier
+ *                     (src/device/prims_simple.h:183-319); 1 the per-wave
+ *                     hand-off, each wave draining its slot behind its next
+ *                     slot's loads and the last one posting,
+ *                     for the kernels built with it (sums over f32 / f16 /
+ *                     bf16, the byte-copy all-gather and broadcast; other
+ *                     calls keep the workgroup hand-off).  Same FIFOs,
+ *                     partition and fold either way, so results are
+ *                     identical and calls may switch between the two.
+ *                     perWave -1 leaves the setting as it is; *waveLaunches
+ *                     (may be NULL): ring launches that ran the per-wave
+ *                     kernel so far.  Host only.
  *   vcclCommDebugSetEpochs  overwrite the device-resident call epochs of the
  *                     one-shot LL and two-shot direct paths (tests of the
  *                     32-bit wrap; the reference's TEST_LL_CLEANUP knob,
@@ -138,6 +154,7 @@ ncclResult_t vcclCommRingTrace(ncclComm_t comm, void* hostBuf, size_t bytes, int
 ncclResult_t vcclCommNetStats(ncclComm_t comm, uint64_t* bytesSent, uint64_t* bytesReceived,
                               int* connections);
 ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences);
+ncclResult_t vcclCommSetRingWave(ncclComm_t comm, int perWave, unsigned long long* waveLaunches);
 ncclResult_t vcclCommDebugSetEpochs(ncclComm_t comm, uint32_t llEpoch, uint32_t directEpoch);
 ncclResult_t vcclRingPartition(int coll, size_t count, ncclDataType_t datatype, int nRanks,
                                int nChannels, int proto, size_t stepBytes, int nThreads,

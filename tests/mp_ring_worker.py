@@ -65,6 +65,7 @@ def main():
     before = comm.launch_stats()
     res["launch_stats"] = np.array(before, dtype=np.int64)
     res["net_stats"] = np.array(comm.net_stats(), dtype=np.int64)
+    res["wave_launches"] = np.int64(comm.set_ring_wave(None))  # ring launches on the per-wave kernel
     err = comm.async_error()
     comm.destroy()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)

@@ -41,10 +41,11 @@ TEST_GEOM = {"VCCL_NCHANNELS": "14", "VCCL_NTHREADS": "512", "VCCL_SLOT_BYTES": 
              "VCCL_LL_MAX_BLOCKS": "32", "VCCL_DIRECT_THRESHOLD": str(4 << 20),
              "VCCL_DIRECT_MAX_BLOCKS": "16", "VCCL_DIRECT_CHUNK_BYTES": str(1 << 20),
              "VCCL_DIRECT_RSAG_THRESHOLD": str(64 << 20),
-             # every SIMPLE-ring slot through the per-wave hand-off (the
-             # default takes it from 512 KiB slots up; "ring_only" below runs
-             # the workgroup hand-off for every slot instead)
-             "VCCL_RING_WAVE_MIN": "0"}
+             # the SIMPLE ring's per-wave hand-off (VCCL_RING_WAVE, the PART 4
+             # kernels: f32 / f16 / bf16 sums, all-gather, broadcast) for every
+             # slot, not only from 512 KiB up; "ring_only" below and the
+             # library-default rows run the workgroup hand-off (the default)
+             "VCCL_RING_WAVE": "1", "VCCL_RING_WAVE_MIN": "0"}
 # the group tests' direct thresholds: a group's aggregate takes the path of
 # its summed size, so the ZeRO loop's 128 MiB of reduce-scatters and 16 MiB
 # of all-reduces need raised thresholds to stay on the direct path
@@ -210,7 +211,7 @@ def _multi_gpu_ns():
     return sorted({2, min(ndev, 8)}) if ndev >= 2 else [2]
 
 
-@pytest.mark.parametrize("geom", ["xgmi", "xgmi_fences", "xgmi_ll128"])
+@pytest.mark.parametrize("geom", ["xgmi", "xgmi_fences", "xgmi_ll128", "xgmi_wave"])
 @pytest.mark.parametrize("n", _multi_gpu_ns())
 def test_one_rank_per_gpu(n, geom):
     ndev = torch.cuda.device_count()
@@ -248,7 +249,7 @@ def _ring_ranks(n, geom):
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
         if geom == "ring_only":  # NCCL_ALGO=Ring: the ring for every all-reduce,
             env["NCCL_ALGO"] = "Ring"  # ring LL (one-hop) for small RS / AG
-            env["VCCL_RING_WAVE_MIN"] = str(1 << 40)  # the workgroup hand-off for every slot
+            env["VCCL_RING_WAVE"] = "0"  # the workgroup hand-off for every slot
             ll_max = direct_max = 0
             ll_rs_max = LL_DEFAULT
         if geom == "direct_only":  # every collective takes the direct path, any size
@@ -277,6 +278,8 @@ def _ring_ranks(n, geom):
         direct_max, chunk = (8 << 20) if n >= 4 else 0, 16 << 20
         if geom == "xgmi_fences":  # system-scope acquire / release around every slot
             env["VCCL_FENCES"] = "1"
+        if geom == "xgmi_wave":  # the per-wave ring hand-off, where remote stores acknowledge slowly
+            env.update(VCCL_RING_WAVE="1", VCCL_RING_WAVE_MIN="0")
         if geom == "xgmi_ll128":  # every collective on the LL128 ring
             env["NCCL_PROTO"] = "LL128"
             ll_max = direct_max = 0
@@ -329,6 +332,13 @@ def _ring_ranks(n, geom):
                 assert conns == 2 * nch and sent > 0 and recvd > 0, (r, sent, recvd, conns)
             else:
                 assert conns == 0 and sent == 0, (r, sent, conns)
+        # VCCL_RING_WAVE=1 rows ran the per-wave ring kernels (their f16 / f32 /
+        # bf16 sum ring calls and all-gathers), the others never did
+        waves = [int(res[r]["wave_launches"]) for r in range(n)]
+        if env.get("VCCL_RING_WAVE") == "1" and geom in ("test", "chain", "net", "xgmi_wave"):
+            assert min(waves) > 0, waves
+        elif env.get("VCCL_RING_WAVE", "0") == "0":
+            assert max(waves) == 0, waves
 
 
 def test_beyond_2gib_two_ranks():

@@ -34,10 +34,14 @@ from vccl_amd import nccl  # noqa: E402
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(n, mode, ncomms, spin_timeout):
+def _run(n, mode, ncomms, spin_timeout, wave=0):
     uids = ",".join(nccl.unique_id_to_bytes(nccl.get_unique_id()).hex() for _ in range(ncomms))
     env = _mp.worker_env(os.environ)
     env["VCCL_SPIN_TIMEOUT_S"] = str(spin_timeout)
+    # the SIMPLE ring's workgroup (0) or per-wave (1) slot hand-off: each has
+    # its own spins (ring.hpp prim_wg / prim_ws), each must end on a lost peer
+    env["VCCL_RING_WAVE"] = str(wave)
+    env["VCCL_RING_WAVE_MIN"] = "0"
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mp_fail_worker.py"),
                                    str(r), str(n), d, mode, uids], env=env,
@@ -58,9 +62,10 @@ def _run(n, mode, ncomms, spin_timeout):
     return res, "\n".join(logs)
 
 
-def test_lost_peer_ends_ring_ll_direct_kernels():
+@pytest.mark.parametrize("wave", [0, 1])
+def test_lost_peer_ends_ring_ll_direct_kernels(wave):
     n, timeout_s = 3, 3
-    res, logs = _run(n, "peer_loss", 3, timeout_s)
+    res, logs = _run(n, "peer_loss", 3, timeout_s, wave)
     for r in res[:-1]:
         for path in ("ring", "ll", "direct"):
             v = r[path]
@@ -70,8 +75,9 @@ def test_lost_peer_ends_ring_ll_direct_kernels():
     assert res[-1]["ok"] and res[-1]["lost_peer"]
 
 
-def test_abort_from_second_thread_ends_spinning_kernel():
-    res, logs = _run(2, "abort", 1, 60)  # the spin timeout alone would take 60 s
+@pytest.mark.parametrize("wave", [0, 1])
+def test_abort_from_second_thread_ends_spinning_kernel(wave):
+    res, logs = _run(2, "abort", 1, 60, wave)  # the spin timeout alone would take 60 s
     v = res[0]["abort_thread"]
     assert v["ok"], (v, logs)
     assert v["kernel_end_s"] < 20 and v["abort_s"] < 15

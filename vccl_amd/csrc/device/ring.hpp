@@ -42,16 +42,16 @@
 #define VCCL_RING_LAST_DRAINS 1
 #endif
 #ifndef VCCL_RING_WAVE_SYNC
-// 0 (default): the workgroup hand-off (RingCtx::prim_wg: every wave drains,
-// a barrier, thread 0 posts).  1: the per-wave hand-off (RingCtx::prim_ws:
-// each wave drains its slot behind its next slot's loads, the last wave
-// posts; workgroup hand-off below VCCL_RING_WAVE_MIN).  Round 5 built and
-// measured it: the drain per slot fell from 9.8 to 3.3 us, but on every
-// shared-GPU rehearsal row the ring was level or slower — 2-3 us per call
-// at 256 KiB - 8 MiB, 2-4 % at 1 GiB (profiles/r05k, r05n, r05o) — so it
-// stays an opt-in build (make VARIANT=_ws DEFS=-DVCCL_RING_WAVE_SYNC=1)
-// until a run over xGMI, where remote stores acknowledge slowly, says
-// otherwise.
+// 0 (PART 0 objects): the workgroup hand-off (RingCtx::prim_wg: every wave
+// drains, a barrier, thread 0 posts).  1 (PART 4 objects, ring_kernels.hip):
+// the per-wave hand-off (RingCtx::prim_ws: each wave drains its slot behind
+// its next slot's loads, the last wave posts; workgroup hand-off below
+// VCCL_RING_WAVE_MIN).  Round 5 measured it: the drain per slot fell from
+// 9.8 to 3.3 us, but on every shared-GPU rehearsal row the ring was level
+// or slower — 2-3 us per call at 256 KiB - 8 MiB, 2-4 % at 1 GiB
+// (profiles/r05k, r05n, r05o) — so a comm runs it only when asked
+// (VCCL_RING_WAVE=1 / vcclCommSetRingWave) until a run over xGMI, where
+// remote stores acknowledge slowly, says otherwise.
 #define VCCL_RING_WAVE_SYNC 0
 #endif
 

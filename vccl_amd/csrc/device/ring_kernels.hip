@@ -1,5 +1,6 @@
 // Collective kernels for ONE kernel element type (VCCL_KT) and ONE family
-// (VCCL_PART: 0 ring, 1 LL, 2 direct — separate objects, built in parallel):
+// (VCCL_PART: 0 ring, 1 LL, 2 direct, 3 LL128 ring, 4 ring with the per-wave
+// hand-off — separate objects, built in parallel):
 // per reduction functor the ring all-reduce / reduce-scatter / reduce (one workgroup
 // per channel, enqueue.cc:1576-1666), the one-shot LL and the direct
 // (two-shot all-reduce, one-hop reduce-scatter) kernels; in the K_U8 unit
@@ -8,7 +9,13 @@
 
 #include "dispatch.hpp"
 #include "ring_launch.hpp"
-#if VCCL_PART == 0 || VCCL_PART == 3
+#if VCCL_PART == 4
+// the per-wave slot hand-off in this object only (ring.hpp prim_ws); its
+// kernels carry kProtoSimpleWave, so no symbol clashes with PART 0's
+#undef VCCL_RING_WAVE_SYNC
+#define VCCL_RING_WAVE_SYNC 1
+#endif
+#if VCCL_PART == 0 || VCCL_PART == 3 || VCCL_PART == 4
 #include "ring.hpp"
 #elif VCCL_PART == 1
 #include "ll.hpp"
@@ -20,16 +27,21 @@
 #error "compile with -DVCCL_KT=<kernel element type>"
 #endif
 #ifndef VCCL_PART
-#error "compile with -DVCCL_PART=<0 ring | 1 LL | 2 direct | 3 LL128 ring>"
+#error "compile with -DVCCL_PART=<0 ring | 1 LL | 2 direct | 3 LL128 ring | 4 per-wave ring>"
 #endif
 
 namespace vccl {
 
-#if VCCL_PART == 0 || VCCL_PART == 3
-// PART 0: the SIMPLE ring; PART 3: the same schedules over LL128 FIFOs.
-constexpr int kPartProto = VCCL_PART == 3 ? kProtoLL128 : kProtoSimple;
+#if VCCL_PART == 0 || VCCL_PART == 3 || VCCL_PART == 4
+// PART 0: the SIMPLE ring; PART 3: the same schedules over LL128 FIFOs;
+// PART 4: the SIMPLE ring with the per-wave hand-off, for the bandwidth
+// kernels only (sum over f32 / f16 / bf16, the byte-copy all-gather and
+// broadcast; Makefile WAVE_KTS), chosen per comm (VCCL_RING_WAVE).
+constexpr int kPartProto = VCCL_PART == 3 ? kProtoLL128 : VCCL_PART == 4 ? kProtoSimpleWave : kProtoSimple;
 #if VCCL_PART == 3
 #define VCCL_RING_LAUNCH ring_launch_ll128
+#elif VCCL_PART == 4
+#define VCCL_RING_LAUNCH ring_launch_wave
 #else
 #define VCCL_RING_LAUNCH ring_launch
 #endif
@@ -119,9 +131,16 @@ hipError_t VCCL_RING_LAUNCH<VCCL_KT>(int coll, int devOp, const RingBatch& w, in
     }
     return hipErrorInvalidValue;
   }
+#if VCCL_PART == 4
+  if (devOp != OP_SUM) return hipErrorInvalidValue;  // ring_wave_kernel() never asks
+#endif
   dispatch_op<T>(devOp, [&]<class Fn>() {
     if constexpr (std::is_same<Fn, FnCopy<T>>::value) {
       err = hipErrorInvalidValue;
+#if VCCL_PART == 4
+    } else if constexpr (!std::is_same<Fn, FnSum<T>>::value || VCCL_KT == K_U8) {
+      err = hipErrorInvalidValue;
+#endif
     } else if (coll == kCollAllReduce) {
       err = launch_k(k_ring<kCollAllReduce, Fn, ring_unroll<Fn>(), kPartProto>, grid, block, stream, stop, w);
     } else if (coll == kCollReduceScatter) {

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include "coll_types.hpp"
+#include "dispatch.hpp"
 #include "ring_types.hpp"
 
 namespace vccl {
@@ -33,11 +34,21 @@ hipError_t ring_launch(int coll, int devOp, const RingBatch& w, int nthreads, hi
 template <int K>
 hipError_t ring_launch_ll128(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream,
                              hipEvent_t stop);
+// The SIMPLE ring with the per-wave slot hand-off (ring.hpp prim_ws): only
+// the bandwidth-regime kernels — sum over f32 / f16 / bf16 (all-reduce,
+// reduce-scatter, reduce) and the byte-copy all-gather / broadcast — see
+// ring_wave_kernel(); every other call takes ring_launch.
 template <int K>
-inline hipError_t ring_launch_any(bool ll128, int coll, int devOp, const RingBatch& w, int nthreads,
+hipError_t ring_launch_wave(int coll, int devOp, const RingBatch& w, int nthreads, hipStream_t stream,
+                            hipEvent_t stop);
+enum : int { kRingVariantSimple = 0, kRingVariantLL128 = 1, kRingVariantWave = 2 };
+template <int K>
+inline hipError_t ring_launch_any(int variant, int coll, int devOp, const RingBatch& w, int nthreads,
                                   hipStream_t stream, hipEvent_t stop) {
-  return ll128 ? ring_launch_ll128<K>(coll, devOp, w, nthreads, stream, stop)
-               : ring_launch<K>(coll, devOp, w, nthreads, stream, stop);
+  if (variant == kRingVariantLL128) return ring_launch_ll128<K>(coll, devOp, w, nthreads, stream, stop);
+  if constexpr (K == K_U8 || K == K_F32 || K == K_F16 || K == K_BF16)
+    if (variant == kRingVariantWave) return ring_launch_wave<K>(coll, devOp, w, nthreads, stream, stop);
+  return ring_launch<K>(coll, devOp, w, nthreads, stream, stop);
 }
 
 // One-hop LL collectives (ll.hpp): 256-thread workgroups, `grid` of them.

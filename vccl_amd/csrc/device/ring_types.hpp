@@ -209,8 +209,11 @@ struct RingWork {
   int root;                          // broadcast / reduce: the root's rank
 };
 
-// Protocols of the ring kernels (nccl_common.h ids).
-enum : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2 };
+// Protocols of the ring kernels (nccl_common.h ids).  kProtoSimpleWave is a
+// device-side tag only: the SIMPLE protocol (same FIFOs, partition and fold)
+// with the per-wave slot hand-off (ring.hpp prim_ws), built as its own
+// kernels (ring_kernels.hip PART 4) and chosen per comm at run time.
+enum : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2, kProtoSimpleWave = 3 };
 // LL128 wire format on gfx950 (ring.hpp ll128_prim): lines of L bytes, one
 // per L/16 lanes — every lane but the line's last carries a 16-byte data
 // piece, the last an 8-byte data piece and the 8-byte flag — so one wave

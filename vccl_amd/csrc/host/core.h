@@ -173,6 +173,8 @@ struct ncclComm {
   static constexpr int kMaxCaptures = 16;
   std::vector<CapOrder> caps;         // most recently used first
   uint64_t fusedLaunches = 0;         // group launches that carried > 1 collective
+  int ringWave = 0;                   // SIMPLE ring launches take the per-wave hand-off (VCCL_RING_WAVE)
+  uint64_t waveLaunches = 0;          // ring launches that ran the per-wave kernel
   // CTA (workgroup) bounds of every collective launch: ncclConfig_t
   // minCTAs / maxCTAs or NCCL_MIN_CTAS / NCCL_MAX_CTAS (init.cc:1478-1540)
   int minCTAs = 1, maxCTAs = 64;

@@ -782,8 +782,19 @@ static ncclResult_t ring_work_of(const Task& t, bool ll128, RingWork* out, int* 
   return ncclSuccess;
 }
 
+// The per-wave SIMPLE ring kernels exist for the bandwidth regime only
+// (ring_kernels.hip PART 4): sums over f32 / f16 / bf16 and the byte-copy
+// all-gather / broadcast.
+static bool ring_wave_kernel(int kt, int devOp, int coll) {
+  if (coll == kCollAllGather || coll == kCollBroadcast) return kt == K_U8;
+  return devOp == OP_SUM && (kt == K_F32 || kt == K_F16 || kt == K_BF16);
+}
+
 // 1 .. kRingMaxWorks ring calls of one comm with the same collective, kernel
-// type and op (fusable) in one launch on ts[0].stream; SIMPLE or LL128.
+// type and op (fusable) in one launch on ts[0].stream; SIMPLE or LL128.  A
+// SIMPLE launch takes the per-wave hand-off when the comm asks for it
+// (VCCL_RING_WAVE / vcclCommSetRingWave) and the kernel exists: same FIFOs,
+// partition and fold, so the two mix freely on a channel.
 static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128, hipEvent_t stop) {
   const Task& t = ts[0];
   ncclComm* comm = t.comm;
@@ -802,17 +813,20 @@ static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128, hipEvent
   }
   b.nParts = nTasks;
   const int coll = dev_coll(t.coll);
+  const int v = ll128 ? kRingVariantLL128
+                : comm->ringWave && ring_wave_kernel(kt, devOp, coll) ? kRingVariantWave : kRingVariantSimple;
+  if (v == kRingVariantWave) comm->waveLaunches++;
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
-    case K_U8: e = ring_launch_any<K_U8>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_U32: e = ring_launch_any<K_U32>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_U64: e = ring_launch_any<K_U64>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_F16: e = ring_launch_any<K_F16>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_F32: e = ring_launch_any<K_F32>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_F64: e = ring_launch_any<K_F64>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_BF16: e = ring_launch_any<K_BF16>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_F8E4M3: e = ring_launch_any<K_F8E4M3>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
-    case K_F8E5M2: e = ring_launch_any<K_F8E5M2>(ll128, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_U8: e = ring_launch_any<K_U8>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_U32: e = ring_launch_any<K_U32>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_U64: e = ring_launch_any<K_U64>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F16: e = ring_launch_any<K_F16>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F32: e = ring_launch_any<K_F32>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F64: e = ring_launch_any<K_F64>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_BF16: e = ring_launch_any<K_BF16>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F8E4M3: e = ring_launch_any<K_F8E4M3>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
+    case K_F8E5M2: e = ring_launch_any<K_F8E5M2>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
   }
   if (e != hipSuccess) {
     VWARN("ring kernel launch failed: %s", hipGetErrorString(e));

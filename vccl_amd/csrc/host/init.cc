@@ -599,9 +599,12 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   dc.useFences = (int)param_int("FENCES", 0);
   if (anyNet) dc.useFences = 1;  // slots and flags in host memory: full system-scope fences
   dc.pollMode = (int)param_int("POLL_MODE", 0);
-  // SIMPLE ring hand-off per slot size (ring.hpp prim_ws): per wave from a
-  // full default slot up (the bandwidth regime), as a workgroup below
-  // (latency-bound slots, profiles/r05k); 0 = always per wave
+  // The per-wave SIMPLE ring (ring_kernels.hip PART 4) for this comm's
+  // launches (VCCL_RING_WAVE=1 or vcclCommSetRingWave; default off: no gain
+  // on a shared GPU).  Inside it, slots below
+  // VCCL_RING_WAVE_MIN (a full default slot) still take the workgroup
+  // hand-off (latency-bound slots, profiles/r05k); 0 = always per wave.
+  c->ringWave = param_int("RING_WAVE", 0) != 0;
   dc.ringWaveMin = std::max<int64_t>(0, param_int("RING_WAVE_MIN", 512 << 10));
   // Opt-in slot timeline of the SIMPLE ring (vcclCommRingTrace)
   c->ringTraceCap = n > 1 ? (int)std::max<int64_t>(0, std::min<int64_t>(param_int("RING_TRACE", 0), 1 << 16)) : 0;
@@ -1138,6 +1141,17 @@ VCCL_EXPORT ncclResult_t vcclCommSetFences(ncclComm_t comm, int useFences) {
   HIPCHECK(hipMemcpy((char*)comm->devComm + offsetof(DevComm, useFences), &useFences, sizeof(int),
                      hipMemcpyHostToDevice));
   if (old >= 0) (void)hipSetDevice(old);
+  return ncclSuccess;
+}
+
+// vccl_ext.h: the SIMPLE ring's slot hand-off for later launches (host
+// only: the launcher picks the kernel; both leave the channel's FIFO state
+// identical, so no wait is needed).
+VCCL_EXPORT ncclResult_t vcclCommSetRingWave(ncclComm_t comm, int perWave, unsigned long long* waveLaunches) {
+  NCCLCHECK(comm_check(comm, "vcclCommSetRingWave"));
+  if (perWave != 0 && perWave != 1 && perWave != -1) return ncclInvalidArgument;
+  if (perWave >= 0) comm->ringWave = perWave;
+  if (waveLaunches) *waveLaunches = comm->waveLaunches;
   return ncclSuccess;
 }
 

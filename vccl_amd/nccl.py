@@ -40,7 +40,7 @@ EXPORTED = [
     "vcclReduceCopy", "vcclReduceCopyEx", "vcclHostToDevRedOp", "vcclKernelTypeOf",
     "vcclBuildInfo", "vcclBootstrapAllGather", "vcclCommCollAlgo", "vcclCommSetAlgo",
     "vcclCommLaunchStats", "vcclCommNetStats", "vcclCommSetFences", "vcclCommDebugSetEpochs",
-    "vcclCommRingTrace", "vcclCommGroupAlgos",
+    "vcclCommSetRingWave", "vcclCommRingTrace", "vcclCommGroupAlgos",
     "vcclRingPartition", "vcclRingChunkOf", "vcclRingOrders", "vcclGroupPlan", "vcclGroupPlanEx", "vcclAlgoSelection",
     # rooted rings, split and debug reload
     "ncclReduce", "ncclBcast", "ncclBroadcast", "ncclCommSplit", "ncclResetDebugInit",
@@ -134,6 +134,7 @@ def lib() -> ctypes.CDLL:
         "vcclKernelTypeOf": [c_int, c_int],
         "vcclBootstrapAllGather": [ctypes.POINTER(ncclUniqueId), c_int, c_int, vp, c_size],
         "vcclCommSetFences": [vp, c_int],
+        "vcclCommSetRingWave": [vp, c_int, ctypes.POINTER(ctypes.c_ulonglong)],
         "vcclRingPartition": [c_int, c_size, c_int, c_int, c_int, c_int, c_size, c_int,
                               ctypes.POINTER(ctypes.c_int64)],
         "vcclCommDebugSetEpochs": [vp, ctypes.c_uint32, ctypes.c_uint32],
@@ -443,6 +444,15 @@ class Comm:
     def set_fences(self, on: bool):
         """vcclCommSetFences: system-scope fences around every slot hand-off (VCCL_FENCES)."""
         check(lib().vcclCommSetFences(self.handle, int(bool(on))), "vcclCommSetFences")
+
+    def set_ring_wave(self, on: bool | None) -> int:
+        """vcclCommSetRingWave: the SIMPLE ring's per-wave slot hand-off for
+        later launches (VCCL_RING_WAVE; None leaves it); returns the ring
+        launches that ran the per-wave kernel so far."""
+        n = ctypes.c_ulonglong(0)
+        check(lib().vcclCommSetRingWave(self.handle, -1 if on is None else int(bool(on)), ctypes.byref(n)),
+              "vcclCommSetRingWave")
+        return int(n.value)
 
     def debug_set_epochs(self, ll_epoch: int, direct_epoch: int):
         """vcclCommDebugSetEpochs: overwrite the LL / direct call epochs (wrap tests)."""
