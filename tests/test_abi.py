@@ -69,6 +69,9 @@ def test_null_comm_queries():
     assert L.ncclCommCount(None, ctypes.byref(v)) == nccl.ncclInvalidArgument
     assert L.ncclCommDestroy(None) == nccl.ncclSuccess
     assert L.ncclAllReduce(None, None, 1, 7, 0, None, None) == nccl.ncclInvalidArgument
+    n = ctypes.c_ulonglong(7)
+    assert L.vcclCommSetRingWave(None, 1, ctypes.byref(n)) == nccl.ncclInvalidArgument and n.value == 7
+    assert L.vcclCommSetFences(None, 1) == nccl.ncclInvalidArgument
 
 
 def test_out_of_scope_calls_are_invalid_usage():
@@ -125,6 +128,9 @@ def test_group_with_failing_call_launches_nothing():
     L = nccl.lib()
     nccl.group_start()
     assert L.ncclAllReduce(None, None, 1, 7, 0, None, None) == nccl.ncclInvalidArgument
+    n = ctypes.c_ulonglong(7)
+    assert L.vcclCommSetRingWave(None, 1, ctypes.byref(n)) == nccl.ncclInvalidArgument and n.value == 7
+    assert L.vcclCommSetFences(None, 1) == nccl.ncclInvalidArgument
     assert L.ncclGroupEnd() == nccl.ncclInvalidArgument
     nccl.group_start()
     nccl.group_end()
