@@ -10,6 +10,7 @@ come from the CPU oracle's ring fold over OUR channel partition
 Spins are bounded (VCCL_SPIN_TIMEOUT_S) so a protocol bug fails the test
 instead of hanging the GPU.
 """
+import json
 import os
 import subprocess
 import sys
@@ -339,6 +340,35 @@ def _ring_ranks(n, geom):
             assert min(waves) > 0, waves
         elif env.get("VCCL_RING_WAVE", "0") == "0":
             assert max(waves) == 0, waves
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_ring_handoff_switch(n):
+    """vcclCommSetRingWave between calls of one comm (tests/mp_handoff_worker.py):
+    the SIMPLE ring's workgroup and per-wave hand-offs share FIFOs, step
+    counters, partition and fold, so f32 / f16 / bf16 sums, all-gather and
+    broadcast give bitwise the same outputs in a workgroup / per-wave /
+    workgroup sequence, the per-wave pass runs the per-wave kernel for
+    exactly its eligible calls, and an f32 prod (no per-wave kernel) keeps the
+    workgroup one."""
+    uid = nccl.get_unique_id()
+    hexid = nccl.unique_id_to_bytes(uid).hex()
+    env = dict(os.environ)
+    env.update(TEST_GEOM)
+    env.setdefault("VCCL_SPIN_TIMEOUT_S", "20")
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_handoff_worker.py"),
+                                   str(r), str(n), hexid, d], env=_mp.worker_env(env),
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        outs = [p.communicate(timeout=300)[0].decode(errors="replace")[-2000:] for p in procs]
+        res = []
+        for r in range(n):
+            path = os.path.join(d, f"rank{r}.json")
+            res.append(json.load(open(path)) if os.path.exists(path) else None)
+        assert [p.returncode for p in procs] == [0] * n, (res, "\n".join(outs))
+    for v in res:
+        assert all(v["equal"].values()), v
+        assert v["wave_launches_per_pass"] == [0, v["eligible"], 0], v
 
 
 def test_beyond_2gib_two_ranks():
@@ -722,7 +752,6 @@ def test_initall_single_process_worker():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mp_initall_worker.py"), arg],
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
-    import json
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["ok"], res
 
