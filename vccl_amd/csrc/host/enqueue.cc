@@ -815,7 +815,6 @@ static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128, hipEvent
   const int coll = dev_coll(t.coll);
   const int v = ll128 ? kRingVariantLL128
                 : comm->ringWave && ring_wave_kernel(kt, devOp, coll) ? kRingVariantWave : kRingVariantSimple;
-  if (v == kRingVariantWave) comm->waveLaunches++;
   hipError_t e = hipErrorInvalidValue;
   switch (kt) {
     case K_U8: e = ring_launch_any<K_U8>(v, coll, devOp, b, comm->nThreads, t.stream, stop); break;
@@ -832,6 +831,7 @@ static ncclResult_t launch_ring(const Task* ts, int nTasks, bool ll128, hipEvent
     VWARN("ring kernel launch failed: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
   }
+  if (v == kRingVariantWave) comm->waveLaunches++;
   return ncclSuccess;
 }
 
