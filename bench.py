@@ -533,6 +533,125 @@ def cpu_baseline(n_full, seconds=5.0):
             "cgroup_cpu_quota": q, "machine_cpus": topo["machine_cpus"]}
 
 
+def cpu_baseline_allreduce(S, world, seconds=5.0):
+    """Host-core baseline beside the N > 1 line (north_star):
+    one rank's share of the ring all-reduce of an S-byte f32 bucket over
+    `world` ranks done as host work by the oracle's C reduce-copy (oracle/
+    cpu_bench.c, -O3 -march=native on this host) — a world-source sum over
+    S / world bytes into the rank's shard (the reduce-scatter's reductions),
+    then a copy of the S gathered bytes (the all-gather) — on pinned, first-
+    touched host buffers, one bounded ~`seconds` sample on the cgroup quota's
+    worth of physical cores (every physical core when no quota is set),
+    checked bit-exactly.  `value` is in the line's unit: the busbw a rank
+    doing that work on these cores would reach, (S / t_pass) * 2(n-1)/n."""
+    from oracle import oracle as O
+    topo = host_topology()
+    q = topo["cgroup_cpu_quota"]
+    if q and 2 <= int(q) < len(topo["cpus"]):
+        cpus, which = _spread(topo["physical_cores"], int(q), topo["node_of"]), "quota_cores"
+    else:
+        cpus, which = topo["physical_cores"], "physical_cores"
+    m, ncopy = S // (4 * world), S // 4
+    r = O.cpu_bench_rank(m, world, ncopy, cpus, seconds, register=_host_register())
+    assert r["correct"], "cpu baseline mismatch"
+    busbw = S / r["s_per_pass"] * 2 * (world - 1) / world / 1e9
+    return {"value": round(busbw, 2), "unit": "GB/s", "cores": r["threads"], "kind": "port",
+            "sample": (f"one rank's share of a {world}-rank ring all-reduce of {S} B f32 as host work: "
+                       f"{world}-source sum over {m} elems + copy of {ncopy} elems, oracle/reduce_ref.c "
+                       f"-O3 -march={r['march']}, pinned={r['pinned']}: {r['iters']} passes in {r['s']} s "
+                       f"on {r['threads']} pinned threads ({which}); checked bit-exactly; value = "
+                       "(S / t_pass) * 2(n-1)/n, the line's busbw convention"),
+            "mem_GBs": r["mem_GB/s"], "s_per_pass": round(r["s_per_pass"], 5), "which": which,
+            "nproc": topo["nproc"], "physical_cores": len(topo["physical_cores"]),
+            "numa_nodes": topo["numa_nodes"], "cgroup_cpu_quota": q, "machine_cpus": topo["machine_cpus"]}
+
+
+def ring_link_peak(orders, nchannels, link_gbs=None):
+    """Per-rank busbw ceiling of the ring set a call runs on, one rank per GPU
+    over point-to-point xGMI: channel c runs on ring c mod R, so a rank's send
+    traffic T splits over the rings as their channel shares w_j / W, and a
+    directed arc (a -> b) carries T * (sum of w_j over the rings that use it)
+    / W <= one link per direction.  Peak T = L * W / (worst arc load).  2 ranks:
+    1 link; 4 ranks (all 6 directed cycles, every arc in 2): 3 links; 6 ranks (4
+    rings on 4 of 5 links): 4; odd n (Walecki, n - 1 arc-disjoint rings): n - 1;
+    8 ranks: 7.  Returns the peak and the links it amounts to."""
+    L = XGMI_LINK_GBS if link_gbs is None else link_gbs
+    R = len(orders)
+    w = [0] * R
+    for c in range(max(1, nchannels)):
+        w[c % R] += 1
+    W = sum(w)
+    load = {}
+    for j, ring in enumerate(orders):
+        if not w[j]:
+            continue
+        for k, a in enumerate(ring):
+            arc = (a, ring[(k + 1) % len(ring)])
+            load[arc] = load.get(arc, 0) + w[j]
+    worst = max(load.values())
+    out_links = max(len({b for (a, b) in load if a == r}) for r in orders[0])
+    return {"peak": L * W / worst, "links": round(W / worst, 4), "links_used_per_rank": out_links,
+            "rings": R, "channels": W, "worst_arc_share": round(worst / W, 4)}
+
+
+def ring_ar_hbm_bytes(world, S):
+    """HBM bytes one rank's ring all-reduce of S bytes moves:
+    in units of S/n, send S->F (1 read, 1 write), n-2 x S+F->F (2, 1),
+    S+F->F+O (2, 2), n-2 x F->F+O (1, 2), F->O (1, 1): (3n-2) reads and (3n-2)
+    writes, 2(3n-2) S / n in all (4 S at n = 2).  FIFO writes land in the next
+    rank's HBM, so every device moves the same total."""
+    return 2 * (3 * world - 2) * S / world
+
+
+def allreduce_roofline(busbw, t_s, S, world, ranks_per_device, algo, orders, nchannels, measured_link=None):
+    """The N > 1 line's roofline.  One rank per GPU: the xGMI bound of the
+    ring set in use (ring_link_peak).  Ranks sharing a device (the rehearsals):
+    no byte crosses a link, so the bound is that device's HBM — every sharing
+    rank's ring_ar_hbm_bytes per call over the call's time — and frac <= 1."""
+    if ranks_per_device > 1:
+        if algo != "ring":
+            return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                    "traffic": None, "note": f"ranks share a device; HBM bytes modelled for the ring only ({algo} ran)"}
+        ach = ranks_per_device * ring_ar_hbm_bytes(world, S) / t_s / 1e9
+        return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "note": (f"{ranks_per_device} ranks share each device, so no byte crosses xGMI: the bound is the "
+                         f"device's HBM, {ranks_per_device} x 2(3n-2)S/n B per call (the ring's HBM bytes per "
+                         "rank, DESIGN.md §4.2) / t")}
+    lp = ring_link_peak(orders, nchannels)
+    return {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(lp["peak"], 2), "unit": "GB/s",
+            "frac": round(busbw / lp["peak"], 4), "traffic": None,
+            "note": (f"per-rank busbw vs the ring set's link ceiling: {lp['links']} link(s) x {XGMI_LINK_GBS} "
+                     f"GB/s per link and direction ({lp['rings']} rings on {lp['channels']} channels, "
+                     f"worst arc share {lp['worst_arc_share']}; MI355X spec 153.6 GB/s per link, bidirectional)"),
+            "links": lp["links"], "links_used_per_rank": lp["links_used_per_rank"],
+            "frac_of_measured_copy": (round(busbw / (lp["links"] * measured_link), 4) if measured_link else None)}
+
+
+def line_roofline_and_baseline(dist, rank, world, last, visible, ring_orders, n_channels, xgmi,
+                               cpu=True, cpu_seconds=5.0):
+    """The N > 1 line's `roofline` and `cpu_baseline`: the
+    host-core baseline of the headline bucket runs after every timed region,
+    on rank 0 while the other ranks wait at the barrier; the roofline switches
+    to the device's HBM when ranks share one (ranks_per_device > 1).  Returns
+    (ranks_per_device, roofline, cpu_baseline or None)."""
+    cpu_base = None
+    if cpu:
+        if rank == 0:
+            try:
+                cpu_base = cpu_baseline_allreduce(last["bytes"], world, cpu_seconds)
+            except Exception as e:  # noqa: BLE001 - a failed baseline is reported, not fatal
+                cpu_base = {"value": None, "error": repr(e)}
+        dist.barrier()
+    rpd = -(-world // max(1, visible))
+    measured_link = (xgmi or {}).get("one_peer_GBs")
+    roof = allreduce_roofline(last["busbw"], last["us"] / 1e6, last["bytes"], world, rpd, last["algo"],
+                              ring_orders, n_channels, measured_link)
+    if rpd == 1:
+        roof["measured_peer_copy"] = xgmi
+    return rpd, roof, cpu_base
+
+
 def _dist_setup():
     import torch.distributed as dist
     rank = int(os.environ["RANK"])
@@ -981,6 +1100,7 @@ def bench_allreduce(args):
                                                                         "algo": algo})
     checks = run_checks(dist, comm, rank, world, plan)
     err = comm.async_error()
+    n_channels, ring_orders = comm.n_channels(), nccl.ring_orders(world)
     comm.destroy()
     initall = None
     if not args.no_initall and world > 1 and torch.cuda.device_count() > 1:
@@ -988,11 +1108,10 @@ def bench_allreduce(args):
         initall = initall_check(torch.cuda.device_count()) if rank == 0 else None
         dist.barrier()
     t_chk = time.perf_counter() - t_chk
-    line_s = time.perf_counter() - _T_START
     last = rows[-1]
-    links = {2: 1, 4: 3, 8: 7}.get(world, 1)
-    peak = links * XGMI_LINK_GBS  # spec, per link and direction (not a measurement)
-    measured_link = (xgmi or {}).get("one_peer_GBs")
+    rpd, roof, cpu_base = line_roofline_and_baseline(dist, rank, world, last, torch.cuda.device_count(),
+                                                     ring_orders, n_channels, xgmi, cpu=not args.no_cpu)
+    line_s = time.perf_counter() - _T_START
     correct_all = _flatten_ok(checks) and (initall is None or initall.get("ok") is True)
     out = {"metric": "device reduce-copy GB/s vs HBM peak; all-reduce busbw at 1/2/4/8 GPUs",
            "value": round(last["busbw"], 2), "unit": "GB/s", "n_gpus": world,
@@ -1008,15 +1127,10 @@ def bench_allreduce(args):
                       "algbw": round(last["algbw"], 2), "parallelism": f"{last['algo']} x{world}",
                       "async_error": err, "correct": correct_all,
                       "launcher": os.environ.get("VCCL_BENCH_LAUNCHER", "torch.distributed.run"),
-                      "devices": {"visible": torch.cuda.device_count(),
-                                  "ranks_per_device": -(-world // max(1, torch.cuda.device_count()))}},
-           "roofline": {"bound": "xgmi", "achieved": round(last["busbw"], 2), "peak": round(peak, 2),
-                        "unit": "GB/s", "frac": round(last["busbw"] / peak, 4), "traffic": None,
-                        "note": (f"per-rank busbw vs {links} link(s) x {XGMI_LINK_GBS} GB/s per link and "
-                                 "direction (MI355X spec 153.6 GB/s per link, bidirectional)"),
-                        "measured_peer_copy": xgmi,
-                        "frac_of_measured_copy": (round(last["busbw"] / (links * measured_link), 4)
-                                                  if measured_link else None)},
+                      "devices": {"visible": torch.cuda.device_count(), "ranks_per_device": rpd},
+                      "channels": n_channels, "rings": len(ring_orders)},
+           "roofline": roof,
+           "cpu_baseline": cpu_base,
            "correct": {"all": correct_all, **checks, "initall_single_process": initall,
                        "check_s": round(t_chk, 2), "check_warmup_s": round(check_warmup_s, 3),
                        "line_s": round(line_s, 2),  # bench.py start (imports included) -> here

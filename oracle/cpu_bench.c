@@ -1,21 +1,24 @@
-/* ORACLE — test infrastructure only (bench.py's cpu_baseline leg; never on
+/* ORACLE — test infrastructure only (bench.py's cpu_baseline legs; never on
  * the product path).
  *
- * Host-core baseline of BASELINE config 2's shape (2-src f32 sum, dst =
- * a + b) run by the oracle's own reduce-copy (ref_reduce_copy, reduce_ref.c)
- * on persistent worker threads, each pinned to one CPU of the caller's list
- * and owning one page-aligned slice of every buffer:
- *   ref_cpu_bench_alloc  mmap the three buffers (page size chosen so no page
- *                        is shared by two workers' slices) and let
- *                        each pinned worker FIRST-TOUCH its own slices, so on
- *                        a multi-socket host every slice lives on the NUMA
- *                        node of the core that reduces it (the caller may pin
- *                        the pages afterwards with hipHostRegister, which
- *                        keeps them where they are);
- *   ref_cpu_bench_run    the same workers loop reduce-copies over their
- *                        slices for `seconds`, one barrier per pass, then
- *                        check their slices bit-exactly;
- *   ref_cpu_bench_free   munmap.
+ * Host-core baselines run by the oracle's own reduce-copy (ref_reduce_copy,
+ * reduce_ref.c) on persistent worker threads, each pinned to one CPU of the
+ * caller's list and owning one page-aligned slice of every buffer:
+ *   - config 2's shape (2-src f32 sum, d = a + b): ref_cpu_bench_{alloc,run,free};
+ *   - one rank's share of a ring all-reduce of S bytes over n ranks, as host
+ *     work (ref_cpu_bench_rank_*): an n-source f32 sum over m = S / (4 n)
+ *     elements into the rank's shard (the reduce-scatter's reductions), then a
+ *     copy of the S gathered bytes (the all-gather); `ncopy` = 0 drops the copy.
+ * Both shapes:
+ *   alloc  mmap the buffers (page size chosen so no page is shared by two
+ *          workers' slices) and let each pinned worker FIRST-TOUCH its own
+ *          slices, so on a multi-socket host every slice lives on the NUMA
+ *          node of the core that works on it (the caller may pin the pages
+ *          afterwards with hipHostRegister, which keeps them where they are);
+ *   run    the same workers loop passes over their slices for `seconds`, one
+ *          barrier per pass, then check their slices bit-exactly (the sum in
+ *          the reduce-copy's left-to-right fold order, the copy byte for byte);
+ *   free   munmap.
  * Thread creation stays outside the timed region (a pthread_create per call
  * and thread would cost ~ms per pass at hundreds of threads).
  */
@@ -31,11 +34,14 @@
 #include "reduce_ref.h"
 
 #define MAXT 1024
+#define MAXSRC 16
 
 typedef struct {
-  float *a, *b, *d;
-  size_t lo, hi;
-  int cpu;
+  float** bufs; /* [0, nsrc) sources, nsrc dst, nsrc+1 copy src, nsrc+2 copy dst */
+  int nsrc;
+  size_t lo, hi;   /* reduce slice */
+  size_t clo, chi; /* copy slice */
+  int cpu, leader;
   int mode; /* 0 first touch + fill, 1 timed loop, 2 check */
   double seconds;
   pthread_barrier_t* bar;
@@ -54,7 +60,7 @@ static double now_s(void) {
 /* Deterministic uniform[-1, 1) value of element i of buffer `which`
  * (splitmix64, exactly representable in f32: 24-bit fractions). */
 static float val_at(size_t i, int which) {
-  uint64_t z = (uint64_t)i * 2 + (uint64_t)which + 0x9E3779B97F4A7C15ull;
+  uint64_t z = (uint64_t)i * MAXSRC + (uint64_t)which + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   z ^= z >> 31;
@@ -72,30 +78,46 @@ static void pin_to(int cpu) {
 static void* worker(void* arg) {
   worker_t* w = (worker_t*)arg;
   pin_to(w->cpu);
+  float** B = w->bufs;
+  const int ns = w->nsrc;
+  float* d = B[ns];
+  float *cs = B[ns + 1], *cd = B[ns + 2];
   if (w->mode == 0) {
-    for (size_t i = w->lo; i < w->hi; i++) {
-      w->a[i] = val_at(i, 0);
-      w->b[i] = val_at(i, 1);
-      w->d[i] = 0.0f;
+    for (int s = 0; s < ns; s++)
+      for (size_t i = w->lo; i < w->hi; i++) B[s][i] = val_at(i, s);
+    for (size_t i = w->lo; i < w->hi; i++) d[i] = 0.0f;
+    for (size_t i = w->clo; i < w->chi; i++) {
+      cs[i] = val_at(i, MAXSRC - 1);
+      cd[i] = 0.0f;
     }
     return NULL;
   }
   if (w->mode == 2) {
     int ok = 1;
-    for (size_t i = w->lo; i < w->hi && ok; i++) ok = w->d[i] == w->a[i] + w->b[i];
+    for (size_t i = w->lo; i < w->hi && ok; i++) {
+      float acc = B[0][i];
+      for (int s = 1; s < ns; s++) acc = acc + B[s][i];
+      ok = memcmp(&acc, &d[i], sizeof(float)) == 0;
+    }
+    if (ok && w->chi > w->clo) ok = memcmp(cs + w->clo, cd + w->clo, (w->chi - w->clo) * sizeof(float)) == 0;
     w->ok = ok;
     return NULL;
   }
-  const void* srcs[2] = {w->a + w->lo, w->b + w->lo};
-  void* dsts[1] = {w->d + w->lo};
+  const void* srcs[MAXSRC];
+  for (int s = 0; s < ns; s++) srcs[s] = B[s] + w->lo;
+  void* dsts[1] = {d + w->lo};
+  const void* csrc[1] = {cs + w->clo};
+  void* cdst[1] = {cd + w->clo};
   const double t0 = now_s();
   long it = 0;
   for (;;) {
     if (w->hi > w->lo)
-      ref_reduce_copy(0, 7 /* ncclFloat32 */, 0, NULL, 0, 0, 2, srcs, 1, dsts, w->hi - w->lo, 1);
+      ref_reduce_copy(0, 7 /* ncclFloat32 */, 0, NULL, 0, 0, ns, srcs, 1, dsts, w->hi - w->lo, 1);
+    if (w->chi > w->clo)  /* the gather: a one-source reduce-copy is a copy */
+      ref_reduce_copy(0, 7, 0, NULL, 0, 0, 1, csrc, 1, cdst, w->chi - w->clo, 1);
     it++;
     /* thread 0 decides when to stop; everyone sees the same decision */
-    if (w->lo == 0 && now_s() - t0 >= w->seconds) *w->stop = 1;
+    if (w->leader && now_s() - t0 >= w->seconds) *w->stop = 1;
     pthread_barrier_wait(w->bar);
     const int stop = *w->stop;
     pthread_barrier_wait(w->bar);
@@ -118,7 +140,14 @@ static size_t slice_elems(size_t n, int nthreads, int* huge) {
   return (raw + g - 1) / g * g;
 }
 
-static int run_workers(float* a, float* b, float* d, size_t n, int nthreads, const int* cpus,
+static void slice(size_t n, int nthreads, int t, size_t* lo, size_t* hi) {
+  const size_t per = slice_elems(n, nthreads, NULL);
+  *lo = per * t < n ? per * t : n;
+  *hi = per * (t + 1) < n ? per * (t + 1) : n;
+  if (t == 0) *lo = 0;
+}
+
+static int run_workers(float** bufs, int nsrc, size_t m, size_t ncopy, int nthreads, const int* cpus,
                        int mode, double seconds, long* iters, double* elapsed) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > MAXT) nthreads = MAXT;
@@ -127,15 +156,15 @@ static int run_workers(float* a, float* b, float* d, size_t n, int nthreads, con
   pthread_barrier_t bar;
   volatile int stop = 0;
   pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
-  const size_t per = slice_elems(n, nthreads, NULL);
   for (int t = 0; t < nthreads; t++) {
     worker_t* w = &ws[t];
     memset(w, 0, sizeof(*w));
-    w->a = a; w->b = b; w->d = d;
-    w->lo = per * t < n ? per * t : n;
-    w->hi = per * (t + 1) < n ? per * (t + 1) : n;
-    if (t == 0) w->lo = 0;
+    w->bufs = bufs;
+    w->nsrc = nsrc;
+    slice(m, nthreads, t, &w->lo, &w->hi);
+    slice(ncopy, nthreads, t, &w->clo, &w->chi);
     w->cpu = cpus ? cpus[t] : -1;
+    w->leader = t == 0;
     w->mode = mode;
     w->seconds = seconds;
     w->bar = &bar;
@@ -153,33 +182,64 @@ static int run_workers(float* a, float* b, float* d, size_t n, int nthreads, con
   return ok;
 }
 
-int ref_cpu_bench_alloc(size_t n, int nthreads, const int* cpus, void** a, void** b, void** d) {
-  const size_t bytes = (n * 4 + 4095) / 4096 * 4096;
-  void* p[3];
-  for (int i = 0; i < 3; i++) {
-    p[i] = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (p[i] == MAP_FAILED) return -1;
-    int huge;
-    slice_elems(n, nthreads, &huge);
-    madvise(p[i], bytes, huge ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
+static size_t map_bytes(size_t n) { return (n * 4 + 4095) / 4096 * 4096; }
+
+static void* map_buf(size_t n, int nthreads) {
+  if (n == 0) return NULL;
+  void* p = mmap(NULL, map_bytes(n), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return NULL;
+  int huge;
+  slice_elems(n, nthreads, &huge);
+  madvise(p, map_bytes(n), huge ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
+  return p;
+}
+
+void ref_cpu_bench_rank_free(void** bufs, size_t m, int nsrc, size_t ncopy) {
+  for (int i = 0; i < nsrc + 3; i++) {
+    if (!bufs[i]) continue;
+    munmap(bufs[i], map_bytes(i <= nsrc ? m : ncopy));
+    bufs[i] = NULL;
   }
-  run_workers((float*)p[0], (float*)p[1], (float*)p[2], n, nthreads, cpus, 0, 0, NULL, NULL);
-  *a = p[0];
-  *b = p[1];
-  *d = p[2];
+}
+
+int ref_cpu_bench_rank_alloc(size_t m, int nsrc, size_t ncopy, int nthreads, const int* cpus, void** bufs) {
+  if (nsrc < 1 || nsrc > MAXSRC || m == 0) return -1;
+  for (int i = 0; i < nsrc + 3; i++) bufs[i] = NULL;
+  for (int i = 0; i < nsrc + 3; i++) {
+    const size_t n = i <= nsrc ? m : ncopy;
+    if (n && !(bufs[i] = map_buf(n, nthreads))) {
+      ref_cpu_bench_rank_free(bufs, m, nsrc, ncopy);
+      return -1;
+    }
+  }
+  run_workers((float**)bufs, nsrc, m, ncopy, nthreads, cpus, 0, 0, NULL, NULL);
   return 0;
 }
 
 /* Returns 1 when every slice checks bit-exactly after the timed loop. */
+int ref_cpu_bench_rank_run(void** bufs, size_t m, int nsrc, size_t ncopy, int nthreads, const int* cpus,
+                           double seconds, long* iters, double* elapsed) {
+  run_workers((float**)bufs, nsrc, m, ncopy, nthreads, cpus, 1, seconds, iters, elapsed);
+  return run_workers((float**)bufs, nsrc, m, ncopy, nthreads, cpus, 2, 0, NULL, NULL);
+}
+
+/* Config 2's shape: the rank shape with two sources and no copy. */
+int ref_cpu_bench_alloc(size_t n, int nthreads, const int* cpus, void** a, void** b, void** d) {
+  void* bufs[5];
+  if (ref_cpu_bench_rank_alloc(n, 2, 0, nthreads, cpus, bufs) != 0) return -1;
+  *a = bufs[0];
+  *b = bufs[1];
+  *d = bufs[2];
+  return 0;
+}
+
 int ref_cpu_bench_run(void* a, void* b, void* d, size_t n, int nthreads, const int* cpus,
                       double seconds, long* iters, double* elapsed) {
-  run_workers((float*)a, (float*)b, (float*)d, n, nthreads, cpus, 1, seconds, iters, elapsed);
-  return run_workers((float*)a, (float*)b, (float*)d, n, nthreads, cpus, 2, 0, NULL, NULL);
+  void* bufs[5] = {a, b, d, NULL, NULL};
+  return ref_cpu_bench_rank_run(bufs, n, 2, 0, nthreads, cpus, seconds, iters, elapsed);
 }
 
 void ref_cpu_bench_free(void* a, void* b, void* d, size_t n) {
-  const size_t bytes = (n * 4 + 4095) / 4096 * 4096;
-  munmap(a, bytes);
-  munmap(b, bytes);
-  munmap(d, bytes);
+  void* bufs[5] = {a, b, d, NULL, NULL};
+  ref_cpu_bench_rank_free(bufs, n, 2, 0);
 }

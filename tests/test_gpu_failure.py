@@ -82,3 +82,33 @@ def test_abort_from_second_thread_ends_spinning_kernel(wave):
     assert v["ok"], (v, logs)
     assert v["kernel_end_s"] < 20 and v["abort_s"] < 15
     assert res[0]["usable_after"], (res[0], logs)
+
+
+@pytest.mark.parametrize("no_mark,launch_event", [("0", "1"), ("1", "1"), ("1", "0")])
+def test_destroy_right_after_launch(no_mark, launch_event):
+    """ncclCommDestroy straight after a launch waits for it in
+    every ordering mode — also under VCCL_DEBUG_NO_MARK=1, where no marker is
+    recorded (the kernel's bound stop event, or with VCCL_LAUNCH_EVENT=0 the
+    stream itself, tracks the launch) — so the FIFOs are never freed under a
+    running kernel and the output is exact."""
+    n = 2
+    env = _mp.worker_env(os.environ)
+    env.update(VCCL_DEBUG_NO_MARK=no_mark, VCCL_LAUNCH_EVENT=launch_event)
+    uid = nccl.unique_id_to_bytes(nccl.get_unique_id()).hex()
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mp_destroy_worker.py"),
+                                   str(r), str(n), d, uid], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        logs = []
+        for p in procs:
+            try:
+                logs.append(p.communicate(timeout=180)[0].decode(errors="replace")[-3000:])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(logs)
+        for r in range(n):
+            with open(os.path.join(d, f"rank{r}.json")) as f:
+                v = json.load(f)
+            assert v["idle_after_destroy"] and v["exact"], (v, logs)

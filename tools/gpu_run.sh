@@ -17,6 +17,8 @@
 #        lat:<n>   tools/coll_latency.py on n ranks sharing the GPU (LAT_* env)
 #        mprof:<n> the N>1 bench line on n ranks sharing the GPU, every rank
 #                  under rocprofv3 --kernel-trace --stats (tools/mp_prof.py)
+#        fence:<n> tools/fence_cost.py on n ranks (fences off / on, interleaved)
+#        lll:<n>[q<k>]  tools/ll_latency.py on n ranks, GPU_MAX_HW_QUEUES=k (4)
 # Outputs go to gpurun_out/<label>/.  Every GPU step has its own time limit
 # and the chain stops at the first failure (no retries).
 set -e
@@ -42,6 +44,8 @@ for s in "$@"; do
     pmc) timeout -k 10 400 python -u tools/pmc_traffic.py > $O/pmc_traffic.log 2>&1 && cp gpurun_out/pmc_traffic.json $O/ ;;
     lat:*) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#lat:} --master-addr 127.0.0.1 --master-port 29534 tools/coll_latency.py > $O/lat_n${s#lat:}.log 2> $O/lat_n${s#lat:}.err ;;
     mprof:*) timeout -k 10 600 python -u tools/mp_prof.py ${s#mprof:} $O/mprof_n${s#mprof:} --steps 5 --warmup 2 > $O/mprof_n${s#mprof:}.log 2>&1 ;;
+    fence:*) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#fence:} --master-addr 127.0.0.1 --master-port 29536 tools/fence_cost.py > $O/fence_n${s#fence:}.json 2> $O/fence_n${s#fence:}.err ;;
+    lll:*) n=${s#lll:}; q=${n#*q}; n=${n%q*}; [ "$q" = "$n" ] && q=4; GPU_MAX_HW_QUEUES=$q timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29537 tools/ll_latency.py > $O/lll_n${n}_q${q}.json 2> $O/lll_n${n}_q${q}.err ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

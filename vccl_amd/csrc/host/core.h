@@ -159,6 +159,9 @@ struct ncclComm {
   hipEvent_t joinEvent = nullptr;     // joins other streams into a fused group launch
   hipStream_t lastStream = nullptr;
   bool hasLastLaunch = false;         // lastLaunch/lastStream are valid
+  // VCCL_DEBUG_NO_MARK=1 with no stop event bound: the last launch left no
+  // event, so waiting for the comm's work polls lastStream instead
+  bool lastUnmarked = false;
   // the same ordering inside each stream capture, keyed by capture id (two
   // captures on one comm may interleave): events recorded in the
   // graph, a small pool reused least-recently-used first (never destroyed

@@ -305,11 +305,14 @@ static ncclResult_t stream_mark(ncclComm* comm, hipStream_t s, const CaptureStat
     c->has = true;
     return ncclSuccess;
   }
-  // VCCL_DEBUG_NO_MARK=1: no ordering event (measurement only: correct for
-  // a comm driven from ONE stream, where stream order suffices)
+  // VCCL_DEBUG_NO_MARK=1: no marker packet (measurement only: correct for a
+  // comm driven from ONE stream, where stream order suffices).  The launch is
+  // still tracked: through the stop event when the kernel bound
+  // it, else by its stream, so destroy / finalize / abort still wait for it.
   static const bool noMark = param_int("DEBUG_NO_MARK", 0) != 0;
-  if (noMark) return ncclSuccess;
-  if (!stop_event(comm, cs)) HIPCHECK(hipEventRecord(comm->lastLaunch, s));  // else bound to the kernel
+  const bool bound = stop_event(comm, cs) != nullptr;
+  if (!noMark && !bound) HIPCHECK(hipEventRecord(comm->lastLaunch, s));  // else bound to the kernel
+  comm->lastUnmarked = noMark && !bound;
   comm->lastStream = s;
   comm->hasLastLaunch = true;
   return ncclSuccess;
@@ -1137,6 +1140,7 @@ static ncclResult_t launch_runs(const std::vector<std::vector<Task>>& runs, cons
     // it even though a later run of this sequence failed
     comm->lastStream = s0;
     comm->hasLastLaunch = true;
+    comm->lastUnmarked = false;
   }
   const hipEvent_t done = stream_last_event(comm, cs);
   for (hipStream_t s : others)

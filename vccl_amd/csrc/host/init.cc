@@ -824,7 +824,9 @@ static bool wait_own_launches(ncclComm* c, double timeoutS) {
   if (!c->hasLastLaunch || !c->lastLaunch) return true;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    const hipError_t e = hipEventQuery(c->lastLaunch);
+    // an unmarked launch (VCCL_DEBUG_NO_MARK without a bound stop event) is
+    // done once its stream has drained
+    const hipError_t e = c->lastUnmarked ? hipStreamQuery(c->lastStream) : hipEventQuery(c->lastLaunch);
     if (e != hipErrorNotReady) return true;  // done (or the event is unusable: nothing to wait for)
     if (timeoutS >= 0 &&
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeoutS)
