@@ -112,3 +112,47 @@ def test_destroy_right_after_launch(no_mark, launch_event):
             with open(os.path.join(d, f"rank{r}.json")) as f:
                 v = json.load(f)
             assert v["idle_after_destroy"] and v["exact"], (v, logs)
+
+
+def test_net_short_slot_is_an_error():
+    """a net slot whose landed byte count is not its step's
+    slice (VCCL_DEBUG_NET_SHORT_SLOT makes rank 0's proxy ship its first
+    slot of >= 64 KiB 16 bytes short, as the stale size of round 5 did) ends
+    the call with an error from ncclCommGetAsyncError on every rank —
+    ncclInternalError where the short slot landed (ring.hpp recv_size_ok),
+    ncclRemoteError where a rank then waits on it — never a silent result;
+    the small call before it (slots below the hook's size) is exact."""
+    n = 2
+    env = _mp.worker_env(os.environ)
+    env.update(VCCL_NET_FORCE="1", VCCL_NET_NCHANNELS="2", VCCL_SPIN_TIMEOUT_S="3")
+    uid = nccl.unique_id_to_bytes(nccl.get_unique_id()).hex()
+    with tempfile.TemporaryDirectory() as d:
+        procs = []
+        for r in range(n):
+            e = dict(env)
+            if r == 0:
+                e["VCCL_DEBUG_NET_SHORT_SLOT"] = str(64 << 10)
+            procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mp_net_guard_worker.py"),
+                                           str(r), str(n), d, uid], env=e,
+                                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        logs = []
+        for p in procs:
+            try:
+                logs.append(p.communicate(timeout=180)[0].decode(errors="replace")[-3000:])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(logs)
+        res = []
+        for r in range(n):
+            with open(os.path.join(d, f"rank{r}.json")) as f:
+                res.append(json.load(f))
+    for v in res:
+        assert v["first_exact"], (v, logs)
+        assert int(v["net_stats"][2]) == 2 * 2, v  # every ring connection through the proxy
+        assert v["async_error"] in (nccl.ncclInternalError, nccl.ncclRemoteError), (v, logs)
+        assert v["kernel_end_s"] < 30, v
+    # rank 1 receives rank 0's short slot and refuses it
+    assert res[1]["async_error"] == nccl.ncclInternalError, (res, logs)
+    assert "slice length" in res[1]["last_error"], res[1]

@@ -127,6 +127,7 @@ struct RingCtx {
   uint64_t* nextRecvTail;
   uint64_t* prevSendHead;
   uint32_t* sendSizes;
+  const uint32_t* recvSizes;
   char* ll128Recv;
   char* ll128Send;
   int ringPos;
@@ -185,6 +186,7 @@ struct RingCtx {
     nextRecvTail = c->nextRecvTail;
     prevSendHead = c->prevSendHead;
     sendSizes = c->sendSizes;
+    recvSizes = c->recvSizes;
     ll128Recv = c->ll128Recv;
     ll128Send = c->ll128Send;
     ringPos = c->ringPos;
@@ -199,6 +201,18 @@ struct RingCtx {
     pollMode = m->pollMode;
     traceCap = m->traceCap;
     waveMin = m->ringWaveMin;
+  }
+
+  // Net slots only (recvSizes set): the bytes the proxy landed for receive
+  // step `step` must be the slice this prim computes — the sender's sendOff +
+  // nelem * sizeof(T) for the same step.  A short or stale slot raises
+  // kErrSlotSize (ncclInternalError) instead of being reduced.
+  __device__ bool recv_size_ok(uint64_t step, uint32_t expect) {
+    const uint32_t got = __hip_atomic_load((VCCL_GLOBAL uint32_t*)(recvSizes + step % kSteps), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (got == expect) return true;
+    __hip_atomic_store(errorFlag, kErrSlotSize, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return false;
   }
 
   __device__ bool aborted() const { return __hip_atomic_load(shAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; }
@@ -417,6 +431,14 @@ struct RingCtx {
       complete_pending<0>();  // never hold a post while waiting on a peer
       if (!(useFences ? poll_credits<RECV>(needTail, needHead) : wait_credits<RECV>(needTail, needHead))) return;
     }
+    if (RECV && recvSizes) {  // a net slot: the landed bytes must be this slice
+      int ok = 1;
+      if (lane == 0) ok = recv_size_ok(recvStep, (uint32_t)(nelem > 0 ? recvOff + nelem * (int64_t)sizeof(T) : 0));
+      if (!__builtin_amdgcn_readfirstlane(ok)) {
+        set_aborted();
+        return;
+      }
+    }
     const uint64_t t1 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
     constexpr int NS = (SRC ? 1 : 0) + (RECV ? 1 : 0);
     constexpr int ND = (SEND ? 1 : 0) + (DST ? 1 : 0);
@@ -506,6 +528,8 @@ struct RingCtx {
       bool ok = true;
       if (RECV) ok = spin_ge(recvTail, recvStep + 1);
       if (SEND && ok && sendStep + 1 > (uint64_t)kSteps) ok = spin_ge(sendHead, sendStep + 1 - kSteps);
+      if (RECV && ok && recvSizes)  // a net slot: the landed bytes must be this slice
+        ok = recv_size_ok(recvStep, (uint32_t)(nelem > 0 ? recvOff + nelem * (int64_t)sizeof(typename Fn::EltType) : 0));
       if (!ok) set_aborted();
       if (useFences) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire

@@ -39,6 +39,15 @@ constexpr int kOrderMaxRanks = 8;
 constexpr int kSlotPad = 64;
 __host__ __device__ constexpr int64_t slot_stride(int slotBytes) { return (int64_t)slotBytes + kSlotPad; }
 
+// Values of the comm's error word (DevComm::errorFlag): a spin without
+// progress (a lost peer, ncclRemoteError), or a net slot whose landed byte
+// count is not the step's slice length (ncclInternalError).
+constexpr int kErrSpinTimeout = 1;
+constexpr int kErrSlotSize = 2;
+// Net slot size word before the GPU writes it / after the proxy shipped the
+// slot (the reference's -1, src/transport/net.cc:1250-1255, 1365-1367).
+constexpr uint32_t kNetSizeUnset = 0xffffffffu;
+
 struct DevChannel {
   // ring order: ringRanks[k] = rank at ring position (myPos + k) mod n
   // (userRanks rotated to self, init.cc:599-615)
@@ -56,6 +65,11 @@ struct DevChannel {
   // Net connection only (null over xGMI): bytes of each posted slot, stored
   // before the tail so the proxy sends only what the step filled.
   uint32_t* sendSizes;
+  // Net connection only: bytes the proxy landed in each slot (written before
+  // recvTail); the ring kernel checks them against the slice length it
+  // computes itself (ring.hpp recv_size_ok) and raises kErrSlotSize on a
+  // mismatch instead of reducing a short or stale slot.
+  const uint32_t* recvSizes;
   // LL128 FIFOs (ring.hpp prim_ll128): kSteps slots of 64-byte lines, local
   // (receive) and next's (send); null when the comm has no LL128 buffers.
   // Steps, credits (sendHead / prevSendHead) and the slot index are shared
@@ -72,7 +86,7 @@ struct DevComm {
   int nChannels;
   int slotBytes;                     // bytes per FIFO slot
   volatile int* abortFlag;           // host-pinned, mapped (ncclCommAbort)
-  int* errorFlag;                    // host-pinned, mapped: 1 = spin timeout
+  int* errorFlag;                    // host-pinned, mapped: kErrSpinTimeout / kErrSlotSize
   uint64_t spinTimeoutTicks;         // s_memrealtime ticks (100 MHz)
   int useFences;                     // 1: system acquire/release around each slot
   int pollMode;                      // 0: system-scope load, 1: atomic RMW poll

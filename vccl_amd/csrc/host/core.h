@@ -194,6 +194,8 @@ constexpr uint64_t kCommMagic = 0x76636363'6c6d6933ull;  // "vccclmi3"
 ncclResult_t comm_check(const ncclComm* comm, const char* api);
 // Waits until every eager launch of `comm` has completed (init.cc).
 ncclResult_t comm_wait_own_launches(ncclComm* comm);
+// The comm's device error word as a result code (init.cc).
+ncclResult_t error_word_result(ncclComm* comm);
 
 // Net proxy (proxy.cc).  net_listen opens this rank's listener before the
 // peer exchange (address published in `me`); net_connect builds the

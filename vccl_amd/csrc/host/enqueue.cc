@@ -1281,8 +1281,9 @@ static ncclResult_t enqueue_check_impl(int coll, const char* name, const void* s
   else t.devOp = OP_COPY;
   t.root = root;
   if (*(volatile int*)comm->errorFlag) {
-    comm->asyncError = ncclRemoteError;
-    return ncclRemoteError;
+    const ncclResult_t e = error_word_result(comm);
+    comm->asyncError = e;
+    return e;
   }
   if (tl_groupDepth > 0) {
     tl_tasks.push_back(t);

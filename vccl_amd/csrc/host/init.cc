@@ -711,6 +711,7 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
       d.sendHead = flag(c->rank, 1);
       d.recvStep = d.sendStep = 0;
       d.sendSizes = nullptr;
+      d.recvSizes = nullptr;
       d.ll128Recv = ll128Of[c->rank] ? ll128Of[c->rank] + ch * ll128PerCh : nullptr;
       d.ll128Send = ll128Of[next] ? ll128Of[next] + ch * ll128PerCh : nullptr;
       // a net end's pointers are set by net_connect below
@@ -1094,6 +1095,20 @@ VCCL_EXPORT const char* ncclGetErrorString(ncclResult_t r) {
   }
 }
 
+// The comm's device error word as an ncclResult_t (ring_types.hpp): a spin
+// that made no progress — a peer stopped — is ncclRemoteError; a net slot
+// whose landed byte count is not its step's slice length is caught before
+// it is reduced and reported as ncclInternalError.
+ncclResult_t vccl::error_word_result(ncclComm* comm) {
+  const int w = *(volatile int*)comm->errorFlag;
+  if (w == kErrSlotSize) {
+    VWARN("rank %d: a net slot landed with a byte count that is not its step's slice length; the call was "
+          "stopped before reducing it", comm->rank);
+    return ncclInternalError;
+  }
+  return w ? ncclRemoteError : ncclSuccess;
+}
+
 // The text of the last WARN, whatever NCCL_DEBUG filters (debug.cc:29,
 // :265-272 ncclLastError; init.cc:2223-2225: comm unused, may be NULL).
 VCCL_EXPORT const char* ncclGetLastError(ncclComm_t) { return last_error(); }
@@ -1103,8 +1118,8 @@ VCCL_EXPORT ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* as
   if (!asyncError) return ncclInvalidArgument;
   int e = comm->asyncError.load();
   if (e == 0 && comm->errorFlag && *(volatile int*)comm->errorFlag) {
-    comm->asyncError = ncclRemoteError;  // a peer stopped making progress
-    e = ncclRemoteError;
+    e = error_word_result(comm);
+    comm->asyncError = e;
   }
   *asyncError = (ncclResult_t)e;
   return ncclSuccess;

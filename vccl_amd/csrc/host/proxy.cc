@@ -66,13 +66,17 @@ struct ChanFlags {
   Line sendHead;      // proxy: slots the remote receiver consumed
   Line recvTail;      // proxy: slots landed
   Line recvHead;      // GPU: slots consumed
-  uint32_t sendSizes[kSteps];
-  char pad[128 - sizeof(uint32_t) * kSteps];
+  uint32_t sendSizes[kSteps];  // GPU: bytes posted per slot; kNetSizeUnset once shipped
+  uint32_t recvSizes[kSteps];  // proxy: bytes landed per slot (the GPU checks them)
+  char pad[128 - 2 * sizeof(uint32_t) * kSteps];
 };
 
 struct Conn {
   int ch = -1;
   int fd = -1;
+  // VCCL_DEBUG_NET_SHORT_SLOT=b (test hook): ship the connection's first slot
+  // of at least b bytes 16 bytes short, as a stale size would
+  int64_t shortSlot = 0;
   char* buf = nullptr;       // kSteps slots, host pointer
   ChanFlags* flags = nullptr;
   uint64_t done = 0;         // send: slots shipped; recv: slots landed
@@ -92,14 +96,18 @@ struct NetProxy {
   std::vector<std::thread> threads;  // one per connection end
   volatile int* errorFlag = nullptr;  // the comm's host-mapped error word
   std::atomic<uint64_t> bytesSent{0}, bytesRecv{0};
+  int64_t sizeWaitS = 60;    // bound on a posted slot's size staying unset
 };
 
 namespace {
 
-void fail(NetProxy* P, const char* what, int ch) {
+// Socket failures read as a lost peer (kErrSpinTimeout: ncclRemoteError); a
+// slot size that is not valid, as kErrSlotSize (ncclInternalError).
+void fail(NetProxy* P, const char* what, int ch, int word = kErrSpinTimeout) {
   if (!P->stop.load()) {
-    VWARN("net proxy: %s on channel %d: %s", what, ch, strerror(errno));
-    *P->errorFlag = 1;
+    if (word == kErrSpinTimeout) VWARN("net proxy: %s on channel %d: %s", what, ch, strerror(errno));
+    else VWARN("net proxy: %s on channel %d", what, ch);
+    *P->errorFlag = word;
   }
 }
 
@@ -129,6 +137,17 @@ void idle_wait(bool busy, int* idle) {
 
 // Send end: ship every posted slot {bytes, payload} in step order; apply the
 // receiver's credits (8-byte head values, read without blocking).
+//
+// Slot sizes carry the reference's sentinel (src/transport/net.cc:1250-1255,
+// 1365-1367: a consumed slot's size is reset to -1 and the proxy sends only
+// once it is valid): a shipped slot's size word goes back to kNetSizeUnset,
+// so a size the GPU has not (yet) published is never shipped as a stale
+// one.  The GPU releases the size before the tail (ring.hpp), so a valid
+// size normally shows at once; one still unset after VCCL_SPIN_TIMEOUT_S, or
+// a size past the slot stride, is an error (the comm's error word), never a
+// clamped or short slot.  The credit that lets the GPU reuse the slot is
+// applied by this same thread after the reset, so the reset cannot land on
+// the next use of the slot.
 void send_loop(NetProxy* P, Conn* c) {
   int idle = 0;
   uint64_t credit = 0;
@@ -138,8 +157,29 @@ void send_loop(NetProxy* P, Conn* c) {
     const uint64_t posted = ld_acq(&c->flags->sendTail.v);
     while (c->done < posted && !P->stop.load(std::memory_order_relaxed)) {
       const int slot = (int)(c->done % kSteps);
-      uint64_t bytes = __atomic_load_n(&c->flags->sendSizes[slot], __ATOMIC_ACQUIRE);
-      bytes = std::min<uint64_t>(bytes, (uint64_t)P->stride);
+      uint32_t sz = __atomic_load_n(&c->flags->sendSizes[slot], __ATOMIC_ACQUIRE);
+      if (sz == kNetSizeUnset) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while ((sz = __atomic_load_n(&c->flags->sendSizes[slot], __ATOMIC_ACQUIRE)) == kNetSizeUnset &&
+               !P->stop.load(std::memory_order_relaxed)) {
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(P->sizeWaitS)) {
+            fail(P, "a posted slot's size never became valid", c->ch, kErrSlotSize);
+            return;
+          }
+          std::this_thread::yield();
+        }
+        if (sz == kNetSizeUnset) return;  // stopping
+      }
+      if (sz > (uint64_t)P->stride) {
+        fail(P, "a posted slot's size is past the slot stride", c->ch, kErrSlotSize);
+        return;
+      }
+      uint64_t bytes = sz;
+      if (c->shortSlot && (int64_t)bytes >= std::max<int64_t>(c->shortSlot, 32)) {
+        bytes -= 16;  // test hook: a stale / short size, which the receiving kernel must refuse
+        c->shortSlot = 0;
+      }
+      __atomic_store_n(&c->flags->sendSizes[slot], kNetSizeUnset, __ATOMIC_RELAXED);
       if (!io_all(P, c->fd, &bytes, sizeof(bytes), true) ||
           (bytes && !io_all(P, c->fd, c->buf + slot * P->stride, bytes, true))) {
         fail(P, "send", c->ch);
@@ -197,6 +237,9 @@ void recv_loop(NetProxy* P, Conn* c) {
         return;
       }
       P->bytesRecv += bytes;
+      // the landed byte count, before the tail (the kernel compares it with
+      // the step's slice length, ring.hpp recv_size_ok)
+      __atomic_store_n(&c->flags->recvSizes[c->done % kSteps], (uint32_t)bytes, __ATOMIC_RELAXED);
       c->done++;
       st_rel(&c->flags->recvTail.v, c->done);
       busy = true;
@@ -261,6 +304,10 @@ ncclResult_t net_connect(ncclComm* c, const std::vector<std::vector<int>>& rings
   const size_t bytes = flagBytes + nConn * kSteps * (size_t)P->stride;
   HIPCHECK(hipHostMalloc((void**)&P->host, bytes, hipHostMallocMapped | hipHostMallocCoherent));
   memset(P->host, 0, flagBytes);
+  for (int ch = 0; ch < nch; ch++)
+    for (int k = 0; k < kSteps; k++) ((ChanFlags*)P->host)[ch].sendSizes[k] = kNetSizeUnset;
+  P->sizeWaitS = std::max<int64_t>(1, param_int("SPIN_TIMEOUT_S", 60));
+  const int64_t shortSlot = param_int("DEBUG_NET_SHORT_SLOT", 0);
   char* dev = nullptr;
   HIPCHECK(hipHostGetDevicePointer((void**)&dev, P->host, 0));
   auto devp = [&](void* h) { return dev + ((char*)h - P->host); };
@@ -288,6 +335,7 @@ ncclResult_t net_connect(ncclComm* c, const std::vector<std::vector<int>>& rings
     k.buf = slots;
     slots += kSteps * P->stride;
     k.flags = &flags[ch];
+    k.shortSlot = shortSlot;
     P->send.push_back(k);
   }
   for (size_t i = 0; i < recvCh.size(); i++) {
@@ -332,6 +380,7 @@ ncclResult_t net_connect(ncclComm* c, const std::vector<std::vector<int>>& rings
     d.recvFifo = devp(k.buf);
     d.recvTail = (uint64_t*)devp(&k.flags->recvTail.v);
     d.prevSendHead = (uint64_t*)devp(&k.flags->recvHead.v);
+    d.recvSizes = (const uint32_t*)devp(k.flags->recvSizes);
   }
   for (Conn& k : P->send) P->threads.emplace_back(send_loop, P, &k);
   for (Conn& k : P->recv) P->threads.emplace_back(recv_loop, P, &k);
