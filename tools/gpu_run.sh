@@ -19,6 +19,8 @@
 #                  under rocprofv3 --kernel-trace --stats (tools/mp_prof.py)
 #        fence:<n> tools/fence_cost.py on n ranks (fences off / on, interleaved)
 #        lll:<n>[q<k>]  tools/ll_latency.py on n ranks, GPU_MAX_HW_QUEUES=k (4)
+#        lltrace:<n> the same under rocprofv3 kernel + HIP API trace per rank, tools/ll_trace.py summary
+#        ll1p:<n>  the LL all-reduce with n ranks in ONE process (tools/ll_latency_1proc.py)
 # Outputs go to gpurun_out/<label>/.  Every GPU step has its own time limit
 # and the chain stops at the first failure (no retries).
 set -e
@@ -46,6 +48,8 @@ for s in "$@"; do
     mprof:*) timeout -k 10 600 python -u tools/mp_prof.py ${s#mprof:} $O/mprof_n${s#mprof:} --steps 5 --warmup 2 > $O/mprof_n${s#mprof:}.log 2>&1 ;;
     fence:*) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#fence:} --master-addr 127.0.0.1 --master-port 29536 tools/fence_cost.py > $O/fence_n${s#fence:}.json 2> $O/fence_n${s#fence:}.err ;;
     lll:*) n=${s#lll:}; q=${n#*q}; n=${n%q*}; [ "$q" = "$n" ] && q=4; GPU_MAX_HW_QUEUES=$q timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29537 tools/ll_latency.py > $O/lll_n${n}_q${q}.json 2> $O/lll_n${n}_q${q}.err ;;
+    lltrace:*) n=${s#lltrace:}; MP_PROF_SCRIPT=tools/ll_latency.py MP_PROF_FLAGS=--hip-runtime-trace timeout -k 10 600 python -u tools/mp_prof.py $n $O/lltrace_n$n > $O/lltrace_n$n.log 2>&1 && python tools/ll_trace.py $O/lltrace_n$n > $O/lltrace_n$n.json ;;
+    ll1p:*) VCCL_ALLOW_SHARED_DEVICE=1 timeout -k 10 300 python -u tools/ll_latency_1proc.py ${s#ll1p:} > $O/ll1p_n${s#ll1p:}.json 2> $O/ll1p_n${s#ll1p:}.err ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
