@@ -37,7 +37,7 @@ import torch  # noqa: E402
 from tests import _mp  # noqa: E402
 from vccl_amd import nccl  # noqa: E402
 
-PATHS = (("ring", 8 << 20), ("ll", 4 << 10), ("direct", 2 << 20))
+PATHS = (("ring", int(os.environ.get("FAIL_RING_BYTES", 8 << 20)) // 4 * 4), ("ll", 4 << 10), ("direct", 2 << 20))
 
 
 def usable_after(res):

@@ -1,9 +1,10 @@
-"""The ring's opt-in build switches (device/ring.hpp) still compile: the
-per-wave hand-off (VCCL_RING_WAVE_SYNC=1), scalar credit polls
-(VCCL_RING_SPOLL=1) and the non-draining last step (VCCL_RING_LAST_DRAINS=0)
-are not in the default library, so nothing else would notice them rotting.
-Front end only (-fsyntax-only: parse + template instantiation of the kernels
-for gfx950), for the SIMPLE ring and the LL128 ring families.  CPU only."""
+"""The ring's opt-in build switches (device/ring.hpp) still compile: scalar
+credit polls (VCCL_RING_SPOLL=1) and the non-draining last step
+(VCCL_RING_LAST_DRAINS=0) of the per-wave hand-off are not in the default
+library, so nothing else would notice them rotting.  Front end only
+(-fsyntax-only: parse + template instantiation of the kernels for gfx950),
+for the per-wave SIMPLE ring (PART 4, where the switches act) and, with the
+switches on, the workgroup SIMPLE and LL128 ring families.  CPU only."""
 import os
 import shutil
 import subprocess
@@ -16,11 +17,11 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="needs hipcc")
 @pytest.mark.parametrize("defs", [
-    ["-DVCCL_RING_WAVE_SYNC=1"],
-    ["-DVCCL_RING_WAVE_SYNC=1", "-DVCCL_RING_SPOLL=1"],
+    ["-DVCCL_RING_SPOLL=1"],
     ["-DVCCL_RING_LAST_DRAINS=0"],
+    ["-DVCCL_RING_SPOLL=1", "-DVCCL_RING_LAST_DRAINS=0"],
 ])
-@pytest.mark.parametrize("part", [0, 3])
+@pytest.mark.parametrize("part", [0, 3, 4])
 def test_ring_switch_compiles(defs, part):
     cmd = [HIPCC, "-std=c++20", "-O3", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
            "--offload-arch=gfx950", "-I", "include", "-DVCCL_KT=4", f"-DVCCL_PART={part}", *defs,

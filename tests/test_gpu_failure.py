@@ -39,9 +39,16 @@ def _run(n, mode, ncomms, spin_timeout, wave=0):
     env = _mp.worker_env(os.environ)
     env["VCCL_SPIN_TIMEOUT_S"] = str(spin_timeout)
     # the SIMPLE ring's workgroup (0) or per-wave (1) slot hand-off: each has
-    # its own spins (ring.hpp prim_wg / prim_ws), each must end on a lost peer
-    env["VCCL_RING_WAVE"] = str(wave)
-    env["VCCL_RING_WAVE_MIN"] = "0"
+    # its own spins (ring.hpp prim_wg / prim_ws), each must end on a lost peer.
+    # "mixed" (ADVICE r5): the per-wave kernels at the default
+    # VCCL_RING_WAVE_MIN with a ragged ring bucket, so one launch mixes
+    # per-wave slots and workgroup slots (prim_ws -> prim_wg) while it aborts
+    env["VCCL_RING_WAVE"] = "0" if wave == 0 else "1"
+    if wave == "mixed":
+        env.pop("VCCL_RING_WAVE_MIN", None)
+        env["FAIL_RING_BYTES"] = str((8 << 20) + (96 << 10) + 20)
+    else:
+        env["VCCL_RING_WAVE_MIN"] = "0"
     with tempfile.TemporaryDirectory() as d:
         procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mp_fail_worker.py"),
                                    str(r), str(n), d, mode, uids], env=env,
@@ -62,7 +69,7 @@ def _run(n, mode, ncomms, spin_timeout, wave=0):
     return res, "\n".join(logs)
 
 
-@pytest.mark.parametrize("wave", [0, 1])
+@pytest.mark.parametrize("wave", [0, 1, "mixed"])
 def test_lost_peer_ends_ring_ll_direct_kernels(wave):
     n, timeout_s = 3, 3
     res, logs = _run(n, "peer_loss", 3, timeout_s, wave)

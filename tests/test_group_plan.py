@@ -179,7 +179,10 @@ def test_algo_selection():
         ("Ring", "LL"): (2, LLRS),                          # ring + LL is a valid pair
         ("Tree", None): (2, LL | LLRS),
         ("Tree", "Simple"): (1, SIMPLE),                    # no SIMPLE tree here: the SIMPLE ring, WARNed
-        ("Tree", "LL128"): (1, SIMPLE),
+        ("Tree", "LL128"): (4, LL128),                      # Simple excluded -> the LL128 ring
+        ("Direct", "LL128"): (4, LL128),
+        ("NVLS", "Simple"): (1, SIMPLE),                    # no NVLS here: the SIMPLE ring, WARNed
+        ("NVLS", "^Simple"): (4, LL128),
         ("Direct", None): (3, DIRECT),
         ("^Direct", None): (0, LL | LLRS | LL128 | SIMPLE),
         ("ring;allreduce:tree", None): (0, LLRS | LL128 | SIMPLE),  # per-collective entries ignored
@@ -188,6 +191,7 @@ def test_algo_selection():
         assert nccl.algo_selection(algo, proto) == want, (algo, proto)
     # unknown names, or lists that leave no protocol / no algorithm at all
     for algo, proto in ((None, "bogus"), ("Ring,Foo", None), (None, "^LL,LL128,Simple"),
+                        ("Direct", "LL"), ("NVLS,PAT", "LL"),  # only LL allowed, no LL path for them
                         ("^Tree,Ring,CollnetDirect,CollnetChain,NVLS,NVLSTree,PAT,Direct", None)):
         with pytest.raises(nccl.VcclError) as e:
             nccl.algo_selection(algo, proto)

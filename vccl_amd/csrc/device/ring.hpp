@@ -41,19 +41,6 @@
 // (prim_ws); 0: every wave defers its drain past its next slot's first loads.
 #define VCCL_RING_LAST_DRAINS 1
 #endif
-#ifndef VCCL_RING_WAVE_SYNC
-// 0 (PART 0 objects): the workgroup hand-off (RingCtx::prim_wg: every wave
-// drains, a barrier, thread 0 posts).  1 (PART 4 objects, ring_kernels.hip):
-// the per-wave hand-off (RingCtx::prim_ws: each wave drains its slot behind
-// its next slot's loads, the last wave posts; workgroup hand-off below
-// VCCL_RING_WAVE_MIN).  Round 5 measured it: the drain per slot fell from
-// 9.8 to 3.3 us, but on every shared-GPU rehearsal row the ring was level
-// or slower — 2-3 us per call at 256 KiB - 8 MiB, 2-4 % at 1 GiB
-// (profiles/r05k, r05n, r05o) — so a comm runs it only when asked
-// (VCCL_RING_WAVE=1 / vcclCommSetRingWave) until a run over xGMI, where
-// remote stores acknowledge slowly, says otherwise.
-#define VCCL_RING_WAVE_SYNC 0
-#endif
 
 // LDS / global pointers are typed as such: through a generic pointer the
 // compiler emits flat_* accesses, which vmcnt counts out of order (a wait on
@@ -393,17 +380,15 @@ struct RingCtx {
   __device__ __forceinline__ void prim_ws(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp, int recvOff,
                           int sendOff) {
     using T = typename Fn::EltType;
-    if (aborted()) return;
-    const bool tr = trace != nullptr && traceN < traceCap && tid == 0;
-    uint64_t t0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (seq >= (uint32_t)kSyncDepth && !wait_done(seq - kSyncDepth)) return;
-    const uint64_t needTail = RECV ? recvStep + 1 : 0;
-    const uint64_t needHead = SEND && sendStep + 1 > (uint64_t)kSteps ? sendStep + 1 - kSteps : 0;
     // Slots below VCCL_RING_WAVE_MIN (latency-bound: a few KiB per wave)
     // hand over as a workgroup: without the barrier the waves drift apart and
     // every step waits for the last of them (+1 us per step from 256 KiB to
     // 8 MiB, profiles/r05k / r05m); the overlap pays from full slots up.
-    const bool waveMode = (nelem > 0 ? nelem * (int64_t)sizeof(T) : 0) >= waveMin;  // wave-uniform
+    // Decided before any abort check: every wave of the workgroup reaches
+    // prim_wg's barriers whatever it has seen of the abort word (each wave
+    // sees it at its own time; prim_wg reads it after a barrier), so barrier
+    // instances keep pairing up on a failing launch.
+    const bool waveMode = (nelem > 0 ? nelem * (int64_t)sizeof(T) : 0) >= waveMin;  // workgroup-uniform
     if (!waveMode) {
       complete_pending<0>();
       drain_vmem();  // a per-wave post of the previous slot retires before this slot's post
@@ -415,6 +400,12 @@ struct RingCtx {
       seq++;
       return;
     }
+    if (aborted()) return;
+    const bool tr = trace != nullptr && traceN < traceCap && tid == 0;
+    uint64_t t0 = tr ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (seq >= (uint32_t)kSyncDepth && !wait_done(seq - kSyncDepth)) return;
+    const uint64_t needTail = RECV ? recvStep + 1 : 0;
+    const uint64_t needHead = SEND && sendStep + 1 > (uint64_t)kSteps ? sendStep + 1 - kSteps : 0;
     bool have = __hip_atomic_load(&ws->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needTail &&
                 __hip_atomic_load(&ws->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= needHead;
 #if VCCL_RING_SPOLL
@@ -502,28 +493,20 @@ struct RingCtx {
     if (RECV) recvStep++;
   }
 
-  template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
-  __device__ __forceinline__ void prim(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
-                                       int recvOff = 0, int sendOff = 0) {
-#if VCCL_RING_WAVE_SYNC
-    prim_ws<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, src, dst, nelem, postOp, recvOff, sendOff);
-#else
-    prim_wg<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, src, dst, nelem, postOp, recvOff, sendOff);
-#endif
-  }
-
   // One primitive call: at most one slot of payload.
   //   srcs = [SRC ? own input] ++ [RECV ? recv slot]
   //   dsts = [SEND ? peer slot] ++ [DST ? own output]
   //   recvOff / sendOff: byte offset of the chunk inside its slot (< 16)
-  // (Rounds 1-4: the workgroup hand-off — VCCL_RING_WAVE_SYNC=0.)
+  // The workgroup hand-off (every ring kernel but the per-wave ones).
   template <class Fn, bool RECV, bool SEND, bool SRC, bool DST, int UNROLL>
   __device__ __forceinline__ void prim_wg(const Fn& fn, const void* src, void* dst, int64_t nelem, bool postOp,
                           int recvOff = 0, int sendOff = 0) {
-    if (aborted()) return;
+    // The abort word is read by every wave only after the first barrier
+    // (thread 0 skips its spins once it is set): in the per-wave kernels the
+    // waves may each have seen it at a different moment before this slot.
     const bool tr = trace != nullptr && traceN < traceCap;
     uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, tc = 0;
-    if (tid == 0) {
+    if (tid == 0 && !aborted()) {
       if (tr) t0 = __builtin_amdgcn_s_memrealtime();
       bool ok = true;
       if (RECV) ok = spin_ge(recvTail, recvStep + 1);
@@ -827,9 +810,15 @@ __device__ __forceinline__ void ring_step(RingCtx& r, const Fn& fn, const void* 
   for (int64_t s = 0; s < nSlices; s++) {
     const int64_t o = s * slotElts;
     const int64_t len = nelem - o < slotElts ? nelem - o : slotElts;
-    r.prim<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, SRC ? (const void*)((const T*)src + o) : nullptr,
-                                             DST ? (void*)((T*)dst + o) : nullptr,
-                                             len > 0 ? len : 0, postOp, recvOff, sendOff);
+    const void* sp = SRC ? (const void*)((const T*)src + o) : nullptr;
+    void* dp = DST ? (void*)((T*)dst + o) : nullptr;
+    // the slot hand-off is part of the kernel's protocol (a template
+    // parameter, so the workgroup and per-wave objects never define one
+    // symbol two ways)
+    if constexpr (PROTO == kProtoSimpleWave)
+      r.template prim_ws<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, sp, dp, len > 0 ? len : 0, postOp, recvOff, sendOff);
+    else
+      r.template prim_wg<Fn, RECV, SEND, SRC, DST, UNROLL>(fn, sp, dp, len > 0 ? len : 0, postOp, recvOff, sendOff);
   }
 }
 

@@ -9,12 +9,6 @@
 
 #include "dispatch.hpp"
 #include "ring_launch.hpp"
-#if VCCL_PART == 4
-// the per-wave slot hand-off in this object only (ring.hpp prim_ws); its
-// kernels carry kProtoSimpleWave, so no symbol clashes with PART 0's
-#undef VCCL_RING_WAVE_SYNC
-#define VCCL_RING_WAVE_SYNC 1
-#endif
 #if VCCL_PART == 0 || VCCL_PART == 3 || VCCL_PART == 4
 #include "ring.hpp"
 #elif VCCL_PART == 1

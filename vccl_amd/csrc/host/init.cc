@@ -98,7 +98,8 @@ std::vector<std::vector<int>> ring_orders(int n) {
 // only one the lists leave; otherwise the excluded ones are dropped from the
 // automatic choice.  A pair the reference accepts but no path here serves
 // (e.g. Tree with Simple: VCCL's SIMPLE tree is out of scope) falls back to
-// the SIMPLE ring with a WARN.
+// the SIMPLE ring, or the LL128 ring when Simple is excluded, with a WARN
+// (ADVICE r4, r5); with neither allowed it fails (ncclInvalidUsage).
 enum { kAllowLL = 1, kAllowLL128 = 2, kAllowSimple = 4, kAllowDirect = 8, kAllowLLRsAg = 16 };
 static ncclResult_t parse_name_list(const char* env, const char* str, const char* const* names, int nNames,
                                     unsigned* mask) {
@@ -162,9 +163,19 @@ ncclResult_t algo_proto_select(const char* algo, const char* proto, int* force, 
   if ((p & 4) && ring) m |= kAllowSimple;
   if ((p & 4) && direct) m |= kAllowDirect;
   if (m == 0) {
-    VWARN("NCCL_ALGO=%s / NCCL_PROTO=%s: no path of this library serves that pair; using the SIMPLE ring",
-          algo ? algo : "", proto ? proto : "");
-    m = kAllowSimple;
+    // No path here serves the pair (e.g. Tree + Simple: VCCL's SIMPLE tree is
+    // out of scope).  Fall back only to a ring whose protocol the user still
+    // allows: the SIMPLE ring, else the LL128 ring; a list that
+    // leaves only LL with no LL path for its algorithms is refused.
+    const int fb = (p & 4) ? kAllowSimple : (p & 2) ? kAllowLL128 : 0;
+    if (!fb) {
+      VWARN("NCCL_ALGO=%s / NCCL_PROTO=%s: no path of this library serves that pair with an allowed protocol",
+            algo ? algo : "", proto ? proto : "");
+      return ncclInvalidUsage;
+    }
+    VWARN("NCCL_ALGO=%s / NCCL_PROTO=%s: no path of this library serves that pair; using the %s ring",
+          algo ? algo : "", proto ? proto : "", fb == kAllowSimple ? "SIMPLE" : "LL128");
+    m = fb;
   }
   const int f = m == kAllowDirect ? 3 : m == kAllowLL128 ? 4 : m == kAllowSimple ? 1
                 : (m & ~(kAllowLL | kAllowLLRsAg)) == 0 ? 2 : 0;
