@@ -267,6 +267,9 @@ __device__ __forceinline__ bool direct_wait(const DirectWork& w, const char* myF
         }
       }
     }
+    // VCCL_FENCES=1: the system-scope acquire the ring takes per slot (the
+    // default needs none: sc0 sc1 loads of uncached inboxes)
+    if (comm->useFences) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
   return *shFail == 0;
@@ -281,6 +284,7 @@ __device__ __forceinline__ void direct_post(const DirectWork& w, const DirectPee
   const int k = threadIdx.x;
   if (k >= 1 && k < w.nRanks) {
     const int p = w.rank + k < w.nRanks ? w.rank + k : w.rank + k - w.nRanks;
+    if (w.comm->useFences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // VCCL_FENCES=1, as the ring
     __hip_atomic_store((uint32_t*)(P.flags[p] + direct_flag_off(phase, parity, w.rank, b)), e,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }

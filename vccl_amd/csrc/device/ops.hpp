@@ -526,7 +526,10 @@ __device__ __forceinline__ u32x4 pack_reduce(const FnPreMulSum<f8e5m2_t>&, u32x4
   return pack_reduce(FnSum<f8e5m2_t>(), a, b);
 }
 #endif
-// (f8_pack_add<false>, the E5M2 form, measured 6.2 TB/s and is unused.)
+// (f8_pack_add<false>, the E5M2 form, measured 6.2 TB/s and is unused.  An
+// E4M3-shaped E5M2 sum — med3 clamp to +-57344 before narrowing, NaN patched
+// from the input codes — was exact on all 65,536 pairs and 7-8 % slower,
+// 6.52 vs 7.07 TB/s: ~10 more VALU per dword, profiles/r06e.)
 
 template <class Fn>
 __device__ __forceinline__ u32x4 pack_preop(const Fn& fn, u32x4 a) {
