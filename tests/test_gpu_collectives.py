@@ -197,7 +197,7 @@ def test_single_process_ranks(n, placement, monkeypatch):
                                     (2, "ring_only"), (4, "ring_only"), (7, "ring_only"),
                                     (8, "ring_only"), (4, "direct_only"), (8, "default8"), (2, "net"),
                                     (3, "net"), (2, "ll128"), (4, "ll128"), (8, "ll128"),
-                                    (4, "chain"), (8, "chain"), (2, "net_ll128")])
+                                    (4, "chain"), (8, "chain"), (2, "net_ll128"), (4, "test_fences")])
 def test_multi_process_ranks(n, geom):
     _ring_ranks(n, geom)
 
@@ -245,8 +245,10 @@ def _ring_ranks(n, geom):
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
         ll_max = direct_max = 0
         proto = 1
-    elif geom in ("test", "ring_only", "direct_only"):
+    elif geom in ("test", "ring_only", "direct_only", "test_fences"):
         env.update(TEST_GEOM)
+        if geom == "test_fences":  # system-scope fences on every ring slot and direct flag (VCCL_FENCES)
+            env["VCCL_FENCES"] = "1"
         nch, slot = int(TEST_GEOM["VCCL_NCHANNELS"]), int(TEST_GEOM["VCCL_SLOT_BYTES"])
         if geom == "ring_only":  # NCCL_ALGO=Ring: the ring for every all-reduce,
             env["NCCL_ALGO"] = "Ring"  # ring LL (one-hop) for small RS / AG
