@@ -1369,6 +1369,10 @@ def bench_extras(dist, comm, rank, world, args):
                                                         min(args.steps, 5))
     except Exception as e:  # noqa: BLE001
         ex["channels_error"] = repr(e)
+    try:  # the ring's slot timeline on the headline bucket, both hand-offs
+        ex["ring_trace"] = _ring_trace_row(dist, rank, world, args.bytes or (1 << 30))
+    except Exception as e:  # noqa: BLE001
+        ex["ring_trace_error"] = repr(e)
     # Last: config 5 without per-call launch cost (nccl-tests -G: HIP graph
     # replay).  Its capture stream is one more hardware queue per process;
     # with 8 ranks sharing one GPU (rehearsal) that oversubscribes the
@@ -1385,6 +1389,94 @@ def bench_extras(dist, comm, rank, world, args):
         ex["graph_error"] = repr(e)
     ex["async_error"] = comm.async_error()
     return ex
+
+
+_TRACE_SHAPES = {0b0110: "S->F", 0b0111: "S+F->F", 0b1111: "S+F->F+O", 0b1101: "S+F->O", 0b1011: "F->F+O",
+                 0b1001: "F->O", 0b1110: "S->F+O"}
+
+
+def ring_trace_summary(tr):
+    """Per primitive shape of a VCCL_RING_TRACE timeline (vcclCommRingTrace,
+    one record per FIFO slot per channel, s_memrealtime at 100 MHz): the mean
+    time per slot waiting for credits (t1-t0), for the workgroup release
+    (t2-t1), moving and draining the payload (t3-t2 = issue tc-t2 + drain
+    t3-tc), posting (t4-t3), the gap to the channel's next slot, and the
+    payload rate of the copy phase."""
+    rows = {}
+    for ch in range(tr.shape[0]):
+        rec = tr[ch][tr[ch]["t4"] > 0]
+        for i, r in enumerate(rec):
+            d = rows.setdefault(_TRACE_SHAPES.get(int(r["shape"]), str(int(r["shape"]))),
+                                {"n": 0, "wait": 0.0, "release": 0.0, "copy": 0.0, "post": 0.0, "gap": 0.0,
+                                 "issue": 0.0, "drain": 0.0, "bytes": 0})
+            d["n"] += 1
+            d["wait"] += (int(r["t1"]) - int(r["t0"])) / 100.0  # us
+            d["release"] += (int(r["t2"]) - int(r["t1"])) / 100.0
+            d["copy"] += (int(r["t3"]) - int(r["t2"])) / 100.0
+            d["post"] += (int(r["t4"]) - int(r["t3"])) / 100.0
+            if int(r["tc"]):
+                d["issue"] += (int(r["tc"]) - int(r["t2"])) / 100.0
+                d["drain"] += (int(r["t3"]) - int(r["tc"])) / 100.0
+            if i + 1 < len(rec):
+                d["gap"] += (int(rec[i + 1]["t0"]) - int(r["t4"])) / 100.0
+            d["bytes"] += int(r["bytes"])
+    out = {}
+    for k, d in rows.items():
+        n = d["n"]
+        out[k] = {"n": n, **{f: round(d[f] / n, 2) for f in ("wait", "release", "copy", "issue", "drain", "post",
+                                                              "gap")},
+                  "payload_GBs_in_copy": round(d["bytes"] / (d["copy"] * 1e3), 1) if d["copy"] else None}
+    return out
+
+
+def _ring_trace_row(dist, rank, world, S, cap=1024):
+    """The SIMPLE ring's slot timeline on the headline bucket (config 3, ring
+    forced), both hand-offs, on a fresh comm created with VCCL_RING_TRACE:
+    on one rank per GPU it shows whether a slot waits on credits (the link /
+    the peer), on its copy or on the drain of its remote stores — what decides
+    the channel model's headroom and the per-wave hand-off.  Two
+    untimed calls, then one traced call per hand-off; per rank the span of
+    the traced call and ring_trace_summary."""
+    old = os.environ.get("VCCL_RING_TRACE")
+    os.environ["VCCL_RING_TRACE"] = str(cap)
+    try:
+        obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        c = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank)
+    finally:
+        if old is None:
+            os.environ.pop("VCCL_RING_TRACE", None)
+        else:
+            os.environ["VCCL_RING_TRACE"] = old
+    sp = torch.cuda.current_stream().cuda_stream
+    n = S // 4
+    x = torch.rand(n, device="cuda")
+    y = torch.empty_like(x)
+    out = {"bytes": n * 4, "channels": c.n_channels()}
+    try:
+        c.set_algo("ring")
+        for wave in (False, True):
+            c.set_ring_wave(wave)
+            for _ in range(2):
+                c.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+            torch.cuda.synchronize()
+            dist.barrier()
+            c.ring_trace()  # clears
+            dist.barrier()
+            c.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+            torch.cuda.synchronize()
+            tr = c.ring_trace()
+            t0 = tr["t0"][tr["t0"] > 0]
+            span = round((int(tr["t4"].max()) - int(t0.min())) / 100.0, 1) if t0.size else None
+            res = [None] * world
+            dist.all_gather_object(res, {"rank": rank, "span_us": span, "shapes": ring_trace_summary(tr)})
+            out["per_wave" if wave else "workgroup"] = res
+        out["async_error"] = c.async_error()
+    finally:
+        c.set_ring_wave(False)
+        c.destroy()
+    del x, y
+    return out
 
 
 BCAST_SIZES = (64 << 10, 8 << 20, 256 << 20)

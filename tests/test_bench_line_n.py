@@ -138,3 +138,21 @@ def test_cpu_rank_shape_checks_every_pass():
     for nsrc, ncopy in ((2, 0), (3, 3000), (8, 1 << 16)):
         r = O.cpu_bench_rank(5000, nsrc, ncopy, [0], 0.05)
         assert r["correct"] and r["iters"] >= 1
+
+
+def test_ring_trace_summary():
+    """bench.ring_trace_summary on a hand-made timeline: one channel, two
+    S+F->F+O slots (shape 0b1111) of 1 MiB at 100 MHz ticks."""
+    import numpy as np
+    dt = np.dtype([("t0", "<u8"), ("t1", "<u8"), ("t2", "<u8"), ("t3", "<u8"), ("t4", "<u8"),
+                   ("shape", "<u4"), ("bytes", "<u4"), ("step", "<u8"), ("tc", "<u8")])
+    tr = np.zeros((1, 4), dtype=dt)
+    # slot 0: wait 1 us, release 0.5, copy 10 (issue 8 + drain 2), post 0.5; gap 1 us to slot 1
+    tr[0, 0] = (1000, 1100, 1150, 2150, 2200, 0b1111, 1 << 20, 0, 1950)
+    tr[0, 1] = (2300, 2300, 2350, 3350, 3400, 0b1111, 1 << 20, 1, 3150)
+    s = bench.ring_trace_summary(tr)["S+F->F+O"]
+    assert s["n"] == 2
+    assert s["wait"] == pytest.approx(0.5) and s["release"] == pytest.approx(0.5)
+    assert s["copy"] == pytest.approx(10.0) and s["issue"] == pytest.approx(8.0) and s["drain"] == pytest.approx(2.0)
+    assert s["post"] == pytest.approx(0.5) and s["gap"] == pytest.approx(0.5)  # one gap of 1 us over 2 slots
+    assert s["payload_GBs_in_copy"] == pytest.approx(round(2 * (1 << 20) / (20.0 * 1e3), 1))

@@ -12,7 +12,6 @@ import json
 import os
 import sys
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -21,36 +20,12 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("VCCL_RING_TRACE", "2048")
 from vccl_amd import nccl  # noqa: E402
 
-SHAPES = {0b0110: "S->F", 0b0111: "S+F->F", 0b1111: "S+F->F+O", 0b1101: "S+F->O", 0b1011: "F->F+O",
-          0b1001: "F->O", 0b1110: "S->F+O"}
-
-
 def summarize(tr):
-    rows = {}
-    for ch in range(tr.shape[0]):
-        rec = tr[ch][tr[ch]["t4"] > 0]
-        for i, r in enumerate(rec):
-            d = rows.setdefault(SHAPES.get(int(r["shape"]), str(int(r["shape"]))),
-                                {"n": 0, "wait": 0.0, "release": 0.0, "copy": 0.0, "post": 0.0, "gap": 0.0,
-                                 "issue": 0.0, "drain": 0.0, "bytes": 0})
-            d["n"] += 1
-            d["wait"] += (int(r["t1"]) - int(r["t0"])) / 100.0  # us (100 MHz)
-            d["release"] += (int(r["t2"]) - int(r["t1"])) / 100.0
-            d["copy"] += (int(r["t3"]) - int(r["t2"])) / 100.0
-            d["post"] += (int(r["t4"]) - int(r["t3"])) / 100.0
-            if int(r["tc"]):  # copy = issue (thread 0's accesses issued) + drain (pipeline empty, all waves)
-                d["issue"] += (int(r["tc"]) - int(r["t2"])) / 100.0
-                d["drain"] += (int(r["t3"]) - int(r["tc"])) / 100.0
-            if i + 1 < len(rec):
-                d["gap"] += (int(rec[i + 1]["t0"]) - int(r["t4"])) / 100.0
-            d["bytes"] += int(r["bytes"])
-    out = {}
-    for k, d in rows.items():
-        n = d["n"]
-        out[k] = {"n": n, **{f: round(d[f] / n, 2) for f in ("wait", "release", "copy", "issue", "drain", "post",
-                                                              "gap")},
-                  "payload_GBs_in_copy": round(d["bytes"] / (d["copy"] * 1e3), 1) if d["copy"] else None}
-    return out
+    """Per primitive shape: mean credit wait, release, copy (issue + drain),
+    post and gap per slot, and the payload rate of the copy phase
+    (bench.ring_trace_summary, shared with the N > 1 bench line)."""
+    import bench
+    return bench.ring_trace_summary(tr)
 
 
 def main():
