@@ -533,37 +533,59 @@ def cpu_baseline(n_full, seconds=5.0):
             "cgroup_cpu_quota": q, "machine_cpus": topo["machine_cpus"]}
 
 
-def cpu_baseline_allreduce(S, world, seconds=5.0):
+def _baseline_cpus():
+    """The cores the N > 1 host baselines run on: the cgroup quota's worth of
+    physical cores spread over the NUMA nodes, every physical core without a
+    quota."""
+    topo = host_topology()
+    q = topo["cgroup_cpu_quota"]
+    if q and 2 <= int(q) < len(topo["cpus"]):
+        return topo, _spread(topo["physical_cores"], int(q), topo["node_of"]), "quota_cores"
+    return topo, topo["physical_cores"], "physical_cores"
+
+
+def cpu_baseline_allreduce(S, world, seconds=5.0, dtype=7, cpus=None):
     """Host-core baseline beside the N > 1 line (north_star):
-    one rank's share of the ring all-reduce of an S-byte f32 bucket over
-    `world` ranks done as host work by the oracle's C reduce-copy (oracle/
+    one rank's share of the ring all-reduce of an S-byte bucket over `world`
+    ranks done as host work by the oracle's C reduce-copy (oracle/
     cpu_bench.c, -O3 -march=native on this host) — a world-source sum over
     S / world bytes into the rank's shard (the reduce-scatter's reductions),
     then a copy of the S gathered bytes (the all-gather) — on pinned, first-
     touched host buffers, one bounded ~`seconds` sample on the cgroup quota's
-    worth of physical cores (every physical core when no quota is set),
-    checked bit-exactly.  `value` is in the line's unit: the busbw a rank
-    doing that work on these cores would reach, (S / t_pass) * 2(n-1)/n."""
+    worth of physical cores (every physical core when no quota is set; or
+    `cpus`), checked bit-exactly.  `value` is in the line's unit: the busbw a
+    rank doing that work on these cores would reach, (S / t_pass) * 2(n-1)/n.
+    dtype: f32 (7, config 3), bf16 (9, config 4), f16 (6, config 5)."""
     from oracle import oracle as O
-    topo = host_topology()
-    q = topo["cgroup_cpu_quota"]
-    if q and 2 <= int(q) < len(topo["cpus"]):
-        cpus, which = _spread(topo["physical_cores"], int(q), topo["node_of"]), "quota_cores"
+    topo, auto, which = _baseline_cpus()
+    if cpus is None:
+        cpus = auto
     else:
-        cpus, which = topo["physical_cores"], "physical_cores"
-    m, ncopy = S // (4 * world), S // 4
-    r = O.cpu_bench_rank(m, world, ncopy, cpus, seconds, register=_host_register())
+        which = f"{len(cpus)} core(s)"
+    esz = {7: 4, 6: 2, 9: 2}[dtype]
+    m, ncopy = S // (esz * world), S // esz
+    r = O.cpu_bench_rank(m, world, ncopy, cpus, seconds, register=_host_register(), dtype=dtype)
     assert r["correct"], "cpu baseline mismatch"
     busbw = S / r["s_per_pass"] * 2 * (world - 1) / world / 1e9
-    return {"value": round(busbw, 2), "unit": "GB/s", "cores": r["threads"], "kind": "port",
-            "sample": (f"one rank's share of a {world}-rank ring all-reduce of {S} B f32 as host work: "
+    tname = {7: "f32", 6: "f16", 9: "bf16"}[dtype]
+    return {"value": round(busbw, 3), "unit": "GB/s", "cores": r["threads"], "kind": "port",
+            "sample": (f"one rank's share of a {world}-rank ring all-reduce of {S} B {tname} as host work: "
                        f"{world}-source sum over {m} elems + copy of {ncopy} elems, oracle/reduce_ref.c "
                        f"-O3 -march={r['march']}, pinned={r['pinned']}: {r['iters']} passes in {r['s']} s "
                        f"on {r['threads']} pinned threads ({which}); checked bit-exactly; value = "
                        "(S / t_pass) * 2(n-1)/n, the line's busbw convention"),
-            "mem_GBs": r["mem_GB/s"], "s_per_pass": round(r["s_per_pass"], 5), "which": which,
+            "mem_GBs": r["mem_GB/s"], "us_per_pass": round(r["s_per_pass"] * 1e6, 2), "which": which,
             "nproc": topo["nproc"], "physical_cores": len(topo["physical_cores"]),
-            "numa_nodes": topo["numa_nodes"], "cgroup_cpu_quota": q, "machine_cpus": topo["machine_cpus"]}
+            "numa_nodes": topo["numa_nodes"], "cgroup_cpu_quota": topo["cgroup_cpu_quota"],
+            "machine_cpus": topo["machine_cpus"]}
+
+
+# The other configs with a reduce (SURVEY.md §8d "CPU baseline (all configs
+# with a reduce)"), on bounded samples: config 4's bf16 bucket shape at
+# 32 MiB (the oracle's bf16 arithmetic is a scalar, integer-exact
+# restatement: the full 4 GiB would take minutes), config 5's largest fp16 LL
+# bucket on one core (a latency-regime call).
+CPU_OTHER = (("config4_rs_ag_bf16", 9, 32 << 20, None), ("config5_ll_f16", 6, 128 << 10, 1))
 
 
 def ring_link_peak(orders, nchannels, link_gbs=None):
@@ -640,6 +662,14 @@ def line_roofline_and_baseline(dist, rank, world, last, visible, ring_orders, n_
         if rank == 0:
             try:
                 cpu_base = cpu_baseline_allreduce(last["bytes"], world, cpu_seconds)
+                cpu_base["other_configs"] = {}
+                for name, dt, S, ncores in CPU_OTHER:
+                    cores = None if ncores is None else _baseline_cpus()[1][:ncores]
+                    try:
+                        cpu_base["other_configs"][name] = cpu_baseline_allreduce(
+                            S, world, min(cpu_seconds, 2.0), dtype=dt, cpus=cores)
+                    except Exception as e:  # noqa: BLE001
+                        cpu_base["other_configs"][name] = {"value": None, "error": repr(e)}
             except Exception as e:  # noqa: BLE001 - a failed baseline is reported, not fatal
                 cpu_base = {"value": None, "error": repr(e)}
         dist.barrier()

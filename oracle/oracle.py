@@ -71,10 +71,10 @@ def _bind_cpu_bench(L):
     L.ref_cpu_bench_run.argtypes = [vp, vp, vp, sz, i32, ctypes.POINTER(i32), dbl,
                                     ctypes.POINTER(ctypes.c_long), ctypes.POINTER(dbl)]
     L.ref_cpu_bench_free.argtypes = [vp, vp, vp, sz]
-    L.ref_cpu_bench_rank_alloc.argtypes = [sz, i32, sz, i32, ctypes.POINTER(i32), ctypes.POINTER(vp)]
-    L.ref_cpu_bench_rank_run.argtypes = [ctypes.POINTER(vp), sz, i32, sz, i32, ctypes.POINTER(i32), dbl,
+    L.ref_cpu_bench_rank_alloc.argtypes = [sz, i32, sz, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(vp)]
+    L.ref_cpu_bench_rank_run.argtypes = [ctypes.POINTER(vp), sz, i32, sz, i32, i32, ctypes.POINTER(i32), dbl,
                                          ctypes.POINTER(ctypes.c_long), ctypes.POINTER(dbl)]
-    L.ref_cpu_bench_rank_free.argtypes = [ctypes.POINTER(vp), sz, i32, sz]
+    L.ref_cpu_bench_rank_free.argtypes = [ctypes.POINTER(vp), sz, i32, sz, i32]
     L.ref_reduce_copy.argtypes = [i32, i32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), i32,
                                   i32, i32, ctypes.POINTER(vp), i32, ctypes.POINTER(vp), sz, i32]
     return L
@@ -135,34 +135,36 @@ def cpu_bench(n: int, cpus, seconds: float, register=None, native: bool = True) 
 
 
 def cpu_bench_rank(m: int, nsrc: int, ncopy: int, cpus, seconds: float, register=None,
-                   native: bool = True) -> dict:
+                   native: bool = True, dtype: int = 7) -> dict:
     """One rank's share of an nsrc-rank ring all-reduce as host work (see
-    cpu_bench.c): an nsrc-source f32 sum over m elements into one shard, then a
-    copy of ncopy elements, on len(cpus) pinned persistent workers, each pass
-    checked bit-exactly at the end.  Returns the seconds per pass, the memory
-    rate ((nsrc + 1) m + 2 ncopy) x 4 B per pass, and the check."""
+    cpu_bench.c): an nsrc-source sum of `dtype` (f32 7, f16 6, bf16 9) over m
+    elements into one shard, then a copy of ncopy elements, on len(cpus)
+    pinned persistent workers, each pass checked bit-exactly at the end.
+    Returns the seconds per pass, the memory rate ((nsrc + 1) m + 2 ncopy)
+    elements per pass, and the check."""
     L, march = native_lib() if native else (_bind_cpu_bench(lib()), "x86-64-v3")
+    esz = np.dtype(NP_DTYPE[dtype]).itemsize
     nt = len(cpus)
     cp = (ctypes.c_int * nt)(*cpus)
     bufs = (ctypes.c_void_p * (nsrc + 3))()
-    if L.ref_cpu_bench_rank_alloc(m, nsrc, ncopy, nt, cp, bufs) != 0:
+    if L.ref_cpu_bench_rank_alloc(m, nsrc, ncopy, dtype, nt, cp, bufs) != 0:
         raise MemoryError("cpu bench allocation")
     undo = []
     try:
         if register is not None:
             for i in range(nsrc + 3):
                 if bufs[i]:
-                    undo.append(register(bufs[i], (m if i <= nsrc else ncopy) * 4))
+                    undo.append(register(bufs[i], (m if i <= nsrc else ncopy) * esz))
         iters, el = ctypes.c_long(), ctypes.c_double()
-        ok = L.ref_cpu_bench_rank_run(bufs, m, nsrc, ncopy, nt, cp, seconds, ctypes.byref(iters),
+        ok = L.ref_cpu_bench_rank_run(bufs, m, nsrc, ncopy, dtype, nt, cp, seconds, ctypes.byref(iters),
                                       ctypes.byref(el))
     finally:
         for u in undo:
             if u:
                 u()
-        L.ref_cpu_bench_rank_free(bufs, m, nsrc, ncopy)
+        L.ref_cpu_bench_rank_free(bufs, m, nsrc, ncopy, dtype)
     per_pass = el.value / max(1, iters.value)
-    return {"s_per_pass": per_pass, "mem_GB/s": round(((nsrc + 1) * m + 2 * ncopy) * 4 / per_pass / 1e9, 2),
+    return {"s_per_pass": per_pass, "mem_GB/s": round(((nsrc + 1) * m + 2 * ncopy) * esz / per_pass / 1e9, 2),
             "threads": nt, "iters": iters.value, "s": round(el.value, 2), "correct": bool(ok),
             "march": march, "pinned": register is not None and bool(undo) and all(undo)}
 

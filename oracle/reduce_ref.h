@@ -89,13 +89,15 @@ int ref_cpu_bench_run(void* a, void* b, void* d, size_t n, int nthreads, const i
                       double seconds, long* iters, double* elapsed);
 void ref_cpu_bench_free(void* a, void* b, void* d, size_t n);
 /* One rank's share of an n-rank ring all-reduce as host work: an nsrc-source
- * f32 sum over m elements into one shard, then a copy of ncopy elements (the
- * gather; 0 = none).  bufs[nsrc + 3]: sources, shard, copy source, copy
- * destination.  run returns 1 when the shard and the copy check bit-exactly. */
-int ref_cpu_bench_rank_alloc(size_t m, int nsrc, size_t ncopy, int nthreads, const int* cpus, void** bufs);
-int ref_cpu_bench_rank_run(void** bufs, size_t m, int nsrc, size_t ncopy, int nthreads, const int* cpus,
-                           double seconds, long* iters, double* elapsed);
-void ref_cpu_bench_rank_free(void** bufs, size_t m, int nsrc, size_t ncopy);
+ * sum over m elements of `type` (f32 7, f16 6 or bf16 9) into one shard, then
+ * a copy of ncopy elements (the gather; 0 = none).  bufs[nsrc + 3]: sources,
+ * shard, copy source, copy destination.  run returns 1 when the shard (folded
+ * left to right with ref_reduce1) and the copy check bit-exactly. */
+int ref_cpu_bench_rank_alloc(size_t m, int nsrc, size_t ncopy, int type, int nthreads, const int* cpus,
+                             void** bufs);
+int ref_cpu_bench_rank_run(void** bufs, size_t m, int nsrc, size_t ncopy, int type, int nthreads,
+                           const int* cpus, double seconds, long* iters, double* elapsed);
+void ref_cpu_bench_rank_free(void** bufs, size_t m, int nsrc, size_t ncopy, int type);
 
 #ifdef __cplusplus
 }

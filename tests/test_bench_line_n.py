@@ -130,13 +130,18 @@ def test_stand_in_ranks_line(visible):
         assert roof["bound"] == "xgmi" and roof["links"] == 1
     assert cpu["value"] > 0 and cpu["unit"] == "GB/s" and cpu["kind"] == "port"
     assert cpu["cores"] >= 1 and "checked bit-exactly" in cpu["sample"]
+    # configs 4 and 5 beside it (bf16 bucket on the baseline cores, f16 LL bucket on one core)
+    oc = cpu["other_configs"]
+    assert oc["config4_rs_ag_bf16"]["value"] > 0 and "bf16" in oc["config4_rs_ag_bf16"]["sample"]
+    assert oc["config5_ll_f16"]["value"] > 0 and oc["config5_ll_f16"]["cores"] == 1
     assert res[1][2] is None  # only rank 0 measures the host
 
 
-def test_cpu_rank_shape_checks_every_pass():
+@pytest.mark.parametrize("dtype", [7, 6, 9])  # f32, f16, bf16
+def test_cpu_rank_shape_checks_every_pass(dtype):
     from oracle import oracle as O
     for nsrc, ncopy in ((2, 0), (3, 3000), (8, 1 << 16)):
-        r = O.cpu_bench_rank(5000, nsrc, ncopy, [0], 0.05)
+        r = O.cpu_bench_rank(5000, nsrc, ncopy, [0, 1], 0.05, dtype=dtype)
         assert r["correct"] and r["iters"] >= 1
 
 
