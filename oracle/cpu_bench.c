@@ -188,9 +188,13 @@ static int run_workers(char** bufs, int nsrc, int type, size_t m, size_t ncopy, 
     w->bar = &bar;
     w->stop = &stop;
   }
+  /* worker 0 is the calling thread: give it back its own affinity after */
+  cpu_set_t own;
+  const int haveOwn = pthread_getaffinity_np(pthread_self(), sizeof(own), &own) == 0;
   for (int t = 1; t < nthreads; t++) pthread_create(&tids[t], NULL, worker, &ws[t]);
   worker(&ws[0]);
   for (int t = 1; t < nthreads; t++) pthread_join(tids[t], NULL);
+  if (haveOwn) pthread_setaffinity_np(pthread_self(), sizeof(own), &own);
   if (elapsed) *elapsed = ws[0].elapsed;  /* thread 0's timed loop (all threads in step) */
   pthread_barrier_destroy(&bar);
   if (iters) *iters = ws[0].iters;

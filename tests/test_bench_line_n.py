@@ -161,3 +161,12 @@ def test_ring_trace_summary():
     assert s["copy"] == pytest.approx(10.0) and s["issue"] == pytest.approx(8.0) and s["drain"] == pytest.approx(2.0)
     assert s["post"] == pytest.approx(0.5) and s["gap"] == pytest.approx(0.5)  # one gap of 1 us over 2 slots
     assert s["payload_GBs_in_copy"] == pytest.approx(round(2 * (1 << 20) / (20.0 * 1e3), 1))
+
+
+def test_cpu_baseline_leaves_the_caller_unpinned():
+    """The bench's calling thread is worker 0 of the host baseline: its own
+    CPU affinity must come back afterwards (a pinned main thread made the next
+    baseline on the N > 1 line see one CPU)."""
+    before = os.sched_getaffinity(0)
+    bench.cpu_baseline_allreduce(1 << 20, 2, 0.1)
+    assert os.sched_getaffinity(0) == before
