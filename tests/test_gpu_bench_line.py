@@ -1,0 +1,45 @@
+"""The N > 1 bench line end to end on the GPU: `bench.py
+--gpus 2` starts its own two rank processes (one per GPU where the box has
+two, sharing the one GPU otherwise) and prints rank 0's line.  The line must
+carry the roofline of the topology it ran on — the device's HBM when the
+ranks share a GPU, the ring set's xGMI ceiling when each has its own — with
+frac <= 1 on a shared device, a checked host-core baseline for configs 3, 4
+and 5, and a correct verdict for every timed path."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_two_rank_line_roofline_and_cpu_baseline():
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("VCCL_ALLOW_SHARED_DEVICE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--bytes", str(64 << 20), "--no-extras", "--no-initall"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["unit"] == "GB/s" and line["value"] > 0
+    assert line["correct"]["all"] is True, line["correct"]
+    rpd = line["config"]["devices"]["ranks_per_device"]
+    roof = line["roofline"]
+    if rpd > 1:
+        assert roof["bound"] == "hbm" and 0 < roof["frac"] <= 1, roof
+    else:
+        assert roof["bound"] == "xgmi" and roof["links"] == 1, roof
+    cpu = line["cpu_baseline"]
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port", cpu
+    assert "checked bit-exactly" in cpu["sample"]
+    for name in ("config4_rs_ag_bf16", "config5_ll_f16"):
+        assert cpu["other_configs"][name]["value"] > 0, cpu["other_configs"]
