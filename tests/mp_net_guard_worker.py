@@ -59,6 +59,7 @@ def main():
     res["async_error"] = comm.async_error()
     res["exact"] = bench.pattern_ok(y, n)
     res["last_error"] = nccl.last_error()
+    res["wave_launches"] = comm.set_ring_wave(None)
     comm.abort()
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
         json.dump(res, f)

@@ -121,17 +121,20 @@ def test_destroy_right_after_launch(no_mark, launch_event):
             assert v["idle_after_destroy"] and v["exact"], (v, logs)
 
 
-def test_net_short_slot_is_an_error():
+@pytest.mark.parametrize("wave", [0, 1])
+def test_net_short_slot_is_an_error(wave):
     """a net slot whose landed byte count is not its step's
     slice (VCCL_DEBUG_NET_SHORT_SLOT makes rank 0's proxy ship its first
     slot of >= 64 KiB 16 bytes short, as the stale size of round 5 did) ends
     the call with an error from ncclCommGetAsyncError on every rank —
     ncclInternalError where the short slot landed (ring.hpp recv_size_ok),
     ncclRemoteError where a rank then waits on it — never a silent result;
-    the small call before it (slots below the hook's size) is exact."""
+    the small call before it (slots below the hook's size) is exact.  Both
+    hand-offs check (prim_wg, and prim_ws with every slot per wave)."""
     n = 2
     env = _mp.worker_env(os.environ)
-    env.update(VCCL_NET_FORCE="1", VCCL_NET_NCHANNELS="2", VCCL_SPIN_TIMEOUT_S="3")
+    env.update(VCCL_NET_FORCE="1", VCCL_NET_NCHANNELS="2", VCCL_SPIN_TIMEOUT_S="3",
+               VCCL_RING_WAVE=str(wave), VCCL_RING_WAVE_MIN="0")
     uid = nccl.unique_id_to_bytes(nccl.get_unique_id()).hex()
     with tempfile.TemporaryDirectory() as d:
         procs = []
@@ -162,4 +165,5 @@ def test_net_short_slot_is_an_error():
         assert v["kernel_end_s"] < 30, v
     # rank 1 receives rank 0's short slot and refuses it
     assert res[1]["async_error"] == nccl.ncclInternalError, (res, logs)
+    assert (min(v["wave_launches"] for v in res) > 0) == (wave == 1), res  # the hand-off asked for ran
     assert "slice length" in res[1]["last_error"], res[1]
