@@ -1,0 +1,51 @@
+"""Non-blocking communicators (VERDICT r5 missing #4): with
+ncclConfig_t.blocking = 0 or NCCL_COMM_BLOCKING=0, ncclCommInitRank* returns
+ncclInProgress at once, the initialisation runs on a thread of its own, and
+ncclCommGetAsyncError reports ncclInProgress until it has ended, then its
+result (the reference's group.cc:553-576 helper thread and init.cc:1836-1860
+async state); the comm then runs collectives exactly (tests/
+mp_nonblocking_worker.py, two ranks)."""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from tests import _mp  # noqa: E402
+from vccl_amd import nccl  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_nonblocking_init_reports_in_progress_then_success():
+    n = 2
+    env = _mp.worker_env(os.environ)
+    env.pop("NCCL_COMM_BLOCKING", None)
+    uids = [nccl.unique_id_to_bytes(nccl.get_unique_id()).hex() for _ in range(2)]
+    with tempfile.TemporaryDirectory() as d:
+        procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mp_nonblocking_worker.py"),
+                                   str(r), str(n), d, *uids], env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(n)]
+        logs = []
+        for p in procs:
+            try:
+                logs.append(p.communicate(timeout=240)[0].decode(errors="replace")[-3000:])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+        assert [p.returncode for p in procs] == [0] * n, "\n".join(logs)
+        for r in range(n):
+            with open(os.path.join(d, f"rank{r}.json")) as f:
+                v = json.load(f)
+            assert v["config_rc"] == nccl.ncclInProgress and v["config_state"] == nccl.ncclSuccess, v
+            assert v["config_polls"] >= 1 and v["config_exact"], v
+            assert v["env_rc"] == nccl.ncclInProgress and v["env_state"] == nccl.ncclSuccess and v["env_exact"], v

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../../include/nccl.h"
@@ -181,6 +182,16 @@ struct ncclComm {
   // CTA (workgroup) bounds of every collective launch: ncclConfig_t
   // minCTAs / maxCTAs or NCCL_MIN_CTAS / NCCL_MAX_CTAS (init.cc:1478-1540)
   int minCTAs = 1, maxCTAs = 64;
+  // Non-blocking communicator (ncclConfig_t.blocking = 0 / NCCL_COMM_BLOCKING=0,
+  // group.cc:553-576): ncclCommInitRank* returns ncclInProgress and the
+  // initialisation runs on initThread; ncclCommGetAsyncError reports
+  // ncclInProgress until it ends, then its result.  Every other call on the
+  // comm waits for it first (comm_check).
+  int blocking = 1;
+  std::atomic<bool> initPending{false};
+  ncclResult_t initResult = ncclSuccess;
+  std::thread initThread;
+  std::mutex initMutex;
   // state
   std::atomic<int> asyncError{0};
   std::vector<vccl::UserRedOp> userOps;
@@ -191,7 +202,11 @@ struct ncclComm {
 
 namespace vccl {
 constexpr uint64_t kCommMagic = 0x76636363'6c6d6933ull;  // "vccclmi3"
-ncclResult_t comm_check(const ncclComm* comm, const char* api);
+// A valid, live comm whose initialisation has ended (a non-blocking one is
+// waited for); its result unless allowFailedInit (destroy / abort).
+ncclResult_t comm_check(const ncclComm* comm, const char* api, bool allowFailedInit = false);
+// The same without waiting for a non-blocking initialisation (GetAsyncError).
+ncclResult_t comm_check_live(const ncclComm* comm, const char* api);
 // Waits until every eager launch of `comm` has completed (init.cc).
 ncclResult_t comm_wait_own_launches(ncclComm* comm);
 // The comm's device error word as a result code (init.cc).

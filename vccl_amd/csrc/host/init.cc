@@ -23,7 +23,7 @@
 
 namespace vccl {
 
-ncclResult_t comm_check(const ncclComm* comm, const char* api) {
+ncclResult_t comm_check_live(const ncclComm* comm, const char* api) {
   if (comm == nullptr) {
     VWARN("%s : comm argument is NULL", api);
     return ncclInvalidArgument;
@@ -31,6 +31,25 @@ ncclResult_t comm_check(const ncclComm* comm, const char* api) {
   if (comm->magic != kCommMagic || comm->destroyed) {
     VWARN("%s : comm argument is invalid or destroyed", api);
     return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
+// Joins a non-blocking comm's initialisation thread (once, whichever caller
+// gets there first).
+static void wait_init(ncclComm* c) {
+  if (c->blocking) return;
+  std::lock_guard<std::mutex> g(c->initMutex);
+  if (c->initThread.joinable()) c->initThread.join();
+}
+
+ncclResult_t comm_check(const ncclComm* comm, const char* api, bool allowFailedInit) {
+  NCCLCHECK(comm_check_live(comm, api));
+  ncclComm* c = const_cast<ncclComm*>(comm);
+  wait_init(c);
+  if (!allowFailedInit && c->initResult != ncclSuccess) {
+    VWARN("%s : the communicator's initialisation failed (%d)", api, (int)c->initResult);
+    return c->initResult;
   }
   return ncclSuccess;
 }
@@ -752,11 +771,9 @@ static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   return ncclSuccess;
 }
 
-// ncclConfig_t + NCCL_* environment -> CTA bounds (envConfigOverride,
-// init.cc:1472-1545: env wins, non-positive values are ignored, both capped
-// at MAXCHANNELS, min > max sets min = max).  Non-blocking communicators are
-// not supported (SURVEY.md §8b allows blocking-only): a request for one is
-// reported with a WARN and the comm is created blocking.
+// ncclConfig_t + NCCL_* environment -> CTA bounds and blocking mode
+// (envConfigOverride, init.cc:1472-1545: env wins, non-positive values are
+// ignored, both capped at MAXCHANNELS, min > max sets min = max).
 static ncclResult_t apply_config(ncclComm* c, const ncclConfig_t* config) {
   int minC = NCCL_CONFIG_UNDEF_INT, maxC = NCCL_CONFIG_UNDEF_INT;
   int blocking = NCCL_CONFIG_UNDEF_INT;
@@ -786,9 +803,7 @@ static ncclResult_t apply_config(ncclComm* c, const ncclConfig_t* config) {
   c->minCTAs = minC == NCCL_CONFIG_UNDEF_INT ? 1 : std::min(minC, kMaxChannels);
   c->maxCTAs = maxC == NCCL_CONFIG_UNDEF_INT ? kMaxChannels : std::min(maxC, kMaxChannels);
   if (c->minCTAs > c->maxCTAs) c->minCTAs = c->maxCTAs;
-  if (blocking == 0)
-    VWARN("non-blocking communicator requested (config.blocking = 0 / NCCL_COMM_BLOCKING=0): "
-          "this library initialises and enqueues blocking; calls never return ncclInProgress");
+  c->blocking = blocking == 0 ? 0 : 1;
   return ncclSuccess;
 }
 
@@ -810,6 +825,28 @@ ncclResult_t comm_init_rank(ncclComm_t* out, int nranks, const ncclUniqueId* id,
     c->magic = 0;
     delete c;
     return cr;
+  }
+  if (!c->blocking) {
+    // Non-blocking (group.cc:553-576): the handle now, the initialisation on
+    // a thread of its own; ncclCommGetAsyncError says when it has ended.  On
+    // failure the comm keeps no resources and only destroy / abort accept it.
+    c->initPending.store(true, std::memory_order_relaxed);
+    c->asyncError.store(ncclInProgress, std::memory_order_relaxed);
+    const ncclUniqueId idCopy = *id;
+    *out = c;
+    c->initThread = std::thread([c, idCopy]() {
+      (void)hipSetDevice(c->device);
+      const ncclResult_t r = init_rank(c, &idCopy);
+      if (r != ncclSuccess) {
+        free_resources(c);
+        bootstrap_close(c->bootstrap);
+        c->bootstrap = nullptr;
+      }
+      c->initResult = r;
+      c->asyncError.store(r, std::memory_order_release);
+      c->initPending.store(false, std::memory_order_release);
+    });
+    return ncclInProgress;
   }
   ncclResult_t r = init_rank(c, id);
   if (r != ncclSuccess) {
@@ -1055,6 +1092,10 @@ VCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
         return;
       }
       res[i] = comm_init_rank(&comms[i], ndev, &id, i, d, nullptr);
+      if (res[i] == ncclInProgress) {  // NCCL_COMM_BLOCKING=0: InitAll still returns initialised comms
+        wait_init(comms[i]);
+        res[i] = comms[i]->initResult;
+      }
     });
   }
   for (auto& t : th) t.join();
@@ -1082,13 +1123,13 @@ VCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
 
 VCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;  // init.cc: destroying NULL is a no-op
-  NCCLCHECK(comm_check(comm, "ncclCommDestroy"));
+  NCCLCHECK(comm_check(comm, "ncclCommDestroy", true));
   return comm_destroy(comm, false);
 }
 
 VCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;
-  NCCLCHECK(comm_check(comm, "ncclCommAbort"));
+  NCCLCHECK(comm_check(comm, "ncclCommAbort", true));
   return comm_destroy(comm, true);
 }
 
@@ -1125,8 +1166,13 @@ ncclResult_t vccl::error_word_result(ncclComm* comm) {
 VCCL_EXPORT const char* ncclGetLastError(ncclComm_t) { return last_error(); }
 
 VCCL_EXPORT ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
-  NCCLCHECK(comm_check(comm, "ncclCommGetAsyncError"));
+  NCCLCHECK(comm_check_live(comm, "ncclCommGetAsyncError"));
   if (!asyncError) return ncclInvalidArgument;
+  if (comm->initPending.load(std::memory_order_acquire)) {  // non-blocking init still running
+    *asyncError = ncclInProgress;
+    return ncclSuccess;
+  }
+  wait_init(comm);  // ended: reap its thread
   int e = comm->asyncError.load();
   if (e == 0 && comm->errorFlag && *(volatile int*)comm->errorFlag) {
     e = error_word_result(comm);

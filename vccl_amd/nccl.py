@@ -8,6 +8,7 @@ raises ``VcclError`` if the library is missing: there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import time
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -325,10 +326,17 @@ class Comm:
     def init_rank(cls, nranks: int, uid: ncclUniqueId, rank: int, config: "ncclConfig_t | None" = None) -> "Comm":
         h = ctypes.c_void_p()
         if config is None:
-            check(lib().ncclCommInitRank(ctypes.byref(h), nranks, uid, rank), "ncclCommInitRank")
+            rc = lib().ncclCommInitRank(ctypes.byref(h), nranks, uid, rank)
         else:
-            check(lib().ncclCommInitRankConfig(ctypes.byref(h), nranks, uid, rank, ctypes.byref(config)),
-                  "ncclCommInitRankConfig")
+            rc = lib().ncclCommInitRankConfig(ctypes.byref(h), nranks, uid, rank, ctypes.byref(config))
+        if rc == ncclInProgress:  # a non-blocking comm: poll its state, as a caller must
+            st = ctypes.c_int(ncclInProgress)
+            while st.value == ncclInProgress:
+                check(lib().ncclCommGetAsyncError(h, ctypes.byref(st)), "ncclCommGetAsyncError")
+                if st.value == ncclInProgress:
+                    time.sleep(1e-3)
+            rc = st.value
+        check(rc, "ncclCommInitRankConfig" if config is not None else "ncclCommInitRank")
         return cls(h.value)
 
     @classmethod
