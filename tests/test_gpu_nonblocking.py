@@ -49,3 +49,36 @@ def test_nonblocking_init_reports_in_progress_then_success():
             assert v["config_rc"] == nccl.ncclInProgress and v["config_state"] == nccl.ncclSuccess, v
             assert v["config_polls"] >= 1 and v["config_exact"], v
             assert v["env_rc"] == nccl.ncclInProgress and v["env_state"] == nccl.ncclSuccess and v["env_exact"], v
+
+
+_ABORT_PENDING = r"""
+import ctypes, json, sys, time
+sys.path.insert(0, %r)
+import torch
+from vccl_amd import nccl
+torch.cuda.set_device(0)
+uid = nccl.get_unique_id()  # the root lives here; rank 1 never comes
+cfg = nccl.ncclConfig_t.initializer(blocking=0)
+h = ctypes.c_void_p()
+rc = nccl.lib().ncclCommInitRankConfig(ctypes.byref(h), 2, uid, 0, ctypes.byref(cfg))
+time.sleep(1.0)
+st = ctypes.c_int(-1)
+nccl.lib().ncclCommGetAsyncError(h, ctypes.byref(st))
+t0 = time.monotonic()
+rc_abort = nccl.lib().ncclCommAbort(h)
+print(json.dumps({"rc": rc, "state_before": st.value, "rc_abort": rc_abort,
+                  "abort_s": round(time.monotonic() - t0, 2)}))
+"""
+
+
+def test_abort_ends_a_pending_nonblocking_init():
+    """ncclCommAbort on a non-blocking comm whose initialisation waits for a
+    peer that never comes (a 2-rank comm, rank 1 absent): the bootstrap
+    socket is shut, the init thread ends, abort returns within seconds — not
+    after the 600 s bootstrap timeout."""
+    p = subprocess.run([sys.executable, "-c", _ABORT_PENDING % ROOT], capture_output=True, text=True,
+                       timeout=120, env=_mp.worker_env(os.environ))
+    assert p.returncode == 0, p.stderr[-3000:]
+    v = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert v["rc"] == nccl.ncclInProgress and v["state_before"] == nccl.ncclInProgress, v
+    assert v["rc_abort"] == nccl.ncclSuccess and v["abort_s"] < 10, v

@@ -185,7 +185,8 @@ ncclResult_t bootstrap_get_unique_id(ncclUniqueId* id) {
   return ncclSuccess;
 }
 
-ncclResult_t bootstrap_init(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out) {
+ncclResult_t bootstrap_init(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out,
+                            const std::atomic<bool>* abortReq) {
   IdLayout L;
   memcpy(&L, id->internal, sizeof(L));
   if (L.magic != kIdMagic) {
@@ -204,6 +205,10 @@ ncclResult_t bootstrap_init(const ncclUniqueId* id, int rank, int nranks, Bootst
     if (std::chrono::steady_clock::now() > deadline) {
       VWARN("bootstrap: cannot reach root");
       return ncclSystemError;
+    }
+    if (abortReq && abortReq->load()) {
+      VWARN("bootstrap: aborted before the root was reached");
+      return ncclRemoteError;
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(10));
   }
@@ -228,6 +233,8 @@ ncclResult_t bootstrap_allgather(Bootstrap* b, void* buf, size_t bytes) {
   if (!recv_all(b->fd, buf, bytes * (size_t)b->nranks)) return ncclSystemError;
   return ncclSuccess;
 }
+
+int bootstrap_fd(const Bootstrap* b) { return b ? b->fd : -1; }
 
 ncclResult_t bootstrap_barrier(Bootstrap* b) {
   std::vector<char> tmp((size_t)b->nranks);

@@ -59,7 +59,11 @@ int64_t param_int(const char* name, int64_t deflt);
 // ----------------------------------------------------------------- bootstrap
 struct Bootstrap;  // opaque (bootstrap.cc)
 ncclResult_t bootstrap_get_unique_id(ncclUniqueId* id);
-ncclResult_t bootstrap_init(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out);
+// The socket to the root (ncclCommAbort shuts it to end a pending init).
+int bootstrap_fd(const Bootstrap* b);
+// `abortReq` (optional): stop retrying the root when it is raised.
+ncclResult_t bootstrap_init(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out,
+                            const std::atomic<bool>* abortReq = nullptr);
 // allgather of `bytes` per rank: buf holds nranks*bytes, own slot filled in.
 ncclResult_t bootstrap_allgather(Bootstrap* b, void* buf, size_t bytes);
 ncclResult_t bootstrap_barrier(Bootstrap* b);
@@ -189,6 +193,11 @@ struct ncclComm {
   // comm waits for it first (comm_check).
   int blocking = 1;
   std::atomic<bool> initPending{false};
+  // ncclCommAbort of a pending non-blocking init: raise initAbort, shut the
+  // bootstrap socket (initFd, published once connected) so a wait on peers
+  // that never come ends at once
+  std::atomic<bool> initAbort{false};
+  std::atomic<int> initFd{-1};
   ncclResult_t initResult = ncclSuccess;
   std::thread initThread;
   std::mutex initMutex;

@@ -7,6 +7,7 @@
 // (SURVEY.md Appendix D); each channel's FIFO and flags live in the receiver's
 // HBM (uncached) and are mapped into the sender by hipIpc* (multi-process) or
 // peer access (single process).
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -294,7 +295,14 @@ static ncclResult_t map_peer(ncclComm* c, const PeerMap& me, const PeerMap& p, i
 
 static ncclResult_t init_rank(ncclComm* c, const ncclUniqueId* id) {
   VINFO("rank %d/%d dev %d: bootstrap", c->rank, c->nRanks, c->device);
-  NCCLCHECK(bootstrap_init(id, c->rank, c->nRanks, &c->bootstrap));
+  NCCLCHECK(bootstrap_init(id, c->rank, c->nRanks, &c->bootstrap, &c->initAbort));
+  // an abort of a pending non-blocking init shuts this socket (ncclCommAbort);
+  // publish first, then look at the flag, so one of the two sides sees the other
+  c->initFd.store(bootstrap_fd(c->bootstrap));
+  if (c->initAbort.load()) {
+    VWARN("rank %d: communicator initialisation aborted", c->rank);
+    return ncclRemoteError;
+  }
   const int n = c->nRanks;
   const auto rings = ring_orders(n);
   const int nRings = (int)rings.size();
@@ -837,11 +845,9 @@ ncclResult_t comm_init_rank(ncclComm_t* out, int nranks, const ncclUniqueId* id,
     c->initThread = std::thread([c, idCopy]() {
       (void)hipSetDevice(c->device);
       const ncclResult_t r = init_rank(c, &idCopy);
-      if (r != ncclSuccess) {
-        free_resources(c);
-        bootstrap_close(c->bootstrap);
-        c->bootstrap = nullptr;
-      }
+      // on failure the bootstrap socket stays open until destroy / abort
+      // closes it: an abort may still be shutting it down (initFd)
+      if (r != ncclSuccess) free_resources(c);
       c->initResult = r;
       c->asyncError.store(r, std::memory_order_release);
       c->initPending.store(false, std::memory_order_release);
@@ -1129,6 +1135,15 @@ VCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
 
 VCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;
+  NCCLCHECK(comm_check_live(comm, "ncclCommAbort"));
+  if (comm->initPending.load()) {
+    // a non-blocking init still running (init.cc commAbort of an initialising
+    // comm): stop it — no more root retries, and the bootstrap socket shut so
+    // a wait on peers that never come returns at once
+    comm->initAbort.store(true);
+    const int fd = comm->initFd.load();
+    if (fd >= 0) (void)shutdown(fd, SHUT_RDWR);
+  }
   NCCLCHECK(comm_check(comm, "ncclCommAbort", true));
   return comm_destroy(comm, true);
 }
