@@ -6,8 +6,10 @@ VCCL's reduction semantics, see ``reduce_ref.h``).  Only ``tests/``,
 this module; the product path (``vccl_amd``) never does.
 
 Parity status: dispatch table pinned by the reference's ``generate.py``; the
-arithmetic is pinned against numpy/torch IEEE implementations only (CUDA's
-fp16/bf16 intrinsic headers are not in /root/reference) — see DESIGN.md.
+arithmetic is pinned to the reference's own fallback expressions (widen, one
+binary32 op, RN-even narrowing; reduce_kernel.h:276-296) evaluated by numpy /
+torch IEEE implementations — no reference-produced fixture exists (CUDA's
+fp16/bf16 intrinsic headers are not in /root/reference); see DESIGN.md §2.
 """
 from __future__ import annotations
 

@@ -14,9 +14,13 @@
  * Parity status: the dispatch/type table is pinned against the reference's own
  * generate.py output (tests/golden/gen_functable.py).  The fp16/bf16 arithmetic
  * comes from CUDA's cuda_fp16.h / cuda_bf16.h intrinsics, which are not vendored
- * in /root/reference and not present in this image, so the ARITHMETIC is pinned
- * only against independent IEEE-754 implementations (numpy, torch-CPU) through
- * tests/golden/reduce_golden.npz — reference arithmetic itself: parity unpinned.
+ * in /root/reference and not present in this image, and no reference-produced
+ * fixture exists.  The ARITHMETIC is pinned to the reference's own fallback
+ * expressions (reduce_kernel.h:276-277, 285, 294-296: widen, one binary32 op,
+ * round RN-even), evaluated by independent IEEE-754 implementations (numpy,
+ * torch-CPU) in tests/golden/reduce_golden.npz; the intrinsic branch gives the
+ * same bits by the innocuous-double-rounding bound (24 >= 2p + 2 for binary16
+ * and bfloat16).  Open: FTZ of subnormals, NaN payloads.
  */
 #ifndef VCCL_ORACLE_REDUCE_REF_H_
 #define VCCL_ORACLE_REDUCE_REF_H_
