@@ -230,3 +230,65 @@ def test_fp8_avg_scalar_encoding():
             dev_op, arg = O.host_to_dev_redop(4, t, n)
             ref = torch.tensor([1.0 / n], dtype=torch.float32).to(FP8_TORCH[t]).view(torch.uint8).item()
             assert (dev_op, arg) == (3, ref)
+
+
+# ---- the reference's two arithmetic branches agree ----------
+# reduce_kernel.h computes f16 / bf16 sums and products either with the
+# intrinsics (__hadd / __hmul: correctly rounded) or, on older architectures,
+# as widen -> one binary32 op -> RN-even narrowing (:276-277, :294-296) — what
+# the golden vectors and the oracle compute.  The two agree because double
+# rounding through binary32 is innocuous for binary16 and bfloat16 (p' = 24 >=
+# 2p + 2).  Checked here on every finite f16 / bf16 value against a spread of
+# partners (subnormals, large exponent gaps, cancellation) and random pairs.
+def _partners(vals, rng, k):
+    fin = vals[np.isfinite(vals.astype(np.float64))]
+    return np.concatenate([fin[rng.integers(0, fin.size, k - 8)],
+                           np.array([0.0, -0.0, 1.0, -1.0, 65504.0, -65504.0, 6e-8, -6e-8],
+                                    dtype=vals.dtype)])
+
+
+def _rn_f16_from_f64(x):
+    return x.astype(np.float16)  # numpy's double -> half conversion rounds once (RN-even)
+
+
+def _round_to_odd_f32(x):
+    """binary64 -> binary32 rounding to odd (exact, or the truncation with its
+    last bit set): a following RN-even rounding to bf16 is then the correct
+    rounding of x (24 >= 8 + 2)."""
+    y = x.astype(np.float32)
+    inexact = y.astype(np.float64) != x
+    over = inexact & (np.abs(y.astype(np.float64)) > np.abs(x))
+    y = np.where(over, np.nextafter(y, np.float32(0)), y)
+    bits = y.view(np.uint32) | inexact.astype(np.uint32)
+    return bits.view(np.float32)
+
+
+def test_f16_fallback_equals_correct_rounding():
+    rng = np.random.default_rng(77)
+    allh = np.arange(1 << 16, dtype=np.uint16).view(np.float16)
+    allh = allh[np.isfinite(allh)]
+    b = _partners(allh, rng, 48)
+    A = np.repeat(allh, b.size)
+    B = np.tile(b, allh.size)
+    with np.errstate(over="ignore", invalid="ignore"):
+        for op in (np.add, np.multiply):
+            fallback = op(A.astype(np.float32), B.astype(np.float32)).astype(np.float16)
+            exact = _rn_f16_from_f64(op(A.astype(np.float64), B.astype(np.float64)))  # exact in binary64
+            assert np.array_equal(fallback.view(np.uint16), exact.view(np.uint16)), op
+
+
+def test_bf16_fallback_equals_correct_rounding():
+    rng = np.random.default_rng(78)
+    allb = torch.arange(1 << 16, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    allb = allb[torch.isfinite(allb)]
+    vals = allb.float().numpy()
+    idx = rng.integers(0, vals.size, 40)
+    b = np.concatenate([vals[idx], np.array([0.0, -0.0, 1.0, -1.0, 1e-38, -1e-38, 3e38, -3e38], np.float32)])
+    A = np.repeat(vals, b.size).astype(np.float64)
+    B = np.tile(b, vals.size).astype(np.float64)
+    with np.errstate(over="ignore", invalid="ignore"):
+        for op in (np.add, np.multiply):
+            fallback = torch.from_numpy(op(A.astype(np.float32), B.astype(np.float32))).to(torch.bfloat16)
+            # binary64 holds the product exactly and the sum to 53 bits (> 2*8 + 2)
+            exact = torch.from_numpy(_round_to_odd_f32(op(A, B))).to(torch.bfloat16)
+            assert torch.equal(fallback.view(torch.int16), exact.view(torch.int16)), op
