@@ -828,8 +828,10 @@ def _digest(lo, hi):
     dev = torch.cuda.current_device()
     g = _DIGEST.get(dev)
     if g is None or g.numel() < hi:
-        nchunks = -(-hi // _DIGEST_CHUNK)
         have = 0 if g is None else g.numel() // _DIGEST_CHUNK
+        # geometric growth: growing by the chunk would leave every outgrown
+        # buffer cached in torch's allocator (quadratic reserved memory)
+        nchunks = max(-(-hi // _DIGEST_CHUNK), 2 * have)
         new = torch.empty(nchunks * _DIGEST_CHUNK, dtype=torch.uint8, device="cuda")
         if g is not None:
             new[:g.numel()] = g
