@@ -18,6 +18,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -107,8 +108,8 @@ static int run_rank(const Args& a, int rank, ncclUniqueId id, ncclDataType_t dt)
   if (rank == 0) {
     printf("# coll_perf %s  ranks %d  dtype %s  op %s  iters %d  warmup %d (libvccl via include/nccl.h)\n",
            a.coll.c_str(), n, a.dtype.c_str(), a.op.c_str(), a.iters, a.warmup);
-    printf("#%12s %12s %8s %6s %10s %9s %9s %7s\n", "size", "count", "type", "redop", "time(us)",
-           "algbw", "busbw", "#wrong");
+    printf("#%12s %12s %8s %6s %10s %9s %9s %7s %8s\n", "size", "count", "type", "redop", "time(us)",
+           "algbw", "busbw", "#wrong", "host(us)");
   }
   double* tdev;
   CK(hipMalloc(&tdev, sizeof(double)));
@@ -156,7 +157,12 @@ static int run_rank(const Args& a, int rank, ncclUniqueId id, ncclDataType_t dt)
     CK(hipEventCreate(&e1));
     CK(hipStreamSynchronize(s));
     CK(hipEventRecord(e0, s));
+    // host(us): wall time of the enqueue loop alone per call (the host side
+    // of a call; equals time(us) when the host is the bottleneck)
+    const auto h0 = std::chrono::steady_clock::now();
     for (int it = 0; it < a.iters; it++) call();
+    const double hostUs =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count() / a.iters;
     CK(hipEventRecord(e1, s));
     CK(hipStreamSynchronize(s));
     float ms = 0;
@@ -180,9 +186,9 @@ static int run_rank(const Args& a, int rank, ncclUniqueId id, ncclDataType_t dt)
     const double sz = (double)std::max(inElts, outElts) * sizeof(T);
     const double algbw = sz / (us * 1e-6) / 1e9;
     if (rank == 0)
-      printf(" %12zu %12zu %8s %6s %10.2f %9.2f %9.2f %7lld\n", (size_t)sz, collCount,
+      printf(" %12zu %12zu %8s %6s %10.2f %9.2f %9.2f %7lld %8.2f\n", (size_t)sz, collCount,
              a.dtype.c_str(), a.coll == "allgather" || a.coll == "broadcast" ? "none" : a.op.c_str(), us, algbw,
-             algbw * busFactor, wrong);
+             algbw * busFactor, wrong, hostUs);
     CK(hipEventDestroy(e0));
     CK(hipEventDestroy(e1));
     CK(hipFree(in));
