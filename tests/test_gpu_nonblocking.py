@@ -64,10 +64,17 @@ rc = nccl.lib().ncclCommInitRankConfig(ctypes.byref(h), 2, uid, 0, ctypes.byref(
 time.sleep(1.0)
 st = ctypes.c_int(-1)
 nccl.lib().ncclCommGetAsyncError(h, ctypes.byref(st))
+# ncclCommEnsureReady: a comm still initialising is not usable, not waited for
+cnt = ctypes.c_int(-1)
+rc_count = nccl.lib().ncclCommCount(h, ctypes.byref(cnt))
+x = torch.zeros(4, device="cuda")
+rc_ar = nccl.lib().ncclAllReduce(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(x.data_ptr()), ctypes.c_size_t(4),
+                                 nccl.ncclFloat32, nccl.ncclSum, h, ctypes.c_void_p(0))
+rc_destroy = nccl.lib().ncclCommDestroy(h)
 t0 = time.monotonic()
 rc_abort = nccl.lib().ncclCommAbort(h)
-print(json.dumps({"rc": rc, "state_before": st.value, "rc_abort": rc_abort,
-                  "abort_s": round(time.monotonic() - t0, 2)}))
+print(json.dumps({"rc": rc, "state_before": st.value, "rc_count": rc_count, "rc_ar": rc_ar,
+                  "rc_destroy": rc_destroy, "rc_abort": rc_abort, "abort_s": round(time.monotonic() - t0, 2)}))
 """
 
 
@@ -75,10 +82,13 @@ def test_abort_ends_a_pending_nonblocking_init():
     """ncclCommAbort on a non-blocking comm whose initialisation waits for a
     peer that never comes (a 2-rank comm, rank 1 absent): the bootstrap
     socket is shut, the init thread ends, abort returns within seconds — not
-    after the 600 s bootstrap timeout."""
+    after the 600 s bootstrap timeout.  Before that, every other use of the
+    comm fails at once with ncclInvalidArgument, as the reference's
+    ncclCommEnsureReady makes it (init.cc:300-317; destroy too, :2066)."""
     p = subprocess.run([sys.executable, "-c", _ABORT_PENDING % ROOT], capture_output=True, text=True,
                        timeout=120, env=_mp.worker_env(os.environ))
     assert p.returncode == 0, p.stderr[-3000:]
     v = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert v["rc"] == nccl.ncclInProgress and v["state_before"] == nccl.ncclInProgress, v
+    assert v["rc_count"] == v["rc_ar"] == v["rc_destroy"] == nccl.ncclInvalidArgument, v
     assert v["rc_abort"] == nccl.ncclSuccess and v["abort_s"] < 10, v

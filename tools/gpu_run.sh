@@ -35,7 +35,7 @@ for s in "$@"; do
   echo "== $s $(date +%T)"
   case $s in
     test) timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 ;;
-    test:*) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#test:}" > $O/pytest_${s#test:}.log 2>&1 ;;
+    test:*) lg=$(printf %s "${s#test:}" | tr -c 'A-Za-z0-9_' '_'); timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#test:}" > "$O/pytest_$lg.log" 2>&1 ;;
     bench) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err ;;
     prof) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --no-extras > $O/bench_prof.json 2> $O/bench_prof.err) ;;
     n2) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 > $O/bench_n2.json 2> $O/bench_n2.err ;;

@@ -44,9 +44,17 @@ static void wait_init(ncclComm* c) {
   if (c->initThread.joinable()) c->initThread.join();
 }
 
+// ncclCommEnsureReady (init.cc:300-317): a comm whose non-blocking
+// initialisation has not ended is not usable yet — every call but
+// ncclCommGetAsyncError and ncclCommAbort fails with ncclInvalidArgument
+// (ncclCommDestroy too, init.cc:2066), it does not wait.
 ncclResult_t comm_check(const ncclComm* comm, const char* api, bool allowFailedInit) {
   NCCLCHECK(comm_check_live(comm, api));
   ncclComm* c = const_cast<ncclComm*>(comm);
+  if (!c->blocking && c->initPending.load(std::memory_order_acquire)) {
+    VWARN("%s : Attempt to use communicator before the previous operation returned ncclSuccess", api);
+    return ncclInvalidArgument;
+  }
   wait_init(c);
   if (!allowFailedInit && c->initResult != ncclSuccess) {
     VWARN("%s : the communicator's initialisation failed (%d)", api, (int)c->initResult);
@@ -1144,7 +1152,7 @@ VCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
     const int fd = comm->initFd.load();
     if (fd >= 0) (void)shutdown(fd, SHUT_RDWR);
   }
-  NCCLCHECK(comm_check(comm, "ncclCommAbort", true));
+  wait_init(comm);  // the init thread ends promptly once told to
   return comm_destroy(comm, true);
 }
 
