@@ -248,6 +248,10 @@ def bench_reduce_copy(args):
                                       "live_error": why}
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(n)
+        try:
+            out["cpu_baseline"]["staging"] = staging_rates(a, b)
+        except Exception as e:  # noqa: BLE001 - reported, not fatal to the headline
+            out["cpu_baseline"]["staging_error"] = repr(e)
     if not args.no_extras:
         out["extras"] = {"config1_allreduce_1KiB_world1": bench_one_rank_latency()}
         del a, b, d
@@ -531,6 +535,54 @@ def cpu_baseline(n_full, seconds=5.0):
             "nproc": topo["nproc"], "physical_cores": len(topo["physical_cores"]),
             "numa_nodes": topo["numa_nodes"], "sockets": topo["sockets"],
             "cgroup_cpu_quota": q, "machine_cpus": topo["machine_cpus"]}
+
+
+def staging_rates(a, b, reps=5):
+    """SURVEY.md §8(d) staging row, the inter-node analogue (VCCL's net
+    transport without GPUDirect stages FIFO slots through host-pinned buffers,
+    src/transport/net.cc:830-835, 1293-1482): config 2's device bucket `a`
+    moved to pinned host memory (D2H), back (H2D), and end to end D2H -> host
+    2-source f32 sum with a "received" peer bucket (`b`'s values, already in
+    pinned host memory) by the oracle's C reduce-copy -> H2D, checked
+    bitwise against a + b.  GB/s of one bucket per pass (median of `reps`)."""
+    from oracle import oracle as O
+    n = a.numel()
+    nbytes = n * a.element_size()
+    h = torch.empty(n, dtype=a.dtype, pin_memory=True)
+    peer = b.cpu().pin_memory()
+    red = torch.empty(n, dtype=a.dtype, pin_memory=True)
+    out = torch.empty_like(a)
+    threads = min(16, os.cpu_count() or 1)
+
+    def med(fn, k=reps):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    t_d2h = med(lambda: h.copy_(a, non_blocking=True))
+    t_h2d = med(lambda: out.copy_(h, non_blocking=True))
+    hn, pn, rn = h.numpy(), peer.numpy(), red.numpy()
+
+    def staged():
+        h.copy_(a, non_blocking=True)
+        torch.cuda.synchronize()
+        O.reduce_copy(O.DEV_SUM, 7, 0, [hn, pn], out=[rn], nthreads=threads)
+        out.copy_(red, non_blocking=True)
+
+    t_st = med(staged, 3)
+    ok = torch.equal(out.view(torch.int32), (a + b).view(torch.int32))
+    del h, peer, red, out
+    return {"bucket_bytes": nbytes, "d2h_GBs": round(nbytes / t_d2h / 1e9, 2),
+            "h2d_GBs": round(nbytes / t_h2d / 1e9, 2), "staged_reduce_GBs": round(nbytes / t_st / 1e9, 2),
+            "host_threads": threads, "correct": bool(ok),
+            "note": "staged = D2H + host 2-src f32 sum (oracle C, pthreads) + H2D of one 256 MiB bucket, "
+                    "end to end; pinned host buffers (SURVEY §8d staging row)"}
 
 
 def _baseline_cpus():

@@ -43,3 +43,17 @@ def test_two_rank_line_roofline_and_cpu_baseline():
     assert "checked bit-exactly" in cpu["sample"]
     for name in ("config4_rs_ag_bf16", "config5_ll_f16"):
         assert cpu["other_configs"][name]["value"] > 0, cpu["other_configs"]
+
+
+def test_staging_row_checked():
+    """SURVEY §8(d)'s staging row (D2H, H2D, D2H -> host sum -> H2D) as the
+    N = 1 line's cpu_baseline carries it, on a 16 MiB bucket: rates positive
+    and the staged sum bitwise equal to the device's a + b."""
+    sys.path.insert(0, ROOT)
+    import bench
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = torch.rand(4 << 20, device="cuda", generator=g) * 2 - 1
+    b = torch.rand(4 << 20, device="cuda", generator=g) * 2 - 1
+    r = bench.staging_rates(a, b, reps=2)
+    assert r["correct"] is True and r["bucket_bytes"] == 16 << 20, r
+    assert min(r["d2h_GBs"], r["h2d_GBs"], r["staged_reduce_GBs"]) > 0, r

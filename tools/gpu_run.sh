@@ -21,6 +21,8 @@
 #        lll:<n>[q<k>]  tools/ll_latency.py on n ranks, GPU_MAX_HW_QUEUES=k (4)
 #        lltrace:<n> the same under rocprofv3 kernel + HIP API trace per rank, tools/ll_trace.py summary
 #        ll1p:<n>  the LL all-reduce with n ranks in ONE process (tools/ll_latency_1proc.py)
+#        net:<n>   tools/net_rate.py on n ranks (xGMI ring vs the net proxy path,
+#                  staging copies included)
 #        fuzz:<n>[s<seed>]  tools/fuzz_coll.py on n ranks (random calls, paths,
 #                  groups; bit-exact; FUZZ_SECONDS 240, FUZZ_ITERS 400)
 # Outputs go to gpurun_out/<label>/.  Every GPU step has its own time limit
@@ -52,6 +54,7 @@ for s in "$@"; do
     lll:*) n=${s#lll:}; q=${n#*q}; n=${n%q*}; [ "$q" = "$n" ] && q=4; GPU_MAX_HW_QUEUES=$q timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29537 tools/ll_latency.py > $O/lll_n${n}_q${q}.json 2> $O/lll_n${n}_q${q}.err ;;
     lltrace:*) n=${s#lltrace:}; MP_PROF_SCRIPT=tools/ll_latency.py MP_PROF_FLAGS=--hip-runtime-trace timeout -k 10 600 python -u tools/mp_prof.py $n $O/lltrace_n$n > $O/lltrace_n$n.log 2>&1 && python tools/ll_trace.py $O/lltrace_n$n > $O/lltrace_n$n.json ;;
     ll1p:*) VCCL_ALLOW_SHARED_DEVICE=1 timeout -k 10 300 python -u tools/ll_latency_1proc.py ${s#ll1p:} > $O/ll1p_n${s#ll1p:}.json 2> $O/ll1p_n${s#ll1p:}.err ;;
+    net:*) timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${s#net:} --master-addr 127.0.0.1 --master-port 29539 tools/net_rate.py > $O/net_n${s#net:}.json 2> $O/net_n${s#net:}.err ;;
     fuzz:*) n=${s#fuzz:}; sd=1; case $n in *s*) sd=${n#*s}; n=${n%%s*};; esac; FUZZ_SEED=$sd FUZZ_ITERS=${FUZZ_ITERS:-400} FUZZ_SECONDS=${FUZZ_SECONDS:-240} timeout -k 10 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29538 tools/fuzz_coll.py > $O/fuzz_n${n}_s${sd}.json 2> $O/fuzz_n${n}_s${sd}.err ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
