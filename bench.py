@@ -1133,6 +1133,7 @@ def bench_allreduce(args):
     xgmi = peer_copy_bench(dist, rank, world) if not args.no_peer else None
     sizes = [1 << p for p in range(3, 31)] if args.sweep else [args.bytes or (1 << 30)]
     rows = []
+    call_errs = []
     for S in sizes:
         n = max(1, S // 4)
         g = torch.Generator(device="cuda").manual_seed(1000 + rank)
@@ -1141,7 +1142,13 @@ def bench_allreduce(args):
         steps = args.steps if S >= (64 << 20) else max(args.steps, 20)
 
         def fn():
-            comm.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+            # a call refused after an async error (ncclInternalError /
+            # ncclRemoteError) is recorded, not raised: every rank must still
+            # reach the same gloo barriers
+            try:
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
+            except nccl.VcclError as e:
+                call_errs.append(e.code)
         dt = _time_coll(dist, fn, steps, args.warmup)
         algbw = n * 4 * steps / dt / 1e9
         busbw = algbw * 2 * (world - 1) / world
@@ -1151,12 +1158,20 @@ def bench_allreduce(args):
         if rank == 0 and args.sweep:
             print(f"# allreduce {n*4:>12d} B  {dt/steps*1e6:10.1f} us  algbw {algbw:8.2f}  "
                   f"busbw {busbw:8.2f} GB/s  {rows[-1]['algo']}", file=sys.stderr, flush=True)
-    extras = None if args.sweep or args.no_extras else bench_extras(dist, comm, rank, world, args)
+    # Fail fast: a spin timeout during the headline timing (the comm's error
+    # word, on any rank) means the path is broken on this topology — every
+    # extras row would open fresh comms and wait out their own timeouts.  The
+    # line is then printed at once with the error and correct: false.
+    e = torch.tensor([comm.async_error() or max(call_errs, default=0)], dtype=torch.int64)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    head_err = int(e.item())
+    full = not args.sweep and not args.no_extras and head_err == 0
+    extras = bench_extras(dist, comm, rank, world, args) if full else None
     # Correctness of everything timed above, on this topology (fences off and on).
     t_chk = time.perf_counter()
     head = rows[-1]["bytes"]
     plan = {f"ar_default_{head}": ("ar", {"nbytes": head})}
-    if not args.sweep and not args.no_extras:
+    if full:
         for S in EXTRA_F32_SIZES:
             plan[f"ar_default_{S}"] = ("ar", {"nbytes": S})
         for S in EXTRA_F16_SIZES:
@@ -1182,12 +1197,16 @@ def bench_allreduce(args):
             for algo in (None, "ring"):
                 plan[f"rs_ag_f32_{algo or 'default'}_{S}"] = ("rs_ag", {"nbytes": S, "dtype": "f32",
                                                                         "algo": algo})
-    checks = run_checks(dist, comm, rank, world, plan)
+    # after a headline error (the same verdict on every rank) nothing more is
+    # run on the comm: its calls are refused, and a rank that raised would
+    # skip the gloo collectives of a check that its peers still enter
+    checks = (run_checks(dist, comm, rank, world, plan) if head_err == 0
+              else {"check_ms": {}, "fences_off": {}, "fences_on": {}})
     err = comm.async_error()
     n_channels, ring_orders = comm.n_channels(), nccl.ring_orders(world)
     comm.destroy()
     initall = None
-    if not args.no_initall and world > 1 and torch.cuda.device_count() > 1:
+    if not args.no_initall and world > 1 and torch.cuda.device_count() > 1 and head_err == 0:
         # one process drives every GPU while the other ranks wait at the barrier
         initall = initall_check(torch.cuda.device_count()) if rank == 0 else None
         dist.barrier()
@@ -1196,7 +1215,8 @@ def bench_allreduce(args):
     rpd, roof, cpu_base = line_roofline_and_baseline(dist, rank, world, last, torch.cuda.device_count(),
                                                      ring_orders, n_channels, xgmi, cpu=not args.no_cpu)
     line_s = time.perf_counter() - _T_START
-    correct_all = _flatten_ok(checks) and (initall is None or initall.get("ok") is True)
+    correct_all = (_flatten_ok(checks) and (initall is None or initall.get("ok") is True)
+                   and head_err == 0)
     out = {"metric": "device reduce-copy GB/s vs HBM peak; all-reduce busbw at 1/2/4/8 GPUs",
            "value": round(last["busbw"], 2), "unit": "GB/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(last["us"] / 1e3, 4),
@@ -1216,6 +1236,9 @@ def bench_allreduce(args):
            "roofline": roof,
            "cpu_baseline": cpu_base,
            "correct": {"all": correct_all, **checks, "initall_single_process": initall,
+                       "headline_async_error": head_err,
+                       **({"extras_skipped": "async error during the headline timing"}
+                          if head_err and not args.sweep and not args.no_extras else {}),
                        "check_s": round(t_chk, 2), "check_warmup_s": round(check_warmup_s, 3),
                        "line_s": round(line_s, 2),  # bench.py start (imports included) -> here
                        "check_frac": round(t_chk / line_s, 3),

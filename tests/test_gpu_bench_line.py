@@ -45,6 +45,27 @@ def test_two_rank_line_roofline_and_cpu_baseline():
         assert cpu["other_configs"][name]["value"] > 0, cpu["other_configs"]
 
 
+def test_broken_path_line_fails_fast():
+    """A path that fails during the headline timing (here every net slot
+    check trips: VCCL_NET_FORCE + VCCL_DEBUG_NET_SHORT_SLOT, ring.hpp
+    recv_size_ok) still yields a line, at once: correct false, the async
+    error recorded, the extras skipped rather than each fresh comm waiting
+    out its own spin timeout."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update({"VCCL_NET_FORCE": "1", "VCCL_DEBUG_NET_SHORT_SLOT": str(64 << 10),
+                "VCCL_SPIN_TIMEOUT_S": "10"})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--bytes", str(64 << 20), "--no-initall"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    c = line["correct"]
+    assert c["all"] is False and c["headline_async_error"] != 0, c
+    assert "extras_skipped" in c and "extras" not in line, sorted(line)
+    assert line["config"]["async_error"] != 0
+
+
 def test_staging_row_checked():
     """SURVEY §8(d)'s staging row (D2H, H2D, D2H -> host sum -> H2D) as the
     N = 1 line's cpu_baseline carries it, on a 16 MiB bucket: rates positive
