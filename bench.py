@@ -763,6 +763,50 @@ def _dist_setup():
     return dist, rank, world, comm
 
 
+class _Tolerant:
+    """A comm as the extras and the checks drive it: a collective the library
+    refuses once the comm carries an async error (ncclRemoteError after a
+    spin timeout, ncclInternalError after a slot-size check) is recorded in
+    `refused`, not raised.  Ranks see their error words at different calls, so
+    a raise on one rank would skip gloo collectives its peers still enter and
+    hang the line — on the driver's one multi-GPU run the line must always
+    print.  Everything else passes through to the comm."""
+    _COLLS = ("all_reduce", "reduce_scatter", "all_gather", "broadcast", "reduce")
+
+    def __init__(self, comm):
+        self._comm = comm
+        self.refused = 0
+
+    def __getattr__(self, name):
+        attr = getattr(self._comm, name)
+        if name not in self._COLLS:
+            return attr
+
+        def call(*a, **kw):
+            try:
+                attr(*a, **kw)
+            except nccl.VcclError as e:
+                self.refused = self.refused or e.code
+        return call
+
+
+def _group_end():
+    """ncclGroupEnd for the bench's grouped rows: a refused launch is left to
+    the comm's async error (reported), not raised (see _Tolerant)."""
+    try:
+        nccl.group_end()
+    except nccl.VcclError:
+        pass
+
+
+def _any_error(dist, comm):
+    """The largest async error of `comm` over the ranks (a collective: every
+    rank calls it at the same point)."""
+    e = torch.tensor([comm.async_error() or getattr(comm, "refused", 0)], dtype=torch.int64)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    return int(e.item())
+
+
 def _time_coll(dist, fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -1001,7 +1045,7 @@ def check_group(dist, comm, rank, world, nbytes, k):
     nccl.group_start()
     for x, y in zip(xs, ys):
         comm.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32, nccl.ncclSum, sp)
-    nccl.group_end()
+    _group_end()
     torch.cuda.synchronize()
     ok = all(pattern_ok(y, world, base=j << 24) for j, y in enumerate(ys))
     return _all_ok(dist, ok and comm.async_error() == 0)
@@ -1023,7 +1067,7 @@ def check_zero_group(dist, comm, rank, world, nbytes, k, dtype="bf16"):
     nccl.group_start()
     for x, y in zip(xs, ys):
         comm.reduce_scatter(x.data_ptr(), y.data_ptr(), rc, _CODE[dtype], nccl.ncclSum, sp)
-    nccl.group_end()
+    _group_end()
     torch.cuda.synchronize()
     ok = all(pattern_ok(y, world, base=(j << 26) + rank * rc) for j, y in enumerate(ys))
     del xs, ys
@@ -1166,7 +1210,8 @@ def bench_allreduce(args):
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
     head_err = int(e.item())
     full = not args.sweep and not args.no_extras and head_err == 0
-    extras = bench_extras(dist, comm, rank, world, args) if full else None
+    tcomm = _Tolerant(comm)
+    extras = bench_extras(dist, tcomm, rank, world, args) if full else None
     # Correctness of everything timed above, on this topology (fences off and on).
     t_chk = time.perf_counter()
     head = rows[-1]["bytes"]
@@ -1200,7 +1245,7 @@ def bench_allreduce(args):
     # after a headline error (the same verdict on every rank) nothing more is
     # run on the comm: its calls are refused, and a rank that raised would
     # skip the gloo collectives of a check that its peers still enter
-    checks = (run_checks(dist, comm, rank, world, plan) if head_err == 0
+    checks = (run_checks(dist, tcomm, rank, world, plan) if head_err == 0
               else {"check_ms": {}, "fences_off": {}, "fences_on": {}})
     err = comm.async_error()
     n_channels, ring_orders = comm.n_channels(), nccl.ring_orders(world)
@@ -1334,7 +1379,7 @@ def _group_row(dist, comm, rank, world, S, k, steps=20, warmup=3):
     def grouped():
         nccl.group_start()
         calls()
-        nccl.group_end()
+        _group_end()
     t_sep = _time_coll(dist, calls, steps, warmup)
     f0 = comm.launch_stats()[1]
     t_grp = _time_coll(dist, grouped, steps, warmup)
@@ -1367,7 +1412,7 @@ def _zero_group_row(dist, comm, rank, world, S=ZERO_BUCKET, k=16, steps=10, warm
     def grouped():
         nccl.group_start()
         calls()
-        nccl.group_end()
+        _group_end()
     t_sep = _time_coll(dist, calls, steps, warmup)
     f0 = comm.launch_stats()[1]
     t_grp = _time_coll(dist, grouped, steps, warmup)
@@ -1389,6 +1434,12 @@ def bench_extras(dist, comm, rank, world, args):
     group aggregation, and config 4 (RS + AG bf16, 4 GiB bucket).  Each part
     records its own error instead of aborting; run_checks verifies each."""
     ex = {}
+
+    def go():  # the same verdict on every rank: stop at the first async error
+        err = _any_error(dist, comm)
+        if err:
+            ex["stopped"] = f"async error {err}: the remaining rows were skipped"
+        return err == 0
     try:
         ex["allreduce_f32_sizes"] = [_ar_size_row(dist, comm, rank, world, S, "f32", 20, 5)
                                      for S in EXTRA_F32_SIZES]
@@ -1401,11 +1452,15 @@ def bench_extras(dist, comm, rank, world, args):
         ex["allreduce_error"] = repr(e)
     finally:
         comm.set_algo(None)
+    if not go():
+        return ex
     try:
         ex["group_fusion_f32"] = [_group_row(dist, comm, rank, world, S, 16) for S in EXTRA_GROUP_SIZES]
         ex["zero_group_rs_bf16"] = _zero_group_row(dist, comm, rank, world)
     except Exception as e:  # noqa: BLE001
         ex["group_error"] = repr(e)
+    if not go():
+        return ex
     try:  # each algorithm forced at two bucket sizes (vcclCommSetAlgo): the SIMPLE
         # ring of the north-star target beside the automatic choice
         ex["allreduce_f32_by_algo"] = {}
@@ -1418,6 +1473,8 @@ def bench_extras(dist, comm, rank, world, args):
         ex["by_algo_error"] = repr(e)
     finally:
         comm.set_algo(None)
+    if not go():
+        return ex
     try:  # the SIMPLE ring's slot hand-off: the workgroup one (default) vs per wave
         # (vcclCommSetRingWave / VCCL_RING_WAVE), config 3 and config 4 on the ring
         ex["ring_handoff"] = {}
@@ -1434,6 +1491,8 @@ def bench_extras(dist, comm, rank, world, args):
     finally:
         comm.set_ring_wave(False)
         comm.set_algo(None)
+    if not go():
+        return ex
     try:  # the mid range (64 KiB - 8 MiB: LL128's slot in VCCL's tuner), each path forced
         ex["allreduce_f32_mid_by_algo"] = {}
         for algo in MID_ALGOS:
@@ -1444,6 +1503,8 @@ def bench_extras(dist, comm, rank, world, args):
         ex["mid_by_algo_error"] = repr(e)
     finally:
         comm.set_algo(None)
+    if not go():
+        return ex
     try:
         ex["rs_ag_bf16"] = _rs_ag(dist, comm, rank, world, args.rs_ag_bytes, min(args.steps, 10), 2)
         comm.set_algo("direct")
@@ -1453,14 +1514,20 @@ def bench_extras(dist, comm, rank, world, args):
         ex["rs_ag_error"] = repr(e)
     finally:
         comm.set_algo(None)
+    if not go():
+        return ex
     try:  # the ring broadcast (DDP's construction-time state broadcast), root 0
         ex["broadcast_f32"] = [_bcast_row(dist, comm, rank, world, S) for S in BCAST_SIZES]
     except Exception as e:  # noqa: BLE001
         ex["broadcast_error"] = repr(e)
+    if not go():
+        return ex
     try:  # the ring reduce into the last rank
         ex["reduce_f32"] = [_reduce_row(dist, comm, rank, world, S) for S in BCAST_SIZES]
     except Exception as e:  # noqa: BLE001
         ex["reduce_error"] = repr(e)
+    if not go():
+        return ex
     try:  # small / mid buckets: the one-hop LL / direct RS + AG vs the ring
         ex["rs_ag_f32_sizes"] = []
         for S in EXTRA_RSAG_SIZES:
@@ -1471,11 +1538,15 @@ def bench_extras(dist, comm, rank, world, args):
         ex["rs_ag_sizes_error"] = repr(e)
     finally:
         comm.set_algo(None)
+    if not go():
+        return ex
     try:  # config 3 on communicators bounded to C ring channels: the link model's headroom
         ex["allreduce_f32_by_channels"] = _channel_rows(dist, rank, world, args.bytes or (1 << 30),
                                                         min(args.steps, 5))
     except Exception as e:  # noqa: BLE001
         ex["channels_error"] = repr(e)
+    if not go():
+        return ex
     try:  # the ring's slot timeline on the headline bucket, both hand-offs
         ex["ring_trace"] = _ring_trace_row(dist, rank, world, args.bytes or (1 << 30))
     except Exception as e:  # noqa: BLE001
@@ -1484,6 +1555,8 @@ def bench_extras(dist, comm, rank, world, args):
     # replay).  Its capture stream is one more hardware queue per process;
     # with 8 ranks sharing one GPU (rehearsal) that oversubscribes the
     # scheduler's queues and every later row would run time-sliced.
+    if not go():
+        return ex
     try:
         # one capture stream for every row: with ranks sharing one GPU, the
         # second stream a process creates served ~28 us per replayed call
@@ -1549,7 +1622,7 @@ def _ring_trace_row(dist, rank, world, S, cap=1024):
     try:
         obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        c = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank)
+        c = _Tolerant(nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank))
     finally:
         if old is None:
             os.environ.pop("VCCL_RING_TRACE", None)
@@ -1609,7 +1682,7 @@ def _channel_rows(dist, rank, world, S, steps, warmup=2):
         obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         cfg = nccl.ncclConfig_t.initializer(minCTAs=C, maxCTAs=C)
-        c = nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank, config=cfg)
+        c = _Tolerant(nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank, config=cfg))
         try:
             c.set_algo("ring")
             dt = _time_coll(dist, lambda: c.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32,
@@ -1620,8 +1693,13 @@ def _channel_rows(dist, rank, world, S, steps, warmup=2):
             rows.append({"channels_asked": C, "n_channels": c.n_channels(), "bytes": n * 4,
                          "us": round(dt / steps * 1e6, 1),
                          "busbw": round(algbw * 2 * (world - 1) / world, 2), "correct": ok})
+            # `ok` is already every rank's verdict; the error gate is a collective
+            stop = ok is not True or _any_error(dist, c) != 0
         finally:
             c.destroy()
+        if stop:
+            rows[-1]["stopped"] = "error on this comm: the larger counts were skipped"
+            break
     del x, y
     return rows
 

@@ -66,6 +66,29 @@ def test_broken_path_line_fails_fast():
     assert line["config"]["async_error"] != 0
 
 
+def test_error_mid_extras_still_prints_line():
+    """The headline passes, then a later row breaks the comm (a 64 KiB
+    headline on the forced net path moves no slot of 512 KiB; the first extras
+    row that does lands short): the ranks see the error at different calls,
+    yet the line prints — the refused calls are recorded (bench._Tolerant),
+    the remaining extras rows are skipped at the next error gate, and every
+    check reports false instead of raising."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update({"VCCL_NET_FORCE": "1", "VCCL_DEBUG_NET_SHORT_SLOT": str(512 << 10),
+                "VCCL_SPIN_TIMEOUT_S": "10"})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--bytes", str(64 << 10), "--no-initall",
+                        "--rs-ag-bytes", str(8 << 20)],
+                       env=env, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    c = line["correct"]
+    assert c["headline_async_error"] == 0 and c["all"] is False, c
+    assert "stopped" in line["extras"], sorted(line["extras"])
+    assert line["config"]["async_error"] != 0
+
+
 def test_staging_row_checked():
     """SURVEY §8(d)'s staging row (D2H, H2D, D2H -> host sum -> H2D) as the
     N = 1 line's cpu_baseline carries it, on a 16 MiB bucket: rates positive
