@@ -1307,6 +1307,20 @@ MID_SIZES = (256 << 10, 1 << 20, 8 << 20)
 MID_ALGOS = ("ring", "direct", "ll128")
 
 
+def handoff_exit_rule(wg, pw, world, ranks_per_device, threshold=0.03):
+    """DESIGN.md §9's exit rule for the per-wave ring hand-off, evaluated on
+    the line's own `ring_handoff` rows (the 1 GiB all-reduce under each
+    hand-off): it decides only on 8 ranks with one GPU each at 1 GiB; the
+    line's `correct` must be green as well."""
+    gain = wg["us"] / pw["us"] - 1 if pw["us"] > 0 else float("nan")
+    applies = world == 8 and ranks_per_device == 1 and wg["bytes"] == 1 << 30
+    verdict = (None if not applies else
+               "per-wave becomes the bandwidth-regime default" if gain >= threshold else
+               "per-wave kernels are deleted (ring_kernels.hip PART 4, prim_ws, WaveSync)")
+    return {"rule": f"per-wave >= {threshold:.0%} faster at 1 GiB, 8 ranks, one per GPU, checks green",
+            "per_wave_gain": round(gain, 4), "applies": applies, "verdict_if_checks_green": verdict}
+
+
 def _ar_size_row(dist, comm, rank, world, S, dtype, steps, warmup):
     sp = torch.cuda.current_stream().cuda_stream
     tdt, code = {"f32": (torch.float32, nccl.ncclFloat32), "f16": (torch.float16, nccl.ncclFloat16)}[dtype]
@@ -1486,6 +1500,10 @@ def bench_extras(dist, comm, rank, world, args):
                                   for S, st in ((64 << 20, 10), (args.bytes or (1 << 30), 5))],
                 "rs_ag_bf16": _rs_ag(dist, comm, rank, world, args.rs_ag_bytes, min(args.steps, 10), 2)}
         ex["ring_handoff"]["per_wave_launches"] = comm.set_ring_wave(False)
+        ex["ring_handoff"]["exit_rule"] = handoff_exit_rule(
+            ex["ring_handoff"]["workgroup"]["allreduce_f32"][-1],
+            ex["ring_handoff"]["per_wave"]["allreduce_f32"][-1], world,
+            -(-world // torch.cuda.device_count()))
     except Exception as e:  # noqa: BLE001
         ex["ring_handoff_error"] = repr(e)
     finally:

@@ -170,3 +170,16 @@ def test_cpu_baseline_leaves_the_caller_unpinned():
     before = os.sched_getaffinity(0)
     bench.cpu_baseline_allreduce(1 << 20, 2, 0.1)
     assert os.sched_getaffinity(0) == before
+
+
+def test_handoff_exit_rule():
+    """DESIGN §9's exit rule on the line's ring_handoff rows: it decides only
+    at 8 ranks, one per GPU, 1 GiB; >= 3 % keeps the per-wave hand-off."""
+    wg = {"bytes": 1 << 30, "us": 1030.0}
+    r = bench.handoff_exit_rule(wg, {"bytes": 1 << 30, "us": 1000.0}, 8, 1)
+    assert r["applies"] and r["per_wave_gain"] == 0.03 and "default" in r["verdict_if_checks_green"]
+    r = bench.handoff_exit_rule(wg, {"bytes": 1 << 30, "us": 1010.0}, 8, 1)
+    assert r["applies"] and "deleted" in r["verdict_if_checks_green"]
+    for world, rpd, S in ((8, 8, 1 << 30), (4, 1, 1 << 30), (8, 1, 64 << 20)):
+        r = bench.handoff_exit_rule({"bytes": S, "us": 2.0}, {"bytes": S, "us": 1.0}, world, rpd)
+        assert not r["applies"] and r["verdict_if_checks_green"] is None
