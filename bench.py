@@ -1307,6 +1307,26 @@ MID_SIZES = (256 << 10, 1 << 20, 8 << 20)
 MID_ALGOS = ("ring", "direct", "ll128")
 
 
+def channel_knee(rows, default_channels, ranks_per_device, within=0.95):
+    """What the `allreduce_f32_by_channels` rows say about the link-bound
+    channel model (DESIGN.md §4.2, H = 8): the fewest channels reaching
+    `within` of the best checked busbw (the knee), and where the default
+    count stands against the best.  Meaningful on one rank per GPU only (a
+    shared device is CU-bound, and says so)."""
+    ok = [r for r in rows if r.get("correct") is True]
+    if not ok:
+        return {"knee_channels": None, "note": "no checked row"}
+    best = max(ok, key=lambda r: r["busbw"])
+    knee = min((r for r in ok if r["busbw"] >= within * best["busbw"]), key=lambda r: r["n_channels"])
+    at_default = [r for r in ok if r["n_channels"] == default_channels]
+    return {"default_channels": default_channels, "best_channels": best["n_channels"],
+            "best_busbw": best["busbw"], "knee_channels": knee["n_channels"], "knee_within": within,
+            "default_over_best": (round(at_default[0]["busbw"] / best["busbw"], 3) if at_default else None),
+            "one_rank_per_gpu": ranks_per_device == 1,
+            "reading": ("link-bound: H is right if the knee <= the default" if ranks_per_device == 1 else
+                        "ranks share a device: every channel is CU-bound, no statement on H")}
+
+
 def handoff_exit_rule(wg, pw, world, ranks_per_device, threshold=0.03):
     """DESIGN.md §9's exit rule for the per-wave ring hand-off, evaluated on
     the line's own `ring_handoff` rows (the 1 GiB all-reduce under each
@@ -1561,6 +1581,8 @@ def bench_extras(dist, comm, rank, world, args):
     try:  # config 3 on communicators bounded to C ring channels: the link model's headroom
         ex["allreduce_f32_by_channels"] = _channel_rows(dist, rank, world, args.bytes or (1 << 30),
                                                         min(args.steps, 5))
+        ex["channel_model"] = channel_knee(ex["allreduce_f32_by_channels"], comm.n_channels(),
+                                           -(-world // torch.cuda.device_count()))
     except Exception as e:  # noqa: BLE001
         ex["channels_error"] = repr(e)
     if not go():

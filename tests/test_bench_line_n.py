@@ -183,3 +183,14 @@ def test_handoff_exit_rule():
     for world, rpd, S in ((8, 8, 1 << 30), (4, 1, 1 << 30), (8, 1, 64 << 20)):
         r = bench.handoff_exit_rule({"bytes": S, "us": 2.0}, {"bytes": S, "us": 1.0}, world, rpd)
         assert not r["applies"] and r["verdict_if_checks_green"] is None
+
+
+def test_channel_knee():
+    rows = [{"n_channels": c, "busbw": b, "correct": True}
+            for c, b in ((14, 100.0), (28, 180.0), (63, 300.0), (126, 310.0))]
+    rows.append({"n_channels": 252, "busbw": 400.0, "correct": False})  # unchecked rows never count
+    k = bench.channel_knee(rows, 63, 1)
+    assert k["best_channels"] == 126 and k["knee_channels"] == 63 and k["default_over_best"] == 0.968
+    assert k["one_rank_per_gpu"]
+    assert bench.channel_knee([], 63, 1)["knee_channels"] is None
+    assert not bench.channel_knee(rows, 16, 8)["one_rank_per_gpu"]
