@@ -54,9 +54,9 @@ def test_broken_path_line_fails_fast():
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env.update({"VCCL_NET_FORCE": "1", "VCCL_DEBUG_NET_SHORT_SLOT": str(64 << 10),
-                "VCCL_SPIN_TIMEOUT_S": "10"})
+                "VCCL_SPIN_TIMEOUT_S": "6"})
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-                        "--warmup", "1", "--bytes", str(64 << 20), "--no-initall"],
+                        "--warmup", "1", "--bytes", str(64 << 20), "--no-initall", "--no-cpu"],
                        env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
@@ -76,9 +76,9 @@ def test_error_mid_extras_still_prints_line():
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env.update({"VCCL_NET_FORCE": "1", "VCCL_DEBUG_NET_SHORT_SLOT": str(512 << 10),
-                "VCCL_SPIN_TIMEOUT_S": "10"})
+                "VCCL_SPIN_TIMEOUT_S": "6"})
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-                        "--warmup", "1", "--bytes", str(64 << 10), "--no-initall",
+                        "--warmup", "1", "--bytes", str(64 << 10), "--no-initall", "--no-cpu",
                         "--rs-ag-bytes", str(8 << 20)],
                        env=env, capture_output=True, text=True, timeout=400, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
