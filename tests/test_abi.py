@@ -193,3 +193,41 @@ print(L.pncclGetLastError(ctypes.c_void_p(0x10)).decode())
     assert first == "ncclCommCount : comm argument is NULL", first
     assert "NULL" in second or "invalid" in second.lower(), second
     assert "WARN" not in r.stderr  # NCCL_DEBUG=NONE: nothing printed, the text still kept
+
+
+def test_debug_file(tmp_path):
+    """NCCL_DEBUG_FILE (debug.cc:209-255): with an explicit level above
+    VERSION the log goes to the named file — %h the host name (up to its
+    first '.'), %p the pid, %% a '%', other %-sequences kept — and not to
+    stderr; ncclResetDebugInit closes it and a later NCCL_DEBUG_FILE opens
+    the next one."""
+    code = r"""
+import ctypes, os, socket, sys
+sys.path.insert(0, sys.argv[1])
+from vccl_amd import nccl
+L = nccl.lib()
+d = sys.argv[2]
+def warn():  # a NULL-comm call: WARN + invalid argument, no GPU needed
+    v = ctypes.c_int()
+    L.ncclCommCount(None, ctypes.byref(v))
+os.environ["NCCL_DEBUG"] = "WARN"
+os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "a.%h.%p.%%.%q.log")
+L.ncclResetDebugInit(); warn()
+os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "b.%p.log")
+L.ncclResetDebugInit(); warn(); warn()
+print(os.getpid(), socket.gethostname().split(".")[0])
+"""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("NCCL_DEBUG", "VCCL_DEBUG", "NCCL_DEBUG_FILE",
+                                                            "VCCL_DEBUG_FILE")}
+    r = subprocess.run([sys.executable, "-c", code, ROOT, str(tmp_path)], capture_output=True, text=True,
+                       env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    pid, host = r.stdout.split()
+    a = tmp_path / f"a.{host}.{pid}.%.%q.log"
+    b = tmp_path / f"b.{pid}.log"
+    assert sorted(p.name for p in tmp_path.iterdir()) == sorted([a.name, b.name])
+    assert a.read_text().count("WARN") == 1 and b.read_text().count("WARN") == 2
+    assert "comm argument is NULL" in b.read_text()
+    assert "WARN" not in r.stderr, r.stderr

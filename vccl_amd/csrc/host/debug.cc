@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <unistd.h>
 
 #include "core.h"
@@ -23,24 +24,74 @@ static int parse_level(const char* s) {
 
 // -1: not read yet (first use, or after ncclResetDebugInit)
 static std::atomic<int> g_level{-1};
+// NCCL_DEBUG_FILE (debug.cc:209-255): the log's file, else stderr.  g_initMu
+// guards the first read of the environment; log_msg holds g_mu while it
+// writes and may then take g_initMu, so every path takes g_mu first.
+static std::mutex g_initMu;
+static std::mutex g_mu;
+static std::atomic<FILE*> g_file{nullptr};
+
+// The file name of NCCL_DEBUG_FILE: %h the host name, %p the pid, %% a
+// '%', any other %-sequence kept as written (debug.cc:215-247).
+std::string debug_file_name(const char* pattern, const char* host, int pid) {
+  std::string out;
+  for (const char* c = pattern; *c; c++) {
+    if (*c != '%') {
+      out += *c;
+      continue;
+    }
+    const char k = *++c;
+    if (k == '%') out += '%';
+    else if (k == 'h') out += host;
+    else if (k == 'p') out += std::to_string(pid);
+    else {
+      out += '%';
+      if (!k) break;
+      out += k;
+    }
+  }
+  return out;
+}
 
 int log_level() {
-  int level = g_level.load(std::memory_order_relaxed);
-  if (level < 0) {
-    const char* s = getenv("VCCL_DEBUG");
-    if (!s) s = getenv("NCCL_DEBUG");
-    level = parse_level(s);
-    g_level.store(level, std::memory_order_relaxed);
+  int level = g_level.load(std::memory_order_acquire);
+  if (level >= 0) return level;
+  std::lock_guard<std::mutex> lk(g_initMu);
+  level = g_level.load(std::memory_order_relaxed);
+  if (level >= 0) return level;
+  const char* s = getenv("VCCL_DEBUG");
+  if (!s) s = getenv("NCCL_DEBUG");
+  level = parse_level(s);
+  // as the reference: only for an explicit level above VERSION
+  const char* f = getenv("VCCL_DEBUG_FILE");
+  if (!f) f = getenv("NCCL_DEBUG_FILE");
+  if (f && s && level >= kLogWarn && strcasecmp(s, "VERSION") != 0 && !g_file.load()) {
+    char host[256] = "";
+    gethostname(host, sizeof(host) - 1);
+    if (char* dot = strchr(host, '.')) *dot = '\0';  // getHostName(..., '.')
+    const std::string name = debug_file_name(f, host, (int)getpid());
+    if (!name.empty()) {
+      if (FILE* fp = fopen(name.c_str(), "w")) {
+        setbuf(fp, nullptr);  // unbuffered, as the reference
+        g_file.store(fp);
+      }
+    }
   }
+  g_level.store(level, std::memory_order_release);
   return level;
 }
 
-// ncclResetDebugInit (debug.cc:367-378): the next log call re-reads the level
-void reset_log_level() { g_level.store(-1, std::memory_order_relaxed); }
+// ncclResetDebugInit (debug.cc:367-378): the next log call re-reads the
+// level, and the debug file is closed
+void reset_log_level() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> li(g_initMu);
+  if (FILE* fp = g_file.exchange(nullptr)) fclose(fp);
+  g_level.store(-1, std::memory_order_release);
+}
 
 // ncclLastError (debug.cc:29): the last WARN as human-readable text, saved
 // before the level filter (debug.cc:265-272), returned by ncclGetLastError.
-static std::mutex g_mu;
 static char g_lastError[1024] = "";
 const char* last_error() { return g_lastError; }
 
@@ -56,8 +107,9 @@ void log_msg(int level, const char* file, int line, const char* fmt, ...) {
   if (warn) memcpy(g_lastError, buf, sizeof(buf));
   if (log_level() < level) return;
   const char* base = strrchr(file, '/');
-  fprintf(stderr, "[vccl %d] %s %s:%d %s\n", (int)getpid(), level == kLogWarn ? "WARN" : "INFO",
-          base ? base + 1 : file, line, buf);
+  FILE* out = g_file.load();
+  fprintf(out ? out : stderr, "[vccl %d] %s %s:%d %s\n", (int)getpid(),
+          level == kLogWarn ? "WARN" : "INFO", base ? base + 1 : file, line, buf);
 }
 
 int64_t param_int(const char* name, int64_t deflt) {
