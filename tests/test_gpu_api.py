@@ -174,3 +174,36 @@ def test_oracle_allreduce_one_rank_semantics():
     # the oracle's API-level restatement agrees (world 1: copy / x*1)
     x = np.arange(10, dtype=np.float32)
     assert np.array_equal(O.allreduce(4, 7, [x]), x)
+
+
+def test_debug_subsys_filters_info_lines():
+    """NCCL_DEBUG_SUBSYS (debug.cc:30, 57-111): with NCCL_DEBUG=INFO the
+    default mask (INIT, BOOTSTRAP, ENV) prints the init lines but not the
+    per-call COLL trace; COLL alone prints only the trace; ^INIT prints every
+    subsystem but INIT."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from vccl_amd import nccl
+c = nccl.Comm.init_rank(1, nccl.get_unique_id(), 0)
+x = torch.ones(256, device="cuda"); y = torch.empty_like(x)
+c.all_reduce(x.data_ptr(), y.data_ptr(), 256, nccl.ncclFloat32, nccl.ncclSum,
+             torch.cuda.current_stream().cuda_stream)
+torch.cuda.synchronize(); c.destroy()
+"""
+    base = {k: v for k, v in os.environ.items()
+            if k not in ("NCCL_DEBUG", "VCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "VCCL_DEBUG_SUBSYS")}
+    seen = {}
+    for sub in (None, "COLL", "^INIT"):
+        env = dict(base, NCCL_DEBUG="INFO")
+        if sub:
+            env["NCCL_DEBUG_SUBSYS"] = sub
+        r = subprocess.run([sys.executable, "-c", code, root], capture_output=True, text=True, env=env,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        seen[sub] = ("dev 0: bootstrap" in r.stderr, "AllReduce: opCount" in r.stderr)
+    assert seen == {None: (True, False), "COLL": (False, True), "^INIT": (False, True)}, seen

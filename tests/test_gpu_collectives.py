@@ -651,7 +651,8 @@ def test_torch_process_group_dropin(init):
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=port, LD_PRELOAD=f"{tlib}:{vlib}", VCCL_ALLOW_SHARED_DEVICE="1",
-                   VCCL_SPIN_TIMEOUT_S="20", VCCL_DEBUG="INFO", TORCH_NCCL_ASYNC_ERROR_HANDLING="1",
+                   VCCL_SPIN_TIMEOUT_S="20", VCCL_DEBUG="INFO", VCCL_DEBUG_SUBSYS="INIT,COLL",
+                   TORCH_NCCL_ASYNC_ERROR_HANDLING="1",
                    VCCL_TEST_TORCH_INIT=init)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp_torch_pg_worker.py")],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))

@@ -3,6 +3,7 @@
 // and NCCL_PARAM (include/param.h:17-25, misc/param.cc:52-98).
 #include <atomic>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -24,6 +25,48 @@ static int parse_level(const char* s) {
 
 // -1: not read yet (first use, or after ncclResetDebugInit)
 static std::atomic<int> g_level{-1};
+
+// NCCL_DEBUG_SUBSYS (debug.cc:57-111): which subsystems' INFO lines print;
+// the reference's default is INIT, BOOTSTRAP and ENV (debug.cc:30), so the
+// per-call COLL trace needs NCCL_DEBUG_SUBSYS=COLL as with libnccl.  WARNs
+// always print.  A line's subsystem is its source file's.
+enum : uint64_t {
+  kSubInit = 1, kSubColl = 2, kSubP2P = 4, kSubShm = 8, kSubNet = 16, kSubGraph = 32,
+  kSubTuning = 64, kSubEnv = 128, kSubAlloc = 256, kSubCall = 512, kSubProxy = 1024,
+  kSubNvls = 2048, kSubBootstrap = 4096, kSubReg = 8192, kSubProfile = 16384, kSubRas = 32768,
+  kSubDefault = kSubInit | kSubBootstrap | kSubEnv
+};
+static std::atomic<uint64_t> g_mask{kSubDefault};
+
+uint64_t debug_subsys_mask(const char* spec) {
+  if (!spec) return kSubDefault;
+  static const struct { const char* name; uint64_t bit; } kNames[] = {
+      {"INIT", kSubInit}, {"COLL", kSubColl}, {"P2P", kSubP2P}, {"SHM", kSubShm}, {"NET", kSubNet},
+      {"GRAPH", kSubGraph}, {"TUNING", kSubTuning}, {"ENV", kSubEnv}, {"ALLOC", kSubAlloc},
+      {"CALL", kSubCall}, {"PROXY", kSubProxy}, {"NVLS", kSubNvls}, {"BOOTSTRAP", kSubBootstrap},
+      {"REG", kSubReg}, {"PROFILE", kSubProfile}, {"RAS", kSubRas}, {"ALL", ~0ull}};
+  const bool invert = spec[0] == '^';
+  uint64_t mask = invert ? ~0ull : 0;
+  std::string list(spec + (invert ? 1 : 0));
+  size_t at = 0;
+  while (at <= list.size()) {
+    size_t end = list.find(',', at);
+    if (end == std::string::npos) end = list.size();
+    const std::string item = list.substr(at, end - at);
+    for (const auto& n : kNames)
+      if (!strcasecmp(item.c_str(), n.name)) mask = invert ? mask & ~n.bit : mask | n.bit;
+    at = end + 1;
+  }
+  return mask;
+}
+
+static uint64_t subsys_of(const char* base) {
+  if (!strncmp(base, "enqueue", 7)) return kSubColl;
+  if (!strncmp(base, "proxy", 5)) return kSubNet | kSubProxy;
+  if (!strncmp(base, "bootstrap", 9)) return kSubBootstrap;
+  if (!strncmp(base, "debug", 5)) return kSubEnv;
+  return kSubInit;
+}
 // NCCL_DEBUG_FILE (debug.cc:209-255): the log's file, else stderr.  g_initMu
 // guards the first read of the environment; log_msg holds g_mu while it
 // writes and may then take g_initMu, so every path takes g_mu first.
@@ -62,6 +105,9 @@ int log_level() {
   const char* s = getenv("VCCL_DEBUG");
   if (!s) s = getenv("NCCL_DEBUG");
   level = parse_level(s);
+  const char* sub = getenv("VCCL_DEBUG_SUBSYS");
+  if (!sub) sub = getenv("NCCL_DEBUG_SUBSYS");
+  g_mask.store(debug_subsys_mask(sub), std::memory_order_relaxed);
   // as the reference: only for an explicit level above VERSION
   const char* f = getenv("VCCL_DEBUG_FILE");
   if (!f) f = getenv("NCCL_DEBUG_FILE");
@@ -107,9 +153,11 @@ void log_msg(int level, const char* file, int line, const char* fmt, ...) {
   if (warn) memcpy(g_lastError, buf, sizeof(buf));
   if (log_level() < level) return;
   const char* base = strrchr(file, '/');
+  base = base ? base + 1 : file;
+  if (!warn && !(subsys_of(base) & g_mask.load(std::memory_order_relaxed))) return;
   FILE* out = g_file.load();
   fprintf(out ? out : stderr, "[vccl %d] %s %s:%d %s\n", (int)getpid(),
-          level == kLogWarn ? "WARN" : "INFO", base ? base + 1 : file, line, buf);
+          level == kLogWarn ? "WARN" : "INFO", base, line, buf);
 }
 
 int64_t param_int(const char* name, int64_t deflt) {
