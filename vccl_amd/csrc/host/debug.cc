@@ -38,7 +38,7 @@ enum : uint64_t {
 };
 static std::atomic<uint64_t> g_mask{kSubDefault};
 
-uint64_t debug_subsys_mask(const char* spec) {
+static uint64_t debug_subsys_mask(const char* spec) {
   if (!spec) return kSubDefault;
   static const struct { const char* name; uint64_t bit; } kNames[] = {
       {"INIT", kSubInit}, {"COLL", kSubColl}, {"P2P", kSubP2P}, {"SHM", kSubShm}, {"NET", kSubNet},
@@ -67,6 +67,7 @@ static uint64_t subsys_of(const char* base) {
   if (!strncmp(base, "debug", 5)) return kSubEnv;
   return kSubInit;
 }
+
 // NCCL_DEBUG_FILE (debug.cc:209-255): the log's file, else stderr.  g_initMu
 // guards the first read of the environment; log_msg holds g_mu while it
 // writes and may then take g_initMu, so every path takes g_mu first.
@@ -76,7 +77,7 @@ static std::atomic<FILE*> g_file{nullptr};
 
 // The file name of NCCL_DEBUG_FILE: %h the host name, %p the pid, %% a
 // '%', any other %-sequence kept as written (debug.cc:215-247).
-std::string debug_file_name(const char* pattern, const char* host, int pid) {
+static std::string debug_file_name(const char* pattern, const char* host, int pid) {
   std::string out;
   for (const char* c = pattern; *c; c++) {
     if (*c != '%') {
