@@ -1591,6 +1591,12 @@ def bench_extras(dist, comm, rank, world, args):
         ex["ring_trace"] = _ring_trace_row(dist, rank, world, args.bytes or (1 << 30))
     except Exception as e:  # noqa: BLE001
         ex["ring_trace_error"] = repr(e)
+    if not go():
+        return ex
+    try:  # the inter-node path with its staging copies, on the ranks of this run
+        ex["allreduce_f32_net"] = _net_row(dist, rank, world)
+    except Exception as e:  # noqa: BLE001
+        ex["net_error"] = repr(e)
     # Last: config 5 without per-call launch cost (nccl-tests -G: HIP graph
     # replay).  Its capture stream is one more hardware queue per process;
     # with 8 ranks sharing one GPU (rehearsal) that oversubscribes the
@@ -1647,6 +1653,42 @@ def ring_trace_summary(tr):
                                                               "gap")},
                   "payload_GBs_in_copy": round(d["bytes"] / (d["copy"] * 1e3), 1) if d["copy"] else None}
     return out
+
+
+def _net_row(dist, rank, world, S=256 << 20, steps=3, warmup=1):
+    """North_star's staged rate, "including the copies to and from the GPU":
+    config 3's fp32 all-reduce of an S-byte bucket on a fresh comm created
+    with VCCL_NET_FORCE=1, so every ring connection moves through host-pinned
+    staging slots and the TCP proxy pair (host/proxy.cc; the reference's net
+    transport without GPUDirect, src/transport/net.cc:1293-1482) — on one rank
+    per GPU each rank stages over its own host link.  busbw per rank, checked
+    (DESIGN.md §4.6)."""
+    old = os.environ.get("VCCL_NET_FORCE")
+    os.environ["VCCL_NET_FORCE"] = "1"
+    try:
+        obj = [nccl.unique_id_to_bytes(nccl.get_unique_id()) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        c = _Tolerant(nccl.Comm.init_rank(world, nccl.unique_id_from_bytes(obj[0]), rank))
+    finally:
+        if old is None:
+            os.environ.pop("VCCL_NET_FORCE", None)
+        else:
+            os.environ["VCCL_NET_FORCE"] = old
+    sp = torch.cuda.current_stream().cuda_stream
+    n = S // 4
+    x = torch.rand(n, device="cuda")
+    y = torch.empty_like(x)
+    try:
+        dt = _time_coll(dist, lambda: c.all_reduce(x.data_ptr(), y.data_ptr(), n, nccl.ncclFloat32,
+                                                   nccl.ncclSum, sp), steps, warmup)
+        ok = check_ar(dist, c, rank, world, S)
+        return {"bytes": n * 4, "channels": c.n_channels(), "us": round(dt / steps * 1e6, 1),
+                "busbw": round(n * 4 * steps / dt / 1e9 * 2 * (world - 1) / world, 3), "correct": ok,
+                "async_error": c.async_error(),
+                "path": "VCCL_NET_FORCE=1: device -> pinned host slot -> TCP proxy -> pinned host -> device"}
+    finally:
+        c.destroy()
+        del x, y
 
 
 def _ring_trace_row(dist, rank, world, S, cap=1024):
